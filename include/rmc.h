@@ -1,0 +1,170 @@
+/*
+ * rmc.h -- C-ABI of the MI355X-native Raft model checker (librmc.so).
+ *
+ * The reference (kikimo/tla-raft) has no library API: its only interface is the
+ * TLC command line in myrun.sh:3
+ *
+ *     java -Xms4g -Xmx12g -jar tla2tools.jar -deadlock -workers 4 -config Raft.cfg Raft.tla $@
+ *
+ * which reads Raft.tla + Raft.cfg, runs TLC's breadth-first model checker and
+ * prints TLC text.  Every entry point below replaces one piece of that run and
+ * cites what it replaces.  A TLC-compatible host driver (tla-raft_amd/launcher,
+ * or a Java FFM / Python ctypes binding -- INTEGRATION.md) sits on top.
+ *
+ * Conventions: plain C types only; every function returns RMC_OK (0) or a
+ * negative RMC_E_* code, with text from rmc_last_error().  A context is owned by
+ * one host thread.  All device memory is owned by the context.  The library
+ * never falls back to a CPU path: without a usable gfx950 device rmc_create
+ * fails with RMC_E_DEVICE.
+ */
+#ifndef RMC_H
+#define RMC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RMC_ABI_VERSION 1
+
+/* ---- return codes ---------------------------------------------------------- */
+#define RMC_OK 0
+#define RMC_DONE 1          /* rmc_step: the state space is exhausted */
+#define RMC_VIOLATION 2     /* an INVARIANT is FALSE in a new state (TLC exit 12) */
+#define RMC_ASSERT 3        /* Assert(role[s] # Leader, "split brain") failed, Raft.tla:185 */
+#define RMC_EVAL_ERROR 4    /* TLC evaluation error while checking an invariant (Raft.tla:499) */
+#define RMC_DEADLOCK 5      /* a state without successors while deadlock checking is on */
+#define RMC_E_ARG -1
+#define RMC_E_DEVICE -2
+#define RMC_E_MEMORY -3
+#define RMC_E_CAPACITY -4   /* a state exceeded the packed layout (|msgs| > msg_cap) */
+#define RMC_E_STATE -5      /* call out of sequence */
+#define RMC_E_PARSE -6      /* cfg / spec validation failed */
+#define RMC_E_COMM -7       /* multi-GPU communicator failure */
+
+/* ---- invariants (Raft.cfg:33-34 selects Inv) --------------------------------- */
+#define RMC_INV_LEADER_HAS_ALL_COMMITTED (1u << 0) /* Inv == LeaderHasAllCommittedEntries, Raft.tla:491-503 */
+#define RMC_INV_NO_SPLIT_VOTE (1u << 1)            /* Raft.tla:444-448 */
+#define RMC_INV_RAFT_CAN_COMMIT (1u << 2)          /* RaftCanCommt, Raft.tla:434 */
+#define RMC_INV_FOLLOWER_CAN_COMMIT (1u << 3)      /* Raft.tla:436-439 */
+#define RMC_INV_COMMIT_ALL (1u << 4)               /* Raft.tla:442 */
+#define RMC_INV_NO_ALL_COMMIT (1u << 5)            /* Raft.tla:451-481 (not yet compiled: rejected) */
+#define RMC_INV_EXIST_LEADER_AND_CANDIDATE (1u << 6) /* Raft.tla:483-487 */
+
+/* ---- spec variants ------------------------------------------------------------ */
+#define RMC_SPEC_RAFT 0    /* Raft.tla as shipped */
+#define RMC_SPEC_SEEDED 1  /* RaftSeeded: Median's threshold (Raft.tla:72) is Cardinality(Servers) */
+
+/* Model configuration: what Raft.cfg's CONSTANTS (Raft.cfg:1-21), INVARIANT
+ * (Raft.cfg:33-34) and TLC's -deadlock flag (myrun.sh:3) bind.  VIEW view
+ * (Raft.cfg:26) is always on; SYMMETRY symmServers (Raft.cfg:24) unless
+ * no_symmetry.  A zero-initialised struct plus the four constants and
+ * invariants = RMC_INV_LEADER_HAS_ALL_COMMITTED is Raft.cfg under myrun.sh. */
+typedef struct rmc_config {
+    int32_t n_servers;      /* |Servers|   Raft.cfg:18, 1..5 */
+    int32_t n_vals;         /* |Vals|      Raft.cfg:21, 0..3 */
+    int32_t max_election;   /* MaxElection Raft.cfg:4,  0..7 */
+    int32_t max_restart;    /* MaxRestart  Raft.cfg:3,  0..15 */
+    uint32_t invariants;    /* RMC_INV_* bits, checked in bit order */
+    int32_t check_deadlock; /* 0 = TLC -deadlock (myrun.sh:3) */
+    int32_t spec_variant;   /* RMC_SPEC_* */
+    int32_t device;         /* HIP device ordinal (-1 = current) */
+    int32_t msg_cap;        /* max |msgs| per state: 0 = auto (64 for n<=3, 128 otherwise) */
+    int32_t seen_log2;      /* initial seen-set slots = 2^seen_log2 (0 = auto); grows on demand */
+    int32_t no_symmetry;    /* 0 = SYMMETRY symmServers (Raft.cfg:24); 1 = cfg without SYMMETRY */
+    uint64_t chunk_successors; /* successors per device chunk (0 = auto) */
+    /* multi-GPU (one process per GPU): world_size 1 = single GPU */
+    int32_t rank, world_size;  /* world_size 0 or 1 = single GPU */
+    const void *comm_unique_id; /* 128-byte RCCL unique id, identical on every rank */
+} rmc_config;
+
+/* Statistics of one BFS level (what TLC's progress line reports). */
+typedef struct rmc_level_stats {
+    int32_t level;            /* BFS level whose states were just expanded (1 = Init's level) */
+    int32_t status;           /* RMC_OK / RMC_DONE / RMC_VIOLATION / ... */
+    uint64_t expanded;        /* states of that level expanded (this rank) */
+    uint64_t generated;       /* successors generated while expanding it (all ranks) */
+    uint64_t new_states;      /* distinct states first found (all ranks) */
+    uint64_t total_generated; /* TLC "states generated", Init included */
+    uint64_t total_distinct;  /* TLC "distinct states found" */
+    uint64_t queue;           /* TLC "states left on queue" */
+    double seconds;           /* wall time of this level */
+    double kernel_ms[6];      /* expand-count, expand-hash, dedup, materialize, exchange, other */
+    uint64_t kernel_launches[6];
+} rmc_level_stats;
+
+/* Final result of a run: TLC's closing lines. */
+typedef struct rmc_result {
+    int32_t status;           /* RMC_DONE / RMC_VIOLATION / RMC_ASSERT / RMC_EVAL_ERROR / RMC_DEADLOCK */
+    int32_t depth;            /* "The depth of the complete state graph search is D" */
+    uint64_t generated, distinct, queue;
+    int32_t violated;         /* index (bit) of the violated invariant, -1 if none */
+    uint32_t trace_len;
+    double seconds;
+} rmc_result;
+
+int rmc_abi_version(void);
+
+/* Parse Raft.cfg text (replaces TLC's ModelConfig for the subset Raft.cfg uses,
+ * Raft.cfg:1-34) and validate Raft.tla text by content (replaces SANY; only
+ * Raft.tla and the documented RaftSeeded variant are compiled in).  tla_text
+ * may be NULL to skip the spec check (then spec_variant is left unchanged). */
+int rmc_parse_config(const char *cfg_text, const char *tla_text, rmc_config *out, char *err, size_t err_cap);
+
+/* Replaces TLC start-up (myrun.sh:3): allocates device state, builds the
+ * message universe and symmetry tables for the configuration. */
+int rmc_create(const rmc_config *cfg, void **ctx_out);
+
+/* Init (Raft.tla:93-105): level 1, invariant check on the initial state. */
+int rmc_init(void *ctx, rmc_level_stats *st);
+
+/* One BFS level of TLC's worker loop: successors of every state of the current
+ * level (Next, Raft.tla:416-430), SYMMETRY+VIEW fingerprint (Raft.tla:21,38),
+ * seen-set insertion with TLC -workers 1 first-discovery order, INVARIANT check
+ * on new states (Raft.cfg:33).  Returns RMC_OK, RMC_DONE or an error status. */
+int rmc_step(void *ctx, rmc_level_stats *st);
+
+/* Loop rmc_step until done or an error; fills the final result. */
+int rmc_run(void *ctx, rmc_result *res);
+int rmc_get_result(void *ctx, rmc_result *res);
+
+/* Counterexample (TLC's "The behavior up to this point is"): states 1..len from
+ * Init to the error state.  Unpacked layout below.  action/server/witness
+ * describe how state i was reached (action -1 for state 0 = Initial predicate). */
+int rmc_trace_len(void *ctx, uint32_t *len);
+int rmc_trace_state(void *ctx, uint32_t i, int32_t *unpacked, size_t cap_ints,
+                    int32_t *action, int32_t *server, int32_t *witness);
+
+const char *rmc_last_error(void *ctx);
+void rmc_destroy(void *ctx);
+
+/* ---- single-state hooks (parity tests; same kernels as rmc_step) -------------- */
+/* Successors of one state, in TLC enumeration order.  keys[i] = server<<24 |
+ * action<<16 | witness (witness: index into the sorted msgs for message actions,
+ * value for ClientReq, destination for LeaderAppendEntry, else 0).  fps gets the
+ * 128-bit symmetry+view fingerprint of each successor (2 words).  Returns the
+ * count, or RMC_ASSERT if UpdateTerm's Assert fails. */
+int rmc_successors(void *ctx, const int32_t *unpacked, int32_t *out, size_t stride_ints, uint32_t cap,
+                   uint32_t *keys, uint64_t *fps, uint32_t *count);
+int rmc_fingerprint(void *ctx, const int32_t *unpacked, uint64_t fp[2]);
+/* 1 = TRUE, 0 = FALSE, RMC_EVAL_ERROR; one invariant bit */
+int rmc_eval_invariant(void *ctx, const int32_t *unpacked, uint32_t invariant_bit, int32_t *value);
+
+/* Unpacked state (int32), the interchange format of every hook:
+ *   votedFor[n] (-1 = None)  currentTerm[n]  role[n] (0 F, 1 C, 2 L)  commitIndex[n]  logLen[n]
+ *   logs[n][V+1][2]          (term, val) per index 1..V+1; index 1 = (0,-1); unused = (0,0)
+ *   matchIndex[n][n]  nextIndex[n][n]  pendingResponse[n][n]
+ *   electionCount  restartCount  valSent[V] (-1 = None, 0 = FALSE)
+ *   nmsgs  msgs[nmsgs][8], sorted in TLC order:
+ *     type (0 VoteReq, 1 VoteResp, 2 AppendReq, 3 AppendResp) src dst term x1 x2 x3 x4
+ *     VoteReq x1 = lastLogIndex x2 = lastLogTerm; AppendResp x1 = prevLogIndex x2 = succ;
+ *     AppendReq x1 = prevLogIndex x2 = prevLogTerm x3 = leaderCommit x4 = entry (-1 none, else term*8+val)
+ */
+#define RMC_UNPACKED_INTS(n, V, nmsgs) (5 * (n) + (n) * ((V) + 1) * 2 + 3 * (n) * (n) + 3 + (V) + 8 * (nmsgs))
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RMC_H */

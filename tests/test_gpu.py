@@ -1,0 +1,148 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the oracle fixtures.
+
+Bit-exact bar: identical successor lists (TLC order, keys and concrete states), identical
+symmetry classes, identical invariant values, identical per-level distinct/generated
+counts, depth, verdict and counterexample traces (tests/golden/, from oracle/)."""
+import json
+import os
+
+import pytest
+
+import raft_ref as R
+import raftmc
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+LEVELS = load("levels.json")
+SAMPLES = load("successors.json")
+TRACES = load("traces.json")
+
+_cache = {}
+
+
+def checker(n, V, E, Rr, **kw):
+    key = (n, V, E, Rr, tuple(sorted(kw.items())))
+    if key not in _cache:
+        _cache[key] = raftmc.ModelChecker(raftmc.ModelConfig(n_servers=n, n_vals=V, max_election=E,
+                                                             max_restart=Rr, **kw))
+    return _cache[key]
+
+
+@pytest.mark.parametrize("name", sorted(SAMPLES))
+def test_successors_match_oracle(name):
+    g = SAMPLES[name]
+    mc = checker(g["n"], g["V"], g["E"], g["R"])
+    for it in g["items"]:
+        got = mc.successors(it["state"])
+        exp = it["successors"]
+        assert [list(k) for k, _, _ in got] == [e["key"] for e in exp]
+        for (k, st, _), e in zip(got, exp):
+            assert st == e["state"], (k, it["state"])
+
+
+@pytest.mark.parametrize("name", sorted(SAMPLES))
+def test_fingerprint_classes_match_oracle(name):
+    g = SAMPLES[name]
+    mc = checker(g["n"], g["V"], g["E"], g["R"])
+    fp_of_canon = {}
+    canon_of_fp = {}
+    for it in g["items"]:
+        assert mc.fingerprint(it["state"]) == mc.fingerprint(it["permuted"])
+        for (k, st, fp), e in zip(mc.successors(it["state"]), it["successors"]):
+            assert mc.fingerprint(st) == fp
+            c = e["canon"]
+            assert fp_of_canon.setdefault(c, fp) == fp
+            assert canon_of_fp.setdefault(fp, c) == c
+
+
+@pytest.mark.parametrize("name", sorted(SAMPLES))
+def test_invariants_match_oracle(name):
+    g = SAMPLES[name]
+    cfg = R.Config(n=g["n"], V=g["V"], max_election=g["E"], max_restart=g["R"])
+    mc = checker(g["n"], g["V"], g["E"], g["R"])
+    names = ["Inv", "NoSplitVote", "RaftCanCommt", "FollowerCanCommit", "CommitAll", "ExistLeaderAndCandidate"]
+    for it in g["items"]:
+        for sc in [it] + it["successors"][:4]:
+            st = R.state_from_json(sc["state"])
+            for nm in names:
+                try:
+                    exp = R.INV_FUNCS[nm](cfg, st)
+                except R.EvalError:
+                    exp = None
+                assert mc.eval_invariant(sc["state"], nm) == exp, nm
+
+
+def test_eval_error_state():
+    mc = checker(3, 2, 3, 3)
+    s = R.state_to_json(R.State((-1, -1, -1), (1, 1, 1), (((0, -1), (1, 0), (1, 1)), ((0, -1), (1, 0)), ((0, -1),)),
+                                ((1, 1, 1),) * 3, ((2, 2, 2),) * 3, (1, 3, 1), frozenset(), (2, 0, 0), 0, 0,
+                                ((False,) * 3,) * 3, (0, 0)))
+    assert mc.eval_invariant(s, "Inv") is None
+
+
+def run_cfg(g, **kw):
+    mc = raftmc.ModelChecker(raftmc.ModelConfig(
+        n_servers=g["n"], n_vals=g["V"], max_election=g["E"], max_restart=g["R"],
+        invariants=tuple(g["invariants"]), check_deadlock=g["check_deadlock"],
+        spec_variant=raftmc.SPEC_SEEDED if g["seeded"] else raftmc.SPEC_RAFT, **kw))
+    res = mc.run()
+    return mc, res
+
+
+def check_levels(g, res):
+    assert res.status == {"ok": "done"}.get(g["verdict"], g["verdict"])
+    assert res.generated == g["generated"] and res.distinct == g["distinct"]
+    if g["verdict"] == "ok":
+        assert res.depth == g["depth"]
+        assert [ls.new_states for ls in res.levels if ls.new_states] == g["levels"]
+        assert [ls.generated for ls in res.levels[1:]] == g["gen_per_level"]
+        assert res.queue == 0
+    else:
+        assert res.trace_len == g["trace_len"]
+        assert res.queue == g["queue_left"]
+        if g["verdict"] == "invariant":
+            assert res.violated == g["violated"]
+
+
+@pytest.mark.parametrize("name", sorted(LEVELS))
+def test_bfs_matches_golden_levels(name):
+    g = LEVELS[name]
+    mc, res = run_cfg(g)
+    check_levels(g, res)
+    mc.close()
+
+
+@pytest.mark.parametrize("name", sorted(TRACES))
+def test_counterexample_trace_matches_oracle(name):
+    g = LEVELS[name]
+    t = TRACES[name]
+    mc, res = run_cfg(g)
+    tr = mc.trace()
+    assert len(tr) == len(t["steps"])
+    for (key, st), e in zip(tr, t["steps"]):
+        assert (list(key) if key else None) == e["key"]
+        assert st == e["state"]
+    mc.close()
+
+
+def test_results_independent_of_chunking_and_seen_growth():
+    """Chunk boundaries and seen-set rehashing must not change TLC's discovery order."""
+    g = LEVELS["n3_v1_e2_r3"]
+    for kw in (dict(chunk_successors=6000, seen_log2=10), dict(chunk_successors=40000, seen_log2=12)):
+        mc, res = run_cfg(g, **kw)
+        check_levels(g, res)
+        mc.close()
+
+
+def test_seeded_trace_independent_of_chunking():
+    g = LEVELS["seeded_n3_v1_e2_r3"]
+    mc, res = run_cfg(g, chunk_successors=6000, seen_log2=10)
+    check_levels(g, res)
+    mc.close()

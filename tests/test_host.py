@@ -1,0 +1,128 @@
+"""CPU tests of the product's host side: C-ABI exports, cfg parsing, spec identification,
+launcher argument handling.  No compute call is made here (no GPU in this container)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import raftmc
+from conftest import ROOT, has_gpu
+
+HEADER = os.path.join(ROOT, "include", "rmc.h")
+LAUNCHER = os.path.join(ROOT, "tla-raft_amd", "build", "raftmc")
+REF_TLA = "/root/reference/Raft.tla"
+
+# A model config equivalent to the shipped Raft.cfg (Raft.cfg:1-34), written for these tests.
+CFG = """CONSTANTS
+    MaxTerm = 3
+    MaxRestart = {R}
+    MaxElection = {E}
+    Follower = Follower
+    Candidate = Candidate
+    Leader = Leader
+    None = None
+    VoteReq = VoteReq
+    VoteResp = VoteResp
+    AppendReq = AppendReq
+    AppendResp = AppendResp
+    s1 = s1
+    s2 = s2
+    s3 = s3
+    Servers = {{{servers}}}
+    v1 = v1
+    v2 = v2
+    Vals = {{{vals}}}
+\\* a comment
+SYMMETRY symmServers
+VIEW view
+INIT Init
+NEXT Next
+INVARIANT
+{inv}
+"""
+
+
+def cfg_text(E=3, R=3, servers="s1, s2, s3", vals="v1, v2", inv="Inv"):
+    return CFG.format(E=E, R=R, servers=servers, vals=vals, inv=inv)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = raftmc.load_library()
+    decl = re.findall(r"^\s*(?:int|void|const char \*)\s*\**\s*(rmc_\w+)\s*\(", open(HEADER).read(), re.M)
+    assert len(decl) >= 14
+    for name in decl:
+        assert hasattr(lib, name), name
+    assert lib.rmc_abi_version() == 1
+
+
+def test_parse_shipped_config_equivalent():
+    c = raftmc.parse_config(cfg_text())
+    assert (c.n_servers, c.n_vals, c.max_election, c.max_restart) == (3, 2, 3, 3)
+    assert c.invariants == ("Inv",) and c.symmetry
+
+
+def test_parse_variants():
+    c = raftmc.parse_config(cfg_text(E=2, servers="s1, s2, s3, s4, s5", vals="v1", inv="Inv\nNoSplitVote"))
+    assert (c.n_servers, c.n_vals, c.max_election) == (5, 1, 2)
+    assert set(c.invariants) == {"Inv", "NoSplitVote"}
+    c = raftmc.parse_config(cfg_text().replace("SYMMETRY symmServers", ""))
+    assert not c.symmetry
+
+
+@pytest.mark.parametrize("bad,msg", [
+    (cfg_text().replace("VIEW view", ""), "VIEW"),
+    (cfg_text().replace("MaxElection = 3", "MaxElection = 9"), "MaxElection"),
+    (cfg_text().replace("Leader = Leader", "Leader = 1"), "Leader"),
+    (cfg_text(inv="Bogus"), "Bogus"),
+    (cfg_text(servers=""), "Servers"),
+    (cfg_text() + "PROPERTY Liveness\n", "PROPERTY"),
+    (cfg_text().replace("INIT Init", "INIT Foo"), "INIT"),
+])
+def test_parse_errors_are_loud(bad, msg):
+    with pytest.raises(raftmc.RmcError, match=msg):
+        raftmc.parse_config(bad)
+
+
+def test_spec_identification():
+    if not os.path.exists(REF_TLA):
+        pytest.skip("reference Raft.tla not present on this machine")
+    tla = open(REF_TLA).read()
+    assert raftmc.parse_config(cfg_text(), tla).spec_variant == raftmc.SPEC_RAFT
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_seeded_spec
+    assert raftmc.parse_config(cfg_text(), make_seeded_spec.seeded(tla)).spec_variant == raftmc.SPEC_SEEDED
+    with pytest.raises(raftmc.RmcError, match="not kikimo"):
+        raftmc.parse_config(cfg_text(), tla.replace("MaxElection", "MaxElections"))
+
+
+def test_create_fails_loudly_without_gpu():
+    if has_gpu():
+        pytest.skip("GPU present")
+    with pytest.raises(raftmc.RmcError, match="RMC_E_DEVICE"):
+        raftmc.ModelChecker(raftmc.ModelConfig())
+
+
+def test_unpacked_roundtrip():
+    import raft_ref as R
+    cfg = R.Config(n=3, V=2)
+    st = R.init_state(cfg)
+    for _, t in R.successors(cfg, st):
+        for _, u in R.successors(cfg, t):
+            d = R.state_to_json(u)
+            assert raftmc.unpacked_to_state(raftmc.state_to_unpacked(d, 3, 2), 3, 2) == d
+
+
+def test_launcher_rejects_unknown_flags(tmp_path):
+    r = subprocess.run([LAUNCHER, "-bogus", "Raft.tla"], capture_output=True, text=True)
+    assert r.returncode == 150 and "unsupported option" in r.stderr
+
+
+def test_launcher_reports_cfg_errors(tmp_path):
+    (tmp_path / "Raft.cfg").write_text(cfg_text().replace("VIEW view", ""))
+    env = dict(os.environ, RMC_SKIP_SPEC_CHECK="1")
+    r = subprocess.run([LAUNCHER, "-deadlock", "-workers", "4", "-config", str(tmp_path / "Raft.cfg"),
+                        str(tmp_path / "Raft.tla")], capture_output=True, text=True, env=env)
+    assert r.returncode == 151 and "VIEW" in r.stdout

@@ -1,0 +1,142 @@
+"""CPU tests of the parity oracle itself (oracle/ is test infrastructure).
+
+Pins the restatement the only ways available: SURVEY.md Appendix C's hand-derived
+answers, agreement between the independent Python and C restatements, and the
+committed golden fixtures (tests/golden/make_golden.py)."""
+import ctypes
+import json
+import os
+import subprocess
+
+import pytest
+
+import raft_ref as R
+from conftest import GOLDEN, ROOT
+
+ORC_DIR = os.path.join(ROOT, "oracle")
+ORC_SO = os.path.join(ORC_DIR, "build", "libraft_oracle.so")
+
+
+@pytest.fixture(scope="module")
+def levels():
+    with open(os.path.join(GOLDEN, "levels.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def corc():
+    if not os.path.exists(ORC_SO):
+        subprocess.check_call(["make", "-s", "-C", ORC_DIR])
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("mg", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    return mg
+
+
+def test_appendix_c_known_answers():
+    # n=3, E>=3: levels 1,1,3,9 with 3,5,17 generated
+    cfg = R.Config(n=3, V=1, max_election=3, max_restart=3)
+    seen_levels, gen = _first_levels(cfg, 4)
+    assert seen_levels == [1, 1, 3, 9]
+    assert gen == [3, 5, 17]
+    cfg2 = R.Config(n=3, V=1, max_election=2, max_restart=3)
+    assert _first_levels(cfg2, 4) == ([1, 1, 3, 6], [3, 5, 11])
+    cfg5 = R.Config(n=5, V=1, max_election=2, max_restart=3)
+    assert _first_levels(cfg5, 3) == ([1, 1, 3], [5, 9])
+
+
+def _first_levels(cfg, L):
+    """BFS truncated after L levels (Python oracle)."""
+    s0 = R.init_state(cfg)
+    seen = {R.canonical(cfg, s0)}
+    frontier = [s0]
+    levels, gens = [1], []
+    for _ in range(L - 1):
+        nxt, g = [], 0
+        for st in frontier:
+            for _, t in R.successors(cfg, st):
+                g += 1
+                c = R.canonical(cfg, t)
+                if c not in seen:
+                    seen.add(c)
+                    nxt.append(t)
+        levels.append(len(nxt))
+        gens.append(g)
+        frontier = nxt
+    return levels, gens
+
+
+def test_init_state_matches_spec():
+    cfg = R.Config(n=3, V=2)
+    s = R.init_state(cfg)
+    assert s.votedFor == (R.NONE,) * 3 and s.currentTerm == (0, 0, 0)
+    assert s.logs[0] == ((0, R.NONE),) and s.matchIndex[1] == (1, 1, 1) and s.nextIndex[2] == (2, 2, 2)
+    assert s.msgs == frozenset() and s.valSent == (R.NONE, R.NONE)
+    assert R.inv_leader_has_all_committed(cfg, s)
+
+
+def test_message_order_is_tlc_record_order():
+    # 4-field VoteResp < 6-field records < 8-field AppendReq; VoteReq < AppendResp at equal dst
+    vp = R.vote_resp(2, 0, 3)
+    vq = R.vote_req(0, 1, 1, 1, 0)
+    ap = R.append_resp(0, 1, 1, 1, True)
+    aq = R.append_req(1, 0, 1, 1, 0, (), 1)
+    assert vp < vq < ap < aq
+    assert R.vote_req(2, 0, 1, 1, 0) < R.append_resp(2, 0, 1, 1, False)
+    assert R.append_req(0, 1, 1, 1, 0, (), 1) < R.append_req(0, 1, 1, 1, 0, ((1, 0),), 1)
+
+
+def test_median_is_kth_smallest():
+    cfg = R.Config(n=3)
+    assert R.median(cfg, (1, 3, 2)) == 2
+    assert R.median(cfg, (3, 3, 1)) == 3
+    cfg5 = R.Config(n=5)
+    assert R.median(cfg5, (1, 2, 3, 4, 5)) == 3
+    seeded = R.Config(n=3, seeded=True)
+    assert R.median(seeded, (1, 3, 2)) == 3  # threshold n: the maximum, i.e. the leader alone
+
+
+def test_inv_eval_error_is_detected():
+    cfg = R.Config(n=3, V=2)
+    s = R.init_state(cfg)
+    # leader s1 with a 3-entry log; s2 committed 3 but holds only 2 entries
+    logs = (((0, -1), (1, 0), (1, 1)), ((0, -1), (1, 0)), ((0, -1),))
+    s = R.State(s.votedFor, (1, 1, 1), logs, s.matchIndex, s.nextIndex, (1, 3, 1), s.msgs, (R.LEADER, 0, 0),
+                0, 0, s.pendingResponse, s.valSent)
+    with pytest.raises(R.EvalError):
+        R.inv_leader_has_all_committed(cfg, s)
+
+
+def test_python_and_c_oracles_agree_small(corc):
+    for (n, V, E, Rr) in [(3, 1, 1, 3), (2, 2, 2, 2)]:
+        c = corc.run_c(n, V, E, Rr)
+        _, p = corc.run_py(n, V, E, Rr)
+        assert (p.generated, p.distinct, p.depth, p.levels, p.generated_per_level) == (
+            c["generated"], c["distinct"], c["depth"], c["levels"], c["gen_per_level"])
+
+
+def test_c_oracle_reproduces_golden_levels(corc, levels):
+    for name, g in levels.items():
+        if g["distinct"] > 500_000:
+            continue
+        c = corc.run_c(g["n"], g["V"], g["E"], g["R"], g["seeded"], tuple(g["invariants"]), g["check_deadlock"])
+        for k in ("verdict", "generated", "distinct", "depth", "levels", "gen_per_level", "trace_len"):
+            assert c[k] == g[k], (name, k)
+
+
+def test_golden_levels_are_self_consistent(levels):
+    for name, g in levels.items():
+        if g["verdict"] == "ok":
+            assert sum(g["levels"]) == g["distinct"], name
+            assert 1 + sum(g["gen_per_level"]) == g["generated"], name
+            assert len(g["levels"]) == g["depth"], name
+            assert g["levels"][:2] == [1, 1], name
+
+
+def test_shuffled_order_gives_same_counts_small():
+    """SURVEY App. D.2 order-sensitivity probe: shuffled successor order, same partition sizes."""
+    cfg = R.Config(n=3, V=2, max_election=1, max_restart=3)
+    a = R.bfs(cfg)
+    b = R.bfs(cfg, order="shuffle", seed=7)
+    assert (a.distinct, a.levels) == (b.distinct, b.levels)

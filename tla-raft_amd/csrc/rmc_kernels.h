@@ -1,0 +1,76 @@
+// rmc_kernels.h -- host-side declarations of the device kernel set.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rmc_spec.h"
+
+namespace rmc {
+
+// Device-resident lookup tables built by the host (Universe) for one configuration.
+struct Tables {
+    const uint32_t *info;     // [U]        message info word by id (TLC order)
+    const uint16_t *nat2id;   // [nat_total] natural index -> id
+    const ulonglong2 *gmsg;   // [U]        per-message hash, families 0/1 (no src/dst)
+    const uint8_t *perms;     // [np][MAXN] server permutations (pi[i] = image of i)
+    const uint64_t *seeds;    // [2][MAXN + MAXN*MAXN] position seeds of the structured hash
+    int np;
+};
+
+enum ErrSlot { ERR_ASSERT = 0, ERR_DEADLOCK = 1, ERR_INV = 2, ERR_EVAL = 3, ERR_NSLOTS = 4 };
+
+// Kernel parameters (passed by value).
+struct KParams {
+    Dims d;
+    int E, R, seeded, check_deadlock;
+    uint32_t inv_mask;
+    Tables t;
+    // current level
+    const uint32_t *front;     // records, RECW words each
+    uint64_t p_begin, p_end;   // parents of this chunk (level-local indices)
+    // per parent (chunk-local: index p - p_begin)
+    uint32_t *cnt;             // successor counts
+    const uint32_t *off;       // exclusive scan of cnt (chunk-local successor index)
+    // per successor (chunk-local index j)
+    ulonglong2 *fp;
+    const uint32_t *wflag;     // 1 = winner (new, first in TLC order)
+    const uint32_t *wpos;      // exclusive scan of wflag
+    // seen set (open addressing, 16-B slots, lo word |= 1, 0 = empty)
+    ulonglong2 *T;
+    uint64_t Tmask;
+    // next level
+    uint32_t *next;            // records
+    uint64_t next_base;        // next-level index of this chunk's first winner
+    uint64_t *par;             // parent global id, indexed by global id
+    uint16_t *pslot;           // slot key, indexed by global id
+    uint64_t gid_next_base;    // global id of next-level index 0
+    uint64_t gid_parent_base;  // global id of level-local parent 0
+    // errors: atomicMin keys (p << 16 | slot), level-local p
+    unsigned long long *err;
+    uint32_t *flags;           // [0] msg-cap overflow, [1] violated invariant bit, [2] eval-error invariant bit
+    // single-state hook outputs
+    uint32_t *out_keys;
+    uint32_t *out_count;
+};
+
+struct KernelSet {
+    int N, V, MR, MCAP, CW, RECW, maxsucc;
+    void (*count)(const KParams &, hipStream_t);
+    void (*hash)(const KParams &, hipStream_t);
+    void (*materialize)(const KParams &, hipStream_t);
+    void (*single)(const KParams &, hipStream_t);           // all successors of front[0] -> next, fp, out_keys
+    void (*fp_states)(const KParams &, uint64_t n, hipStream_t);  // fp of front[0..n) -> fp
+    void (*inv_states)(const KParams &, uint64_t n, int32_t *out, hipStream_t); // per state: 1/0/-1 for inv_mask bits
+};
+
+// returns false if (N, V) has no compiled instantiation
+bool get_kernels(int N, int V, int msg_cap, KernelSet *ks);
+
+// generic (template-free) kernels
+void launch_dedup(const ulonglong2 *fp, uint64_t G, const ulonglong2 *T, uint64_t Tmask, uint32_t *L, uint64_t Lmask,
+                  uint32_t *lslot, hipStream_t s);
+void launch_winflag(const uint32_t *lslot, const uint32_t *L, uint64_t G, uint32_t *wflag, hipStream_t s);
+void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, ulonglong2 *Tnew, uint64_t new_mask, hipStream_t s);
+void launch_insert_fps(const ulonglong2 *fp, uint64_t n, ulonglong2 *T, uint64_t Tmask, hipStream_t s);
+
+}  // namespace rmc

@@ -1,0 +1,869 @@
+// rmc_kernels.hip -- CDNA4 (gfx950) kernels of the BFS hot path.
+//
+// One wavefront expands one frontier state ("parent").  Lane k of message round r
+// owns message r*64+k of the parent's msgs set and evaluates every message-witness
+// disjunct for it (UpdateTerm tla:175, ResponseVote tla:132, FollowerAcceptEntry
+// tla:275, FollowerRejectEntry tla:302, HandleAppendResp tla:374 -- for a given
+// message at most one is enabled, because they split on (role, type, term)).  The
+// last round's lanes own the non-message slots (BecomeCandidate tla:107,
+// BecomeLeader tla:157, ClientReq tla:233 per value, LeaderAppendEntry tla:242 per
+// destination, LeaderCanCommit tla:398, Restart tla:409).  Enabling conditions are
+// evaluated per lane; a ballot + in-wave rank by slot key puts the successors in
+// TLC's enumeration order (Next, tla:416-430) without any sort.
+//
+// Modes of the same expansion:
+//   COUNT        successors per parent (+ Assert tla:185 / deadlock detection)
+//   HASH         symmetry+view fingerprint of every successor -> fp[off[p] + rank]
+//   MATERIALIZE  winners (new states, first in TLC order) -> next frontier records,
+//                seen-set insert, parent pointers, INVARIANT check (Raft.cfg:33)
+//   SINGLE       every successor of one state -> records (parity-test hook)
+#include <hip/hip_runtime.h>
+
+#include "rmc_kernels.h"
+
+namespace rmc {
+
+enum Mode { M_COUNT = 0, M_HASH = 1, M_MAT = 2, M_SINGLE = 3 };
+
+template <int N>
+__device__ __forceinline__ uint32_t sel(const uint32_t *a, int i) {
+    uint32_t r = a[0];
+#pragma unroll
+    for (int k = 1; k < N; k++) r = (i == k) ? a[k] : r;
+    return r;
+}
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
+    uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+    uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int N, int V, int MR>
+struct Spec {
+    using L = Layout<N, V>;
+    static constexpr int NW = L::NW, CW = L::CW;
+    static constexpr int MCAP = 64 * MR;
+    static constexpr int RECW = CW + MCAP / 2;
+    static constexpr int NADD = (N > 1) ? N - 1 : 1;
+    static constexpr int SLOTS_PER_SERVER = 4 + V + (N - 1);  // BC BL CR*V LAE*(N-1) LCC RS
+    static_assert(N * SLOTS_PER_SERVER <= 64, "non-message slots must fit one wave");
+};
+
+// per-lane successor candidate
+template <int N, int V, int MR>
+struct Succ {
+    uint32_t c[Spec<N, V, MR>::NW];
+    uint32_t add[Spec<N, V, MR>::NADD];
+    uint32_t nadd;
+    uint32_t key;  // KEY_NONE = disabled
+    uint32_t s;    // acting server (row of the structured hash that changed)
+};
+
+// ---- log helpers (logs[i][x], tla:97, 1-based) ---------------------------------------
+template <int N, int V>
+__device__ __forceinline__ uint32_t log_word(const uint32_t *c, int i) {
+    return sel<N>(c + Layout<N, V>::W_LOG, i);
+}
+__device__ __forceinline__ uint32_t lw_term(uint32_t lw, uint32_t x) {  // x >= 1
+    return x <= 1 ? 0u : (lw >> (8 * (x - 2))) & 15u;
+}
+__device__ __forceinline__ uint32_t lw_byte(uint32_t lw, uint32_t x) {  // x >= 2: term | val<<4
+    return (lw >> (8 * (x - 2))) & 0xFFu;
+}
+
+// membership in the parent's sorted id list (LDS)
+__device__ __forceinline__ bool has_id(const uint16_t *ids, uint32_t nm, uint32_t id) {
+    uint32_t lo = 0, hi = nm;
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (ids[mid] < id) lo = mid + 1; else hi = mid;
+    }
+    return lo < nm && ids[lo] == id;
+}
+
+// Median(F) (tla:70-75): smallest F[s] with |{p : F[p] <= F[s]}| >= k.
+template <int N>
+__device__ __forceinline__ uint32_t median_row(uint32_t row, uint32_t k) {
+    uint32_t best = 15;
+#pragma unroll
+    for (int s = 0; s < N; s++) {
+        uint32_t fs = nib(row, s), cnt = 0;
+#pragma unroll
+        for (int p = 0; p < N; p++) cnt += nib(row, p) <= fs;
+        if (cnt >= k && fs < best) best = fs;
+    }
+    return best;
+}
+
+// ---- invariants (on a concrete state; TLC's left-to-right short-circuit) ---------------
+// returns 1 TRUE, 0 FALSE, -1 evaluation error
+template <int N, int V>
+__device__ __forceinline__ int inv_lhace(const uint32_t *c) {  // LeaderHasAllCommittedEntries tla:491-499
+    using Lo = Layout<N, V>;
+    bool any = false;
+#pragma unroll
+    for (int p = 0; p < N; p++) any |= nib(c[Lo::W_ROLE], p) == LEA;
+    if (!any) return 1;
+#pragma unroll
+    for (int l = 0; l < N; l++) {
+        if (nib(c[Lo::W_ROLE], l) != LEA) continue;
+        bool bad = false;
+        const uint32_t ll_l = nib(c[Lo::W_LL], l), lw_l = c[Lo::W_LOG + l], ct_l = nib(c[Lo::W_CT], l);
+#pragma unroll
+        for (int p = 0; p < N; p++) {
+            if (p == l || bad) continue;
+            if (!(nib(c[Lo::W_CT], p) <= ct_l)) continue;
+            const uint32_t ci_p = nib(c[Lo::W_CI], p);
+            if (ci_p > ll_l) { bad = true; continue; }
+            const uint32_t ll_p = nib(c[Lo::W_LL], p), lw_p = c[Lo::W_LOG + p];
+            for (uint32_t i = 2; i <= ci_p; i++) {  // index 1 is [0,None] on both sides
+                if (i > ll_p) return -1;                 // logs[p][index] out of domain (tla:499)
+                if (lw_byte(lw_p, i) != lw_byte(lw_l, i)) { bad = true; break; }
+            }
+        }
+        if (!bad) return 1;
+    }
+    return 0;
+}
+
+template <int N, int V>
+__device__ __forceinline__ int inv_eval(const uint32_t *c, int id) {
+    using Lo = Layout<N, V>;
+    switch (id) {
+    case 0: return inv_lhace<N, V>(c);
+    case 1: {  // NoSplitVote tla:444-448
+#pragma unroll
+        for (int a = 0; a < N; a++)
+#pragma unroll
+            for (int b = 0; b < N; b++)
+                if (a != b && nib(c[Lo::W_CT], a) == nib(c[Lo::W_CT], b) && nib(c[Lo::W_ROLE], a) == LEA &&
+                    nib(c[Lo::W_ROLE], b) == LEA)
+                    return 0;
+        return 1;
+    }
+    case 2: {  // RaftCanCommt tla:434
+#pragma unroll
+        for (int s = 0; s < N; s++) if (nib(c[Lo::W_CI], s) > 1) return 1;
+        return 0;
+    }
+    case 3: {  // FollowerCanCommit tla:436-439
+#pragma unroll
+        for (int s = 0; s < N; s++) if (nib(c[Lo::W_ROLE], s) == FOL && nib(c[Lo::W_CI], s) > 1) return 1;
+        return 0;
+    }
+    case 4: {  // CommitAll tla:442
+#pragma unroll
+        for (int s = 0; s < N; s++) if (nib(c[Lo::W_CI], s) != 3) return 0;
+        return 1;
+    }
+    case 6: {  // ExistLeaderAndCandidate tla:483-487
+#pragma unroll
+        for (int a = 0; a < N; a++)
+#pragma unroll
+            for (int b = 0; b < N; b++)
+                if (a != b && nib(c[Lo::W_ROLE], a) == LEA && nib(c[Lo::W_ROLE], b) == CAN) return 1;
+        return 0;
+    }
+    default: return 1;
+    }
+}
+
+// all selected invariants in bit order; returns 1 ok, 0 violated, -1 eval error; *which = bit
+template <int N, int V>
+__device__ __forceinline__ int check_invs(const uint32_t *c, uint32_t mask, int *which) {
+    for (int i = 0; i < 7; i++) {
+        if (!(mask & (1u << i))) continue;
+        int r = inv_eval<N, V>(c, i);
+        if (r != 1) { *which = i; return r; }
+    }
+    return 1;
+}
+
+// ---- structured symmetry fingerprint --------------------------------------------------
+// seeds layout: [f][0..MAXN) server position seeds, [f][MAXN + k*MAXN + l] pair seeds
+template <int N, int V>
+__device__ __forceinline__ ulonglong2 fingerprint(const uint32_t *c, int srow, const uint64_t *row0, const uint64_t *row1,
+                                  const uint64_t *M0, const uint64_t *M1, const Tables &t) {
+    using Lo = Layout<N, V>;
+    uint64_t U[N];
+    uint64_t X0[N * N], X1[N * N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint32_t vf = nib(c[Lo::W_VF], i);
+        const uint32_t vrel = vf == VF_NONE ? 0u : (vf == (uint32_t)i ? 1u : 2u);
+        const uint32_t own = vrel | (nib(c[Lo::W_CT], i) << 2) | (nib(c[Lo::W_ROLE], i) << 6) |
+                             (nib(c[Lo::W_CI], i) << 10) | (nib(c[Lo::W_LL], i) << 14) |
+                             (nib(c[Lo::W_MI + i], i) << 18) | (nib(c[Lo::W_NI + i], i) << 22);
+        U[i] = ((uint64_t)c[Lo::W_LOG + i] << 32) | own;
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            if (i == j) continue;
+            const uint64_t small = (uint64_t)(nib(c[Lo::W_MI + i], j) | (nib(c[Lo::W_NI + i], j) << 4) |
+                                              ((vf == (uint32_t)j) ? 256u : 0u));
+            const uint64_t m0 = (i == srow) ? row0[j] : M0[i * N + j];
+            const uint64_t m1 = (i == srow) ? row1[j] : M1[i * N + j];
+            X0[i * N + j] = m0 ^ (small * PAIR_K0);
+            X1[i * N + j] = m1 ^ (small * PAIR_K1);
+        }
+    }
+    uint64_t b0 = ~0ull, b1 = ~0ull;
+    const uint64_t *S0 = t.seeds, *S1 = t.seeds + (MAXN + MAXN * MAXN);
+    for (int p = 0; p < t.np; p++) {
+        const uint8_t *pi = t.perms + p * MAXN;
+        uint32_t img[N];
+#pragma unroll
+        for (int i = 0; i < N; i++) img[i] = pi[i];
+        uint64_t h0 = 0, h1 = 0;
+#pragma unroll
+        for (int i = 0; i < N; i++) {
+            h0 += mix64(U[i] ^ S0[img[i]]);
+            h1 += mix64(U[i] ^ S1[img[i]]);
+#pragma unroll
+            for (int j = 0; j < N; j++) {
+                if (i == j) continue;
+                const uint32_t q = MAXN + img[i] * MAXN + img[j];
+                h0 += mix64(X0[i * N + j] ^ S0[q]);
+                h1 += mix64(X1[i * N + j] ^ S1[q]);
+            }
+        }
+        if (h1 < b1 || (h1 == b1 && h0 < b0)) { b1 = h1; b0 = h0; }
+    }
+    return make_ulonglong2(b0 | 1ull, b1);
+}
+
+// ---- expansion of one parent per wavefront ------------------------------------------------
+template <int N, int V, int MR>
+struct Wave {
+    using S = Spec<N, V, MR>;
+    using Lo = Layout<N, V>;
+    uint32_t c[S::NW];   // parent core (wave-uniform), constant-index reads
+    const uint32_t *lds; // same core in LDS [NW] + vpcnt [N]: runtime-indexed reads
+    uint32_t nm;
+    uint32_t id[MR];     // message id owned by this lane per round (0xFFFF = none)
+    uint32_t inf[MR];
+};
+
+// Evaluate the message lane (round r) -> at most one successor.
+template <int N, int V, int MR>
+__device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> &W, const uint16_t *ids, int r, int lane,
+                         Succ<N, V, MR> &o, uint32_t &assert_key) {
+    using Lo = Layout<N, V>;
+    o.key = KEY_NONE;
+    o.nadd = 0;
+    o.s = 0;
+#pragma unroll
+    for (int a = 0; a < Spec<N, V, MR>::NADD; a++) o.add[a] = 0;
+    const uint32_t k = (uint32_t)(r * 64 + lane);
+    if (k >= W.nm) return;
+    const uint32_t m = W.inf[r];
+    const uint32_t s = mi_dst(m), typ = mi_type(m), mt = mi_term(m), src = mi_src(m);
+    const uint32_t ct = nib(W.c[Lo::W_CT], s), role = nib(W.c[Lo::W_ROLE], s);
+#pragma unroll
+    for (int w = 0; w < Lo::NW; w++) o.c[w] = W.c[w];
+    o.s = s;
+    if (mt > ct) {  // UpdateTerm, first disjunct (tla:178-182)
+        o.c[Lo::W_ROLE] = setnib(o.c[Lo::W_ROLE], s, FOL);
+        o.c[Lo::W_CT] = setnib(o.c[Lo::W_CT], s, mt);
+        o.c[Lo::W_VF] = setnib(o.c[Lo::W_VF], s, VF_NONE);
+        o.key = slot_key(s, UT, k);
+        return;
+    }
+    if (mt != ct) return;
+    if (typ == AREQ && role != FOL) {  // UpdateTerm, second disjunct (tla:183-188)
+        if (role == LEA) { assert_key = slot_key(s, UT, 0); return; }  // Assert(role[s] # Leader) tla:185
+        o.c[Lo::W_ROLE] = setnib(o.c[Lo::W_ROLE], s, FOL);
+        o.key = slot_key(s, UT, k);
+        return;
+    }
+    const uint32_t ll = nib(W.c[Lo::W_LL], s);
+    const uint32_t lw = W.lds[Lo::W_LOG + s];
+    if (typ == VREQ && role == FOL) {  // ResponseVote tla:132-155
+        const uint32_t vf = nib(W.c[Lo::W_VF], s);
+        if (!(vf == VF_NONE || vf == src)) return;
+        const uint32_t llt = lw_term(lw, ll), mlli = mi_x1(m), mllt = mi_x2(m);
+        if (!(mllt > llt || (mllt == llt && mlli >= ll))) return;
+        const uint32_t g = P.t.nat2id[nat_vresp(P.d, s, src, mt)];
+        if (has_id(ids, W.nm, g)) return;
+        o.c[Lo::W_VF] = setnib(o.c[Lo::W_VF], s, src);
+        o.add[0] = g; o.nadd = 1;
+        o.key = slot_key(s, RV, k);
+        return;
+    }
+    if (typ == AREQ && role == FOL) {  // FollowerAcceptEntry / FollowerRejectEntry tla:275-321
+        const uint32_t pli = mi_x1(m), plt = mi_x2(m), lc = mi_x3(m), ent = mi_ent(m);
+        const bool match = pli <= ll && plt == lw_term(lw, pli);  // LogMatch tla:271-273
+        if (match) {
+            const uint32_t nl = pli + ent;
+            const bool append_new = nl > ll;
+            const uint32_t eb = mi_et(m) | (mi_ev(m) << 4);
+            const bool truncated = nl <= ll && ent && lw_byte(lw, nl) != eb;
+            const uint32_t mn = lc < nl ? lc : nl;
+            const uint32_t ci = nib(W.c[Lo::W_CI], s);
+            const uint32_t nci = ci > mn ? ci : mn;
+            const uint32_t resp = P.t.nat2id[nat_aresp(P.d, s, src, mt, pli + ent, 1)];
+            o.c[Lo::W_CI] = setnib(o.c[Lo::W_CI], s, nci);
+            if (truncated || append_new) {
+                // newLog == SubSeq(logs[s], 1, prevLogIndex) \o entries   (tla:291)
+                uint32_t keep = pli >= 2 ? (pli - 1) * 8 : 0;  // bytes of indices 2..pli
+                uint32_t nlw = keep >= 32 ? lw : (lw & ((1u << keep) - 1u));
+                if (ent) nlw |= eb << (8 * (nl - 2));
+#pragma unroll
+                for (int q = 0; q < N; q++) o.c[Lo::W_LOG + q] = ((uint32_t)q == s) ? nlw : o.c[Lo::W_LOG + q];
+                o.c[Lo::W_LL] = setnib(o.c[Lo::W_LL], s, nl);
+            }
+            if (!has_id(ids, W.nm, resp)) { o.add[0] = resp; o.nadd = 1; }
+            o.key = slot_key(s, FAE, k);
+        } else {
+            const uint32_t resp = P.t.nat2id[nat_aresp(P.d, s, src, mt, pli, 0)];
+            if (has_id(ids, W.nm, resp)) return;
+            o.add[0] = resp; o.nadd = 1;
+            o.key = slot_key(s, FRE, k);
+        }
+        return;
+    }
+    if (typ == ARESP && role == LEA) {  // HandleAppendResp tla:374-396
+        const uint32_t pend = W.c[Lo::W_PEND];
+        const uint32_t pb = s * N + src;
+        if (!((pend >> pb) & 1u)) return;
+        const uint32_t pli = mi_x1(m);
+        const uint32_t mirow = W.lds[Lo::W_MI + s], nirow = W.lds[Lo::W_NI + s];
+        const uint32_t mi = nib(mirow, src), ni = nib(nirow, src);
+        uint32_t nmi = mirow, nni = nirow;
+        if (mi_x2(m)) {
+            if (!(mi < pli)) return;
+            nmi = setnib(mirow, src, pli);
+            nni = setnib(nirow, src, pli + 1);
+        } else {
+            if (!(pli + 1 == ni)) return;
+            if (!(pli > mi)) return;
+            nni = setnib(nirow, src, pli);
+        }
+#pragma unroll
+        for (int q = 0; q < N; q++) {
+            o.c[Lo::W_MI + q] = ((uint32_t)q == s) ? nmi : o.c[Lo::W_MI + q];
+            o.c[Lo::W_NI + q] = ((uint32_t)q == s) ? nni : o.c[Lo::W_NI + q];
+        }
+        o.c[Lo::W_PEND] = pend & ~(1u << pb);
+        o.key = slot_key(s, HAR, k);
+        return;
+    }
+}
+
+// Evaluate the non-message slot owned by this lane (last round).
+template <int N, int V, int MR>
+__device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR> &W, const uint16_t *ids, int lane,
+                          Succ<N, V, MR> &o) {
+    using Lo = Layout<N, V>;
+    using S = Spec<N, V, MR>;
+    o.key = KEY_NONE;
+    o.nadd = 0;
+    o.s = 0;
+#pragma unroll
+    for (int a = 0; a < S::NADD; a++) o.add[a] = 0;
+    if (lane >= N * S::SLOTS_PER_SERVER) return;
+    const uint32_t s = (uint32_t)lane / S::SLOTS_PER_SERVER, t = (uint32_t)lane % S::SLOTS_PER_SERVER;
+    const uint32_t role = nib(W.c[Lo::W_ROLE], s), ct = nib(W.c[Lo::W_CT], s), ll = nib(W.c[Lo::W_LL], s);
+    const uint32_t ci = nib(W.c[Lo::W_CI], s);
+    const uint32_t lw = W.lds[Lo::W_LOG + s];
+    const uint32_t misc = W.c[Lo::W_MISC];
+#pragma unroll
+    for (int w = 0; w < Lo::NW; w++) o.c[w] = W.c[w];
+    o.s = s;
+    if (t == 0) {  // BecomeCandidate tla:107-130
+        const uint32_t ec = misc & 15u;
+        if (!((int)ec < P.E)) return;
+        if (!(role == FOL || role == CAN)) return;
+        const uint32_t term = ct + 1, llt = lw_term(lw, ll);
+        o.c[Lo::W_CT] = setnib(o.c[Lo::W_CT], s, term);
+        o.c[Lo::W_ROLE] = setnib(o.c[Lo::W_ROLE], s, CAN);
+        o.c[Lo::W_VF] = setnib(o.c[Lo::W_VF], s, s);
+        o.c[Lo::W_MISC] = (misc & ~15u) | (ec + 1);
+        uint32_t na = 0;
+#pragma unroll
+        for (int p = 0; p < N; p++) {
+            if ((uint32_t)p == s) continue;
+            const uint32_t id = P.t.nat2id[nat_vreq(P.d, s, p, term, ll, llt)];
+            if (!has_id(ids, W.nm, id)) {
+#pragma unroll
+                for (int a = 0; a < S::NADD; a++) o.add[a] = ((uint32_t)a == na) ? id : o.add[a];
+                na++;
+            }
+        }
+        o.nadd = na;
+        o.key = slot_key(s, BC, 0);
+        return;
+    }
+    if (t == 1) {  // BecomeLeader tla:157-173
+        if (role != CAN) return;
+        const uint32_t vp = W.lds[Lo::NW + s];
+        if (!(vp + 1 >= (uint32_t)(N / 2 + 1))) return;
+        uint32_t mirow = 0, nirow = 0;
+#pragma unroll
+        for (int u = 0; u < N; u++) {
+            mirow = setnib(mirow, u, (uint32_t)u != s ? 1u : ll);
+            nirow = setnib(nirow, u, ll + 1);
+        }
+#pragma unroll
+        for (int q = 0; q < N; q++) {
+            o.c[Lo::W_MI + q] = ((uint32_t)q == s) ? mirow : o.c[Lo::W_MI + q];
+            o.c[Lo::W_NI + q] = ((uint32_t)q == s) ? nirow : o.c[Lo::W_NI + q];
+        }
+        o.c[Lo::W_PEND] = W.c[Lo::W_PEND] & ~(((1u << N) - 1u) << (s * N));
+        o.c[Lo::W_ROLE] = setnib(o.c[Lo::W_ROLE], s, LEA);
+        o.key = slot_key(s, BL, 0);
+        return;
+    }
+    if (t < 2 + (uint32_t)V) {  // ClientReq tla:233-240, witness v
+        const uint32_t v = t - 2;
+        if (role != LEA) return;
+        if ((misc >> (8 + v)) & 1u) return;  // valSent[v] # None
+        o.c[Lo::W_MISC] = misc | (1u << (8 + v));
+        const uint32_t nlw = lw | ((ct | (v << 4)) << (8 * (ll + 1 - 2)));
+        const uint32_t mirow = setnib(W.lds[Lo::W_MI + s], s, ll + 1);
+#pragma unroll
+        for (int q = 0; q < N; q++) {
+            o.c[Lo::W_LOG + q] = ((uint32_t)q == s) ? nlw : o.c[Lo::W_LOG + q];
+            o.c[Lo::W_MI + q] = ((uint32_t)q == s) ? mirow : o.c[Lo::W_MI + q];
+        }
+        o.c[Lo::W_LL] = setnib(o.c[Lo::W_LL], s, ll + 1);
+        o.key = slot_key(s, CR, v);
+        return;
+    }
+    if (t < 2 + (uint32_t)V + (N - 1)) {  // LeaderAppendEntry tla:242-269, witness dst
+        const uint32_t q = t - 2 - V;
+        const uint32_t dst = q < s ? q : q + 1;
+        if (role != LEA) return;
+        const uint32_t ni = nib(W.lds[Lo::W_NI + s], dst);
+        if (!(ni <= ll + 1)) return;
+        const uint32_t pb = s * N + dst;
+        if ((W.c[Lo::W_PEND] >> pb) & 1u) return;
+        const uint32_t pli = ni - 1, plt = lw_term(lw, pli);
+        const uint32_t ent = ni <= ll ? 1u : 0u;
+        const uint32_t eb = ent ? lw_byte(lw, ni) : 0u;
+        const uint32_t id = P.t.nat2id[nat_areq(P.d, s, dst, ct, pli, plt, ent, eb & 15u, eb >> 4, ci)];
+        if (has_id(ids, W.nm, id)) return;  // m \notin msgs
+        o.c[Lo::W_PEND] = W.c[Lo::W_PEND] | (1u << pb);
+        o.add[0] = id;
+        o.nadd = 1;
+        o.key = slot_key(s, LAE, dst);
+        return;
+    }
+    if (t == 2 + (uint32_t)V + (N - 1)) {  // LeaderCanCommit tla:398-407
+        if (role != LEA) return;
+        const uint32_t thr = P.seeded ? (uint32_t)N : (uint32_t)(N / 2 + 1);
+        const uint32_t med = median_row<N>(W.lds[Lo::W_MI + s], thr);
+        if (!(med > ci)) return;
+        o.c[Lo::W_CI] = setnib(o.c[Lo::W_CI], s, med);
+        o.key = slot_key(s, LCC, 0);
+        return;
+    }
+    {  // Restart tla:409-414
+        const uint32_t rc = (misc >> 4) & 15u;
+        if (role != LEA || !((int)rc < P.R)) return;
+        o.c[Lo::W_ROLE] = setnib(o.c[Lo::W_ROLE], s, FOL);
+        o.c[Lo::W_MISC] = (misc & ~0xF0u) | ((rc + 1) << 4);
+        o.key = slot_key(s, RS, 0);
+    }
+}
+
+// Load a state record into the wave: uniform core, per-lane message ids, LDS copy of
+// the sorted ids and the per-(src,dst) message hash sums.
+template <int N, int V, int MR, bool SUMS>
+__device__ __forceinline__ void load_parent(const KParams &P, const uint32_t *rec, int lane, Wave<N, V, MR> &W, uint16_t *ids,
+                            uint64_t *M0, uint64_t *M1, uint32_t *pcore) {
+    using Lo = Layout<N, V>;
+    using S = Spec<N, V, MR>;
+#pragma unroll
+    for (int w = 0; w < Lo::NW; w++) W.c[w] = rec[w];
+    if (lane < Lo::NW) pcore[lane] = rec[lane];
+    W.lds = pcore;
+    W.nm = (W.c[Lo::W_MISC] >> 16) & 0xFFu;
+    if (SUMS && lane < N * N) { M0[lane] = 0; M1[lane] = 0; }
+    __syncthreads();
+    const uint16_t *rid = reinterpret_cast<const uint16_t *>(rec + S::CW);
+#pragma unroll
+    for (int r = 0; r < MR; r++) {
+        const uint32_t k = (uint32_t)(r * 64 + lane);
+        uint32_t id = 0xFFFFu, inf = 0;
+        if (k < W.nm) {
+            id = rid[k];
+            inf = P.t.info[id];
+            if (SUMS) {
+                const ulonglong2 g = P.t.gmsg[id];
+                const uint32_t pr = mi_src(inf) * N + mi_dst(inf);
+                atomicAdd((unsigned long long *)&M0[pr], (unsigned long long)g.x);
+                atomicAdd((unsigned long long *)&M1[pr], (unsigned long long)g.y);
+            }
+        }
+        ids[k] = (uint16_t)id;
+        W.id[r] = id;
+        W.inf[r] = inf;
+    }
+#pragma unroll
+    for (int s = 0; s < N; s++) {
+        const uint32_t ct = nib(W.c[Lo::W_CT], s);
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int r = 0; r < MR; r++) {
+            const uint32_t m = W.inf[r];
+            const bool hit = (uint32_t)(r * 64 + lane) < W.nm && mi_type(m) == VRESP && mi_dst(m) == (uint32_t)s &&
+                             mi_term(m) == ct;
+            cnt += (uint32_t)__popcll(__ballot(hit));
+        }
+        if (lane == 0) pcore[Lo::NW + s] = cnt;
+    }
+    __syncthreads();
+}
+
+// hash row of the acting server: parent sums + the messages this successor adds
+template <int N, int V, int MR>
+__device__ __forceinline__ void succ_row(const KParams &P, const Succ<N, V, MR> &o, const uint64_t *M0,
+                                         const uint64_t *M1, uint64_t *row0, uint64_t *row1) {
+#pragma unroll
+    for (int j = 0; j < N; j++) { row0[j] = M0[o.s * N + j]; row1[j] = M1[o.s * N + j]; }
+#pragma unroll
+    for (int a = 0; a < Spec<N, V, MR>::NADD; a++) {
+        if ((uint32_t)a >= o.nadd) break;
+        const uint32_t id = o.add[a];
+        const uint32_t dst = mi_dst(P.t.info[id]);
+        const ulonglong2 g = P.t.gmsg[id];
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            row0[j] += ((uint32_t)j == dst) ? g.x : 0ull;
+            row1[j] += ((uint32_t)j == dst) ? g.y : 0ull;
+        }
+    }
+}
+
+// Write the successor held by lane t (round r) as a record at rec_out (whole wave).
+template <int N, int V, int MR>
+__device__ __forceinline__ void write_record(const Wave<N, V, MR> &W, const Succ<N, V, MR> &o, int t, int lane, uint32_t *rec_out) {
+    using Lo = Layout<N, V>;
+    using S = Spec<N, V, MR>;
+    const uint32_t nadd = rdlane(o.nadd, t);
+    uint32_t add[S::NADD];
+#pragma unroll
+    for (int a = 0; a < S::NADD; a++) add[a] = rdlane(o.add[a], t);
+    uint32_t v = 0;
+#pragma unroll
+    for (int w = 0; w < Lo::NW; w++) {
+        uint32_t x = rdlane(o.c[w], t);
+        if (w == Lo::W_MISC) x = (x & ~0xFF0000u) | ((W.nm + nadd) << 16);
+        v = (lane == w) ? x : v;
+    }
+    if (lane < S::CW) rec_out[lane] = v;
+    uint16_t *oid = reinterpret_cast<uint16_t *>(rec_out + S::CW);
+#pragma unroll
+    for (int r = 0; r < MR; r++) {
+        const uint32_t k = (uint32_t)(r * 64 + lane);
+        if (k < W.nm) {
+            const uint32_t id = W.id[r];
+            uint32_t pos = k;
+#pragma unroll
+            for (int a = 0; a < S::NADD; a++) pos += ((uint32_t)a < nadd && add[a] < id) ? 1u : 0u;
+            oid[pos] = (uint16_t)id;
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < S::NADD; a++) {
+        if ((uint32_t)a >= nadd) break;
+        uint32_t less = 0;
+#pragma unroll
+        for (int r = 0; r < MR; r++)
+            less += (uint32_t)__popcll(__ballot((uint32_t)(r * 64 + lane) < W.nm && W.id[r] < add[a]));
+#pragma unroll
+        for (int b = 0; b < S::NADD; b++) less += ((uint32_t)b < nadd && add[b] < add[a]) ? 1u : 0u;
+        if (lane == 0) oid[less] = (uint16_t)add[a];
+    }
+}
+
+__device__ __forceinline__ uint64_t t_index(const ulonglong2 f, uint64_t mask) {
+    return (f.y ^ (f.y >> 29) ^ (f.x >> 23)) & mask;
+}
+
+__device__ __forceinline__ void t_insert(ulonglong2 *T, uint64_t mask, ulonglong2 f) {
+    uint64_t h = t_index(f, mask);
+    for (;;) {
+        unsigned long long prev = atomicCAS((unsigned long long *)&T[h].x, 0ull, (unsigned long long)f.x);
+        if (prev == 0ull) { T[h].y = f.y; return; }
+        h = (h + 1) & mask;
+    }
+}
+
+template <int N, int V, int MR, int MODE>
+__global__ __launch_bounds__(64) void k_expand(KParams P) {
+    using S = Spec<N, V, MR>;
+    using Lo = Layout<N, V>;
+    constexpr bool SUMS = (MODE == M_HASH || MODE == M_SINGLE);
+    __shared__ uint16_t ids[S::MCAP];
+    __shared__ uint64_t M0[N * N], M1[N * N];
+    __shared__ uint32_t pcore[Lo::NW + N];
+    const int lane = threadIdx.x;
+    for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
+        const uint32_t *rec = P.front + p * (uint64_t)S::RECW;
+        Wave<N, V, MR> W;
+        load_parent<N, V, MR, SUMS>(P, rec, lane, W, ids, M0, M1, pcore);
+        Succ<N, V, MR> cand[MR + 1];
+        uint32_t akey = KEY_NONE;
+#pragma unroll
+        for (int r = 0; r < MR; r++) eval_msg<N, V, MR>(P, W, ids, r, lane, cand[r], akey);
+        eval_slot<N, V, MR>(P, W, ids, lane, cand[MR]);
+        // rank of every enabled successor in TLC order
+        uint64_t en[MR + 1];
+        uint32_t total = 0;
+#pragma unroll
+        for (int r = 0; r <= MR; r++) {
+            en[r] = __ballot(cand[r].key != KEY_NONE);
+            total += (uint32_t)__popcll(en[r]);
+        }
+        uint32_t rank[MR + 1];
+#pragma unroll
+        for (int r = 0; r <= MR; r++) rank[r] = 0;
+#pragma unroll
+        for (int q = 0; q <= MR; q++) {
+            for (uint64_t m = en[q]; m; m &= m - 1) {
+                const int t = __ffsll((unsigned long long)m) - 1;
+                const uint32_t kt = rdlane(cand[q].key, t);
+#pragma unroll
+                for (int r = 0; r <= MR; r++) rank[r] += kt < cand[r].key ? 1u : 0u;
+            }
+        }
+        const uint64_t pl = p - P.p_begin;  // chunk-local parent index
+        uint64_t am = 0;
+        if (MODE == M_COUNT || MODE == M_SINGLE) {
+            bool ovf = false;
+#pragma unroll
+            for (int r = 0; r <= MR; r++) ovf |= cand[r].key != KEY_NONE && W.nm + cand[r].nadd > (uint32_t)S::MCAP;
+            if (__ballot(ovf) && lane == 0) atomicOr(&P.flags[0], 1u);
+            am = __ballot(akey != KEY_NONE);
+            if (am) {
+                uint32_t best = KEY_NONE;
+                for (uint64_t m = am; m; m &= m - 1) {
+                    const uint32_t k = rdlane(akey, __ffsll((unsigned long long)m) - 1);
+                    best = k < best ? k : best;
+                }
+                if (lane == 0) atomicMin(&P.err[ERR_ASSERT], (((unsigned long long)p << 16) | best) << 8);
+            }
+        }
+        if (MODE == M_COUNT) {
+            if (lane == 0) {
+                P.cnt[pl] = total;
+                if (total == 0 && !am && P.check_deadlock) atomicMin(&P.err[ERR_DEADLOCK], ((unsigned long long)p << 16) << 8);
+            }
+            continue;
+        }
+        if (MODE == M_HASH || MODE == M_SINGLE) {
+            const uint64_t base = (MODE == M_HASH) ? P.off[pl] : 0;
+#pragma unroll
+            for (int r = 0; r <= MR; r++) {
+                if (cand[r].key != KEY_NONE) {
+                    uint64_t row0[N], row1[N];
+                    succ_row<N, V, MR>(P, cand[r], M0, M1, row0, row1);
+                    P.fp[base + rank[r]] = fingerprint<N, V>(cand[r].c, (int)cand[r].s, row0, row1, M0, M1, P.t);
+                }
+            }
+        }
+        if (MODE == M_HASH) continue;
+        // MATERIALIZE / SINGLE: write chosen successors
+#pragma unroll
+        for (int r = 0; r <= MR; r++) {
+            bool win = false;
+            uint64_t out = 0;
+            if (cand[r].key != KEY_NONE) {
+                if (MODE == M_SINGLE) {
+                    win = true;
+                    out = rank[r];
+                    P.out_keys[out] = cand[r].key;
+                } else {
+                    const uint64_t j = P.off[pl] + rank[r];
+                    win = P.wflag[j] != 0;
+                    if (win) {
+                        out = P.next_base + P.wpos[j];
+                        const uint64_t gid = P.gid_next_base + out;
+                        t_insert(P.T, P.Tmask, P.fp[j]);
+                        P.par[gid] = P.gid_parent_base + p;
+                        P.pslot[gid] = (uint16_t)cand[r].key;
+                        int which = 0;
+                        const int iv = check_invs<N, V>(cand[r].c, P.inv_mask, &which);
+                        if (iv != 1) {
+                            const unsigned long long ek =
+                                ((((unsigned long long)p << 16) | cand[r].key) << 8) | (unsigned long long)which;
+                            atomicMin(&P.err[iv == 0 ? ERR_INV : ERR_EVAL], ek);
+                        }
+                    }
+                }
+            }
+            for (uint64_t m = __ballot(win); m; m &= m - 1) {
+                const int t = __ffsll((unsigned long long)m) - 1;
+                const uint64_t ot = rdlane64(out, t);
+                write_record<N, V, MR>(W, cand[r], t, lane, P.next + ot * (uint64_t)S::RECW);
+            }
+        }
+        if (MODE == M_SINGLE && lane == 0) *P.out_count = total;
+    }
+}
+
+// fingerprints of whole states (Init, test hooks): one wave per state
+template <int N, int V, int MR>
+__global__ __launch_bounds__(64) void k_fp_states(KParams P, uint64_t n) {
+    using S = Spec<N, V, MR>;
+    __shared__ uint16_t ids[S::MCAP];
+    __shared__ uint64_t M0[N * N], M1[N * N];
+    __shared__ uint32_t pcore[Layout<N, V>::NW + N];
+    const int lane = threadIdx.x;
+    for (uint64_t p = blockIdx.x; p < n; p += gridDim.x) {
+        Wave<N, V, MR> W;
+        load_parent<N, V, MR, true>(P, P.front + p * (uint64_t)S::RECW, lane, W, ids, M0, M1, pcore);
+        uint64_t row0[N], row1[N];
+#pragma unroll
+        for (int j = 0; j < N; j++) { row0[j] = 0; row1[j] = 0; }
+        const ulonglong2 f = fingerprint<N, V>(W.c, -1, row0, row1, M0, M1, P.t);
+        if (lane == 0) P.fp[p] = f;
+    }
+}
+
+template <int N, int V, int MR>
+__global__ __launch_bounds__(64) void k_inv_states(KParams P, uint64_t n, int32_t *out) {
+    using S = Spec<N, V, MR>;
+    using Lo = Layout<N, V>;
+    const uint64_t i = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t *rec = P.front + i * (uint64_t)S::RECW;
+    uint32_t c[Lo::NW];
+#pragma unroll
+    for (int w = 0; w < Lo::NW; w++) c[w] = rec[w];
+    for (int b = 0; b < 7; b++) out[i * 7 + b] = inv_eval<N, V>(c, b);
+}
+
+static inline unsigned grid_for(uint64_t n) {
+    const uint64_t cap = 256ull * 32ull;  // 32 one-wave blocks per CU on 256 CUs
+    return (unsigned)(n < cap ? (n ? n : 1) : cap);
+}
+
+template <int N, int V, int MR>
+struct Launch {
+    static void count(const KParams &P, hipStream_t s) {
+        hipLaunchKernelGGL((k_expand<N, V, MR, M_COUNT>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
+    }
+    static void hash(const KParams &P, hipStream_t s) {
+        hipLaunchKernelGGL((k_expand<N, V, MR, M_HASH>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
+    }
+    static void mat(const KParams &P, hipStream_t s) {
+        hipLaunchKernelGGL((k_expand<N, V, MR, M_MAT>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
+    }
+    static void single(const KParams &P, hipStream_t s) {
+        hipLaunchKernelGGL((k_expand<N, V, MR, M_SINGLE>), dim3(1), dim3(64), 0, s, P);
+    }
+    static void fps(const KParams &P, uint64_t n, hipStream_t s) {
+        hipLaunchKernelGGL((k_fp_states<N, V, MR>), dim3(grid_for(n)), dim3(64), 0, s, P, n);
+    }
+    static void invs(const KParams &P, uint64_t n, int32_t *out, hipStream_t s) {
+        hipLaunchKernelGGL((k_inv_states<N, V, MR>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, P, n, out);
+    }
+};
+
+template <int N, int V, int MR>
+static void fill(KernelSet *ks) {
+    using S = Spec<N, V, MR>;
+    ks->N = N; ks->V = V; ks->MR = MR; ks->MCAP = S::MCAP; ks->CW = S::CW; ks->RECW = S::RECW;
+    ks->maxsucc = S::MCAP + N * S::SLOTS_PER_SERVER;
+    ks->count = &Launch<N, V, MR>::count;
+    ks->hash = &Launch<N, V, MR>::hash;
+    ks->materialize = &Launch<N, V, MR>::mat;
+    ks->single = &Launch<N, V, MR>::single;
+    ks->fp_states = &Launch<N, V, MR>::fps;
+    ks->inv_states = &Launch<N, V, MR>::invs;
+}
+
+bool get_kernels(int N, int V, int msg_cap, KernelSet *ks) {
+    const int MR = msg_cap <= 64 ? 1 : 2;
+#define RMC_CASE(n, v, mr) \
+    if (N == n && V == v && MR == mr) { fill<n, v, mr>(ks); return true; }
+    RMC_CASE(2, 1, 1) RMC_CASE(2, 2, 1)
+    RMC_CASE(3, 1, 1) RMC_CASE(3, 2, 1) RMC_CASE(3, 3, 1)
+    RMC_CASE(3, 1, 2) RMC_CASE(3, 2, 2)
+    RMC_CASE(4, 1, 2) RMC_CASE(4, 2, 2)
+    RMC_CASE(5, 1, 2) RMC_CASE(5, 2, 2)
+#undef RMC_CASE
+    return false;
+}
+
+// ---- seen-set / chunk dedup (thread per successor) -------------------------------------
+// Probe the global seen set T (read-only in this launch) and, for fingerprints not in
+// it, elect the first successor in TLC order per fingerprint in the chunk table L
+// (slots hold chunk-local successor indices; index order == TLC order).
+__global__ __launch_bounds__(256) void k_dedup(const ulonglong2 *__restrict__ fp, uint64_t G,
+                                               const ulonglong2 *__restrict__ T, uint64_t Tmask, uint32_t *L,
+                                               uint64_t Lmask, uint32_t *lslot) {
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < G; j += (uint64_t)gridDim.x * blockDim.x) {
+        const ulonglong2 f = fp[j];
+        uint64_t h = t_index(f, Tmask);
+        bool old = false;
+        for (;;) {
+            const ulonglong2 e = T[h];
+            if (e.x == 0ull) break;
+            if (e.x == f.x && e.y == f.y) { old = true; break; }
+            h = (h + 1) & Tmask;
+        }
+        if (old) { lslot[j] = 0xFFFFFFFFu; continue; }
+        uint64_t g = (f.x ^ (f.x >> 31) ^ (f.y >> 7)) & Lmask;
+        for (;;) {
+            uint32_t v = __hip_atomic_load(&L[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v == 0xFFFFFFFFu) {
+                const uint32_t prev = atomicCAS(&L[g], 0xFFFFFFFFu, (uint32_t)j);
+                if (prev == 0xFFFFFFFFu) break;
+                v = prev;
+            }
+            const ulonglong2 o = fp[v];
+            if (o.x == f.x && o.y == f.y) { atomicMin(&L[g], (uint32_t)j); break; }
+            g = (g + 1) & Lmask;
+        }
+        lslot[j] = (uint32_t)g;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_winflag(const uint32_t *__restrict__ lslot, const uint32_t *__restrict__ L,
+                                                 uint64_t G, uint32_t *__restrict__ w) {
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < G; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t g = lslot[j];
+        w[j] = (g != 0xFFFFFFFFu && L[g] == (uint32_t)j) ? 1u : 0u;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_rehash(const ulonglong2 *__restrict__ Told, uint64_t old_cap, ulonglong2 *Tn,
+                                                uint64_t mask) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < old_cap;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const ulonglong2 e = Told[i];
+        if (e.x) t_insert(Tn, mask, e);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_insert(const ulonglong2 *__restrict__ fp, uint64_t n, ulonglong2 *T,
+                                                uint64_t mask) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        t_insert(T, mask, fp[i]);
+}
+
+static inline unsigned grid256(uint64_t n) {
+    const uint64_t b = (n + 255) / 256, cap = 256ull * 16ull;
+    return (unsigned)(b < cap ? (b ? b : 1) : cap);
+}
+
+void launch_dedup(const ulonglong2 *fp, uint64_t G, const ulonglong2 *T, uint64_t Tmask, uint32_t *L, uint64_t Lmask,
+                  uint32_t *lslot, hipStream_t s) {
+    hipLaunchKernelGGL(k_dedup, dim3(grid256(G)), dim3(256), 0, s, fp, G, T, Tmask, L, Lmask, lslot);
+}
+void launch_winflag(const uint32_t *lslot, const uint32_t *L, uint64_t G, uint32_t *wflag, hipStream_t s) {
+    hipLaunchKernelGGL(k_winflag, dim3(grid256(G)), dim3(256), 0, s, lslot, L, G, wflag);
+}
+void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, ulonglong2 *Tnew, uint64_t new_mask, hipStream_t s) {
+    hipLaunchKernelGGL(k_rehash, dim3(grid256(old_cap)), dim3(256), 0, s, Told, old_cap, Tnew, new_mask);
+}
+void launch_insert_fps(const ulonglong2 *fp, uint64_t n, ulonglong2 *T, uint64_t Tmask, hipStream_t s) {
+    hipLaunchKernelGGL(k_insert, dim3(grid256(n)), dim3(256), 0, s, fp, n, T, Tmask);
+}
+
+}  // namespace rmc

@@ -1,0 +1,327 @@
+// raftmc -- TLC-compatible command line over librmc (the drop-in for myrun.sh:3).
+//
+//   raftmc [-deadlock] [-workers N] [-config Raft.cfg] [-device D] [-msgcap C] [-seenlog2 K] Raft.tla
+//
+// Accepts the flags myrun.sh passes to TLC (myrun.sh:3), reads the same Raft.tla /
+// Raft.cfg, and prints TLC's result lines (states generated, distinct states, depth,
+// the counterexample) so that parsers of raft.log keep working.  GPU-specific lines
+// are printed after TLC's block.  Exit codes follow TLC's (0 ok, 11 deadlock,
+// 12 safety violation, 14 Assert, 75 evaluation error, 150/151 spec/config errors).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "rmc.h"
+#include "rmc_cfg.h"
+
+namespace {
+
+const char *kActionNames[11] = {"BecomeCandidate", "UpdateTerm", "ResponseVote", "BecomeLeader",
+                                "ClientReq", "LeaderAppendEntry", "FollowerAcceptEntry", "FollowerRejectEntry",
+                                "HandleAppendResp", "LeaderCanCommit", "Restart"};
+const char *kInvNames[7] = {"Inv", "NoSplitVote", "RaftCanCommt", "FollowerCanCommit", "CommitAll", "NoAllCommit",
+                            "ExistLeaderAndCandidate"};
+
+std::string now_str() {
+    char buf[64];
+    std::time_t t = std::time(nullptr);
+    std::strftime(buf, sizeof buf, "%Y-%m-%d %H:%M:%S", std::localtime(&t));
+    return buf;
+}
+
+bool read_file(const std::string &path, std::string *out) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    std::stringstream ss;
+    ss << f.rdbuf();
+    *out = ss.str();
+    return true;
+}
+
+// Source range of each action definition body in the spec text: TLC prints
+// "<Name line L, col C to line L2, col C2 of module M>" for trace steps.
+struct Loc {
+    int l0 = 0, c0 = 0, l1 = 0, c1 = 0;
+};
+
+std::vector<Loc> action_locations(const std::string &tla) {
+    std::vector<std::string> lines;
+    std::stringstream ss(tla);
+    std::string ln;
+    while (std::getline(ss, ln)) {
+        if (!ln.empty() && ln.back() == '\r') ln.pop_back();
+        lines.push_back(ln);
+    }
+    std::vector<Loc> locs(11);
+    for (int a = 0; a < 11; a++) {
+        const std::string head = std::string(kActionNames[a]) + "(s) ==";
+        for (size_t i = 0; i < lines.size(); i++) {
+            if (lines[i].compare(0, head.size(), head) != 0) continue;
+            // body starts at the first non-blank character after "=="
+            size_t li = i, col = head.size();
+            while (li < lines.size()) {
+                while (col < lines[li].size() && isspace((unsigned char)lines[li][col])) col++;
+                if (col < lines[li].size()) break;
+                li++;
+                col = 0;
+            }
+            Loc L;
+            L.l0 = (int)li + 1;
+            L.c0 = (int)col + 1;
+            // body ends at the last non-blank line before the next column-1 line
+            size_t j = li + 1;
+            while (j < lines.size() && (lines[j].empty() || isspace((unsigned char)lines[j][0]))) j++;
+            size_t e = j - 1;
+            while (e > li && lines[e].find_first_not_of(" \t") == std::string::npos) e--;
+            size_t endc = lines[e].find_last_not_of(" \t");
+            L.l1 = (int)e + 1;
+            L.c1 = (int)endc + 1;
+            locs[a] = L;
+            break;
+        }
+    }
+    return locs;
+}
+
+struct Printer {
+    const rmc::ParsedModel &pm;
+    int n, V;
+    std::string sv(int i) const { return i < 0 ? "None" : pm.servers[i]; }
+    std::string fn_servers(const std::vector<std::string> &vals) const {
+        std::string s = "(";
+        for (int i = 0; i < n; i++) s += (i ? " @@ " : "") + pm.servers[i] + " :> " + vals[i];
+        return s + ")";
+    }
+    std::string entry(int t, int v) const {
+        return "[term |-> " + std::to_string(t) + ", val |-> " + (v < 0 ? std::string("None") : pm.vals[v]) + "]";
+    }
+    std::string state(const int32_t *u) const {
+        int k = 0;
+        std::vector<std::string> vf, ct, role, ci, logs;
+        for (int i = 0; i < n; i++) vf.push_back(sv(u[k++]));
+        for (int i = 0; i < n; i++) ct.push_back(std::to_string(u[k++]));
+        static const char *rn[3] = {"Follower", "Candidate", "Leader"};
+        for (int i = 0; i < n; i++) role.push_back(rn[u[k++]]);
+        for (int i = 0; i < n; i++) ci.push_back(std::to_string(u[k++]));
+        std::vector<int> ll;
+        for (int i = 0; i < n; i++) ll.push_back(u[k++]);
+        for (int i = 0; i < n; i++) {
+            std::string s = "<<";
+            for (int x = 1; x <= V + 1; x++) {
+                int t = u[k], v = u[k + 1];
+                k += 2;
+                if (x <= ll[i]) s += (x > 1 ? ", " : "") + entry(t, v);
+            }
+            logs.push_back(s + ">>");
+        }
+        auto matrix = [&](bool boolean) {
+            std::vector<std::string> rows;
+            for (int i = 0; i < n; i++) {
+                std::vector<std::string> r;
+                for (int j = 0; j < n; j++) {
+                    int v = u[k++];
+                    r.push_back(boolean ? (v ? "TRUE" : "FALSE") : std::to_string(v));
+                }
+                rows.push_back(fn_servers(r));
+            }
+            return fn_servers(rows);
+        };
+        std::string mi = matrix(false), ni = matrix(false), pend = matrix(true);
+        int ec = u[k++], rc = u[k++];
+        std::string vs = "(";
+        for (int v = 0; v < V; v++) vs += (v ? " @@ " : "") + pm.vals[v] + " :> " + (u[k++] < 0 ? "None" : "FALSE");
+        vs += ")";
+        if (V == 0) vs = "<<>>";
+        int nm = u[k++];
+        std::string msgs = "{";
+        static const char *tn[4] = {"VoteReq", "VoteResp", "AppendReq", "AppendResp"};
+        for (int q = 0; q < nm; q++, k += 8) {
+            const int32_t *m = u + k;
+            std::string r;
+            switch (m[0]) {
+            case 0:
+                r = "[dst |-> " + sv(m[2]) + ", lastLogIndex |-> " + std::to_string(m[4]) + ", lastLogTerm |-> " +
+                    std::to_string(m[5]) + ", src |-> " + sv(m[1]) + ", term |-> " + std::to_string(m[3]) +
+                    ", type |-> VoteReq]";
+                break;
+            case 1:
+                r = "[dst |-> " + sv(m[2]) + ", src |-> " + sv(m[1]) + ", term |-> " + std::to_string(m[3]) +
+                    ", type |-> VoteResp]";
+                break;
+            case 2:
+                r = "[dst |-> " + sv(m[2]) + ", entries |-> <<" + (m[7] < 0 ? "" : entry(m[7] / 8, m[7] % 8)) +
+                    ">>, leaderCommit |-> " + std::to_string(m[6]) + ", prevLogIndex |-> " + std::to_string(m[4]) +
+                    ", prevLogTerm |-> " + std::to_string(m[5]) + ", src |-> " + sv(m[1]) + ", term |-> " +
+                    std::to_string(m[3]) + ", type |-> AppendReq]";
+                break;
+            default:
+                r = "[dst |-> " + sv(m[2]) + ", prevLogIndex |-> " + std::to_string(m[4]) + ", src |-> " + sv(m[1]) +
+                    ", succ |-> " + (m[5] ? "TRUE" : "FALSE") + ", term |-> " + std::to_string(m[3]) +
+                    ", type |-> AppendResp]";
+            }
+            (void)tn;
+            msgs += (q ? ",\n   " : "") + r;
+        }
+        msgs += "}";
+        std::string o;
+        o += "/\\ votedFor = " + fn_servers(vf) + "\n";
+        o += "/\\ currentTerm = " + fn_servers(ct) + "\n";
+        o += "/\\ logs = " + fn_servers(logs) + "\n";
+        o += "/\\ matchIndex = " + mi + "\n";
+        o += "/\\ nextIndex = " + ni + "\n";
+        o += "/\\ commitIndex = " + fn_servers(ci) + "\n";
+        o += "/\\ msgs = " + msgs + "\n";
+        o += "/\\ role = " + fn_servers(role) + "\n";
+        o += "/\\ electionCount = " + std::to_string(ec) + "\n";
+        o += "/\\ restartCount = " + std::to_string(rc) + "\n";
+        o += "/\\ pendingResponse = " + pend + "\n";
+        o += "/\\ valSent = " + vs + "\n";
+        return o;
+    }
+};
+
+int usage(const char *msg) {
+    std::fprintf(stderr, "raftmc: %s\nusage: raftmc [-deadlock] [-workers N] [-config FILE.cfg] [-device D] "
+                         "[-msgcap C] [-seenlog2 K] FILE.tla\n", msg);
+    return 150;
+}
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    std::string tla_path, cfg_path;
+    int check_deadlock = 1, device = -1, msgcap = 0, seenlog2 = 0, workers = 1;
+    for (int i = 1; i < argc; i++) {
+        std::string a = argv[i];
+        auto need = [&](const char *f) -> const char * {
+            if (i + 1 >= argc) { std::fprintf(stderr, "raftmc: %s needs an argument\n", f); std::exit(150); }
+            return argv[++i];
+        };
+        if (a == "-deadlock") check_deadlock = 0;  // TLC: -deadlock turns deadlock checking OFF
+        else if (a == "-workers") workers = std::atoi(need("-workers"));  // CPU threads in TLC; the GPU path ignores it
+        else if (a == "-config") cfg_path = need("-config");
+        else if (a == "-device") device = std::atoi(need("-device"));
+        else if (a == "-msgcap") msgcap = std::atoi(need("-msgcap"));
+        else if (a == "-seenlog2") seenlog2 = std::atoi(need("-seenlog2"));
+        else if (a.size() > 4 && a.compare(a.size() - 4, 4, ".tla") == 0) tla_path = a;
+        else if (a[0] != '-' && tla_path.empty()) tla_path = a + ".tla";
+        else return usage(("unsupported option " + a).c_str());
+    }
+    if (tla_path.empty()) return usage("missing spec file");
+    if (cfg_path.empty()) cfg_path = tla_path.substr(0, tla_path.size() - 4) + ".cfg";
+    std::string tla, cfgtxt;
+    const bool skip_spec = std::getenv("RMC_SKIP_SPEC_CHECK") && std::string(std::getenv("RMC_SKIP_SPEC_CHECK")) == "1";
+    if (!read_file(tla_path, &tla)) {
+        if (!skip_spec) { std::fprintf(stderr, "Error: cannot read %s\n", tla_path.c_str()); return 150; }
+        tla.clear();
+    }
+    if (!read_file(cfg_path, &cfgtxt)) { std::fprintf(stderr, "Error: cannot read %s\n", cfg_path.c_str()); return 151; }
+    rmc::ParsedModel pm;
+    std::string err;
+    if (!rmc::parse_model(cfgtxt, skip_spec ? nullptr : tla.c_str(), &pm, err)) {
+        std::fprintf(stdout, "Error: %s\n", err.c_str());
+        return err.rfind("cfg", 0) == 0 || err.rfind("CONSTANT", 0) == 0 ? 151 : 150;
+    }
+    if (skip_spec) {
+        const std::string base = tla_path.substr(tla_path.find_last_of('/') + 1);
+        if (base == "RaftSeeded.tla") { pm.cfg.spec_variant = RMC_SPEC_SEEDED; pm.module = "RaftSeeded"; }
+    }
+    if (pm.check_deadlock_cfg >= 0 && check_deadlock) check_deadlock = pm.check_deadlock_cfg;
+    rmc_config cfg = pm.cfg;
+    cfg.check_deadlock = check_deadlock;
+    cfg.device = device;
+    cfg.msg_cap = msgcap;
+    cfg.seen_log2 = seenlog2;
+
+    std::printf("raftmc (MI355X-native model checker for kikimo/tla-raft) -- TLC-compatible output\n");
+    std::printf("Running breadth-first search Model-Checking on the GPU (TLC -workers %d order: 1).\n", workers);
+    std::printf("Parsing file %s\n", tla_path.c_str());
+    std::printf("Semantic processing of module %s\n", pm.module.c_str());
+    for (const auto &c : pm.ignored_constants) std::printf("(ignoring assignment to undeclared constant %s)\n", c.c_str());
+    std::printf("Starting... (%s)\n", now_str().c_str());
+    const auto t0 = std::chrono::steady_clock::now();
+    void *ctx = nullptr;
+    int rc = rmc_create(&cfg, &ctx);
+    if (rc != RMC_OK) { std::printf("Error: could not start the GPU model checker (code %d)\n", rc); return 75; }
+    std::printf("Computing initial states...\n");
+    rmc_level_stats st;
+    rc = rmc_init(ctx, &st);
+    if (rc < 0) { std::printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 75; }
+    std::printf("Finished computing initial states: 1 distinct state generated at %s.\n", now_str().c_str());
+    double gpu_seconds = 0;
+    while (rc == RMC_OK) {
+        rc = rmc_step(ctx, &st);
+        if (rc < 0) break;
+        gpu_seconds += st.seconds;
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("Progress(%d) at %s: %llu states generated (%.0f s/min), %llu distinct states found (%.0f ds/min), "
+                    "%llu states left on queue.\n",
+                    st.level + 1, now_str().c_str(), (unsigned long long)st.total_generated,
+                    st.total_generated / el * 60.0, (unsigned long long)st.total_distinct,
+                    st.total_distinct / el * 60.0, (unsigned long long)st.queue);
+        std::fflush(stdout);
+    }
+    if (rc < 0) {
+        std::printf("Error: %s\n", rmc_last_error(ctx));
+        rmc_destroy(ctx);
+        return 75;
+    }
+    rmc_result res;
+    rmc_get_result(ctx, &res);
+    int exit_code = 0;
+    if (res.status == RMC_DONE) {
+        std::printf("Model checking completed. No error has been found.\n");
+    } else {
+        if (res.status == RMC_VIOLATION) {
+            std::printf("Error: Invariant %s is violated.\n",
+                        res.violated == 0 && !pm.invariant_names.empty() ? pm.invariant_names[0].c_str()
+                                                                          : kInvNames[res.violated]);
+            exit_code = 12;
+        } else if (res.status == RMC_ASSERT) {
+            std::printf("Error: The first argument of Assert evaluated to FALSE; the second argument was:\n\"split brain\"\n");
+            exit_code = 14;
+        } else if (res.status == RMC_EVAL_ERROR) {
+            std::printf("Error: Evaluating invariant %s failed.\nAttempted to apply a tuple to an index out of its domain "
+                        "(logs[p][index], %s.tla line 499).\n", kInvNames[res.violated], pm.module.c_str());
+            exit_code = 75;
+        } else if (res.status == RMC_DEADLOCK) {
+            std::printf("Error: Deadlock reached.\n");
+            exit_code = 11;
+        }
+        std::printf("Error: The behavior up to this point is:\n");
+        std::vector<Loc> locs = action_locations(tla);
+        Printer pr{pm, cfg.n_servers, cfg.n_vals};
+        std::vector<int32_t> buf(RMC_UNPACKED_INTS(5, 3, 256));
+        for (uint32_t i = 0; i < res.trace_len; i++) {
+            int32_t a, s, w;
+            int nints = rmc_trace_state(ctx, i, buf.data(), buf.size(), &a, &s, &w);
+            if (nints < 0) break;
+            if (a < 0) std::printf("State %u: <Initial predicate>\n", i + 1);
+            else {
+                const Loc &L = locs[a];
+                if (L.l0)
+                    std::printf("State %u: <%s line %d, col %d to line %d, col %d of module %s>\n", i + 1,
+                                kActionNames[a], L.l0, L.c0, L.l1, L.c1, pm.module.c_str());
+                else
+                    std::printf("State %u: <%s(%s)>\n", i + 1, kActionNames[a], pm.servers[s].c_str());
+            }
+            std::printf("%s\n", pr.state(buf.data()).c_str());
+        }
+    }
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::printf("%llu states generated, %llu distinct states found, %llu states left on queue.\n",
+                (unsigned long long)res.generated, (unsigned long long)res.distinct, (unsigned long long)res.queue);
+    if (res.status == RMC_DONE)
+        std::printf("The depth of the complete state graph search is %d.\n", res.depth);
+    std::printf("Finished in %.2fs at (%s)\n", el, now_str().c_str());
+    std::printf("GPU: %.0f distinct states/s over %.3f s of BFS levels (MI355X, 1 device).\n",
+                gpu_seconds > 0 ? res.distinct / gpu_seconds : 0.0, gpu_seconds);
+    rmc_destroy(ctx);
+    return exit_code;
+}

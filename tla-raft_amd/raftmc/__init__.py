@@ -1,0 +1,389 @@
+"""raftmc -- Python binding of librmc.so, the MI355X-native model checker for kikimo/tla-raft.
+
+This is the host-side mirror of the reference's only interface, the TLC run in
+``myrun.sh:3`` (``-deadlock -workers 4 -config Raft.cfg Raft.tla``): parse the
+model config, exhaust ``Raft.tla``'s state space breadth-first and report TLC's
+numbers (states generated, distinct states, depth, counterexample).  Everything
+runs in the HIP kernels behind the C-ABI declared in ``include/rmc.h``; there is
+no CPU fallback -- ``ModelChecker`` raises if the library or the GPU is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "librmc.so")
+
+RMC_OK, RMC_DONE, RMC_VIOLATION, RMC_ASSERT, RMC_EVAL_ERROR, RMC_DEADLOCK = 0, 1, 2, 3, 4, 5
+STATUS_NAMES = {RMC_OK: "ok", RMC_DONE: "done", RMC_VIOLATION: "invariant", RMC_ASSERT: "assert",
+                RMC_EVAL_ERROR: "eval_error", RMC_DEADLOCK: "deadlock"}
+ERRORS = {-1: "RMC_E_ARG", -2: "RMC_E_DEVICE", -3: "RMC_E_MEMORY", -4: "RMC_E_CAPACITY",
+          -5: "RMC_E_STATE", -6: "RMC_E_PARSE", -7: "RMC_E_COMM"}
+
+# invariant bits (include/rmc.h), Raft.tla:434-503
+INVARIANT_BITS = {
+    "Inv": 1 << 0, "LeaderHasAllCommittedEntries": 1 << 0, "NoSplitVote": 1 << 1, "RaftCanCommt": 1 << 2,
+    "FollowerCanCommit": 1 << 3, "CommitAll": 1 << 4, "NoAllCommit": 1 << 5, "ExistLeaderAndCandidate": 1 << 6,
+}
+INVARIANT_BY_BIT = ["Inv", "NoSplitVote", "RaftCanCommt", "FollowerCanCommit", "CommitAll", "NoAllCommit",
+                    "ExistLeaderAndCandidate"]
+ACTIONS = ("BecomeCandidate", "UpdateTerm", "ResponseVote", "BecomeLeader", "ClientReq", "LeaderAppendEntry",
+           "FollowerAcceptEntry", "FollowerRejectEntry", "HandleAppendResp", "LeaderCanCommit", "Restart")
+SPEC_RAFT, SPEC_SEEDED = 0, 1
+
+
+class RmcError(RuntimeError):
+    pass
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [
+        ("n_servers", ctypes.c_int32), ("n_vals", ctypes.c_int32), ("max_election", ctypes.c_int32),
+        ("max_restart", ctypes.c_int32), ("invariants", ctypes.c_uint32), ("check_deadlock", ctypes.c_int32),
+        ("spec_variant", ctypes.c_int32), ("device", ctypes.c_int32), ("msg_cap", ctypes.c_int32),
+        ("seen_log2", ctypes.c_int32), ("no_symmetry", ctypes.c_int32), ("chunk_successors", ctypes.c_uint64),
+        ("rank", ctypes.c_int32), ("world_size", ctypes.c_int32), ("comm_unique_id", ctypes.c_void_p),
+    ]
+
+
+class _LevelStats(ctypes.Structure):
+    _fields_ = [
+        ("level", ctypes.c_int32), ("status", ctypes.c_int32), ("expanded", ctypes.c_uint64),
+        ("generated", ctypes.c_uint64), ("new_states", ctypes.c_uint64), ("total_generated", ctypes.c_uint64),
+        ("total_distinct", ctypes.c_uint64), ("queue", ctypes.c_uint64), ("seconds", ctypes.c_double),
+        ("kernel_ms", ctypes.c_double * 6), ("kernel_launches", ctypes.c_uint64 * 6),
+    ]
+
+
+class _Result(ctypes.Structure):
+    _fields_ = [
+        ("status", ctypes.c_int32), ("depth", ctypes.c_int32), ("generated", ctypes.c_uint64),
+        ("distinct", ctypes.c_uint64), ("queue", ctypes.c_uint64), ("violated", ctypes.c_int32),
+        ("trace_len", ctypes.c_uint32), ("seconds", ctypes.c_double),
+    ]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load librmc.so; raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RmcError(f"librmc.so not found at {path}: run __graft_entry__.build() (make -C tla-raft_amd)")
+    lib = ctypes.CDLL(path)
+    vp, i32, u32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
+    P = ctypes.POINTER
+    lib.rmc_abi_version.restype = ctypes.c_int
+    lib.rmc_parse_config.argtypes = [ctypes.c_char_p, ctypes.c_char_p, P(_Config), ctypes.c_char_p, ctypes.c_size_t]
+    lib.rmc_create.argtypes = [P(_Config), P(vp)]
+    lib.rmc_init.argtypes = [vp, P(_LevelStats)]
+    lib.rmc_step.argtypes = [vp, P(_LevelStats)]
+    lib.rmc_run.argtypes = [vp, P(_Result)]
+    lib.rmc_get_result.argtypes = [vp, P(_Result)]
+    lib.rmc_trace_len.argtypes = [vp, P(u32)]
+    lib.rmc_trace_state.argtypes = [vp, u32, P(i32), ctypes.c_size_t, P(i32), P(i32), P(i32)]
+    lib.rmc_last_error.argtypes = [vp]
+    lib.rmc_last_error.restype = ctypes.c_char_p
+    lib.rmc_destroy.argtypes = [vp]
+    lib.rmc_destroy.restype = None
+    lib.rmc_successors.argtypes = [vp, P(i32), P(i32), ctypes.c_size_t, u32, P(u32), P(u64), P(u32)]
+    lib.rmc_fingerprint.argtypes = [vp, P(i32), P(u64)]
+    lib.rmc_eval_invariant.argtypes = [vp, P(i32), u32, P(i32)]
+    _lib = lib
+    return lib
+
+
+# ------------------------------------------------------------------------------ config
+@dataclass
+class ModelConfig:
+    """What Raft.cfg binds (Raft.cfg:1-34) plus TLC's -deadlock flag (myrun.sh:3)."""
+    n_servers: int = 3
+    n_vals: int = 2
+    max_election: int = 3
+    max_restart: int = 3
+    invariants: Tuple[str, ...] = ("Inv",)
+    check_deadlock: bool = False
+    spec_variant: int = SPEC_RAFT
+    symmetry: bool = True
+    device: int = -1
+    msg_cap: int = 0
+    seen_log2: int = 0
+    chunk_successors: int = 0
+
+    def to_c(self) -> _Config:
+        c = _Config()
+        c.n_servers, c.n_vals = self.n_servers, self.n_vals
+        c.max_election, c.max_restart = self.max_election, self.max_restart
+        mask = 0
+        for name in self.invariants:
+            mask |= INVARIANT_BITS[name]
+        c.invariants = mask
+        c.check_deadlock = int(self.check_deadlock)
+        c.spec_variant = self.spec_variant
+        c.device = self.device
+        c.msg_cap = self.msg_cap
+        c.seen_log2 = self.seen_log2
+        c.no_symmetry = 0 if self.symmetry else 1
+        c.chunk_successors = self.chunk_successors
+        c.rank, c.world_size = 0, 1
+        return c
+
+
+def parse_config(cfg_text: str, tla_text: Optional[str] = None) -> ModelConfig:
+    """Parse Raft.cfg text (and identify Raft.tla by content) through the library's parser."""
+    lib = load_library()
+    c = _Config()
+    err = ctypes.create_string_buffer(512)
+    rc = lib.rmc_parse_config(cfg_text.encode(), tla_text.encode() if tla_text is not None else None,
+                              ctypes.byref(c), err, 512)
+    if rc != RMC_OK:
+        raise RmcError(err.value.decode())
+    invs = tuple(name for bit, name in enumerate(INVARIANT_BY_BIT) if c.invariants & (1 << bit))
+    return ModelConfig(n_servers=c.n_servers, n_vals=c.n_vals, max_election=c.max_election,
+                       max_restart=c.max_restart, invariants=invs, check_deadlock=bool(c.check_deadlock),
+                       spec_variant=c.spec_variant, symmetry=not c.no_symmetry)
+
+
+# ------------------------------------------------------------------------------ unpacked states
+MSG_TYPES = ("VoteReq", "VoteResp", "AppendReq", "AppendResp")
+
+
+def unpacked_len(n: int, V: int, nmsgs: int) -> int:
+    return 5 * n + n * (V + 1) * 2 + 3 * n * n + 3 + V + 8 * nmsgs
+
+
+def state_to_unpacked(d: dict, n: int, V: int) -> List[int]:
+    """JSON state (oracle fixture format) -> rmc unpacked int32 layout (include/rmc.h)."""
+    u: List[int] = []
+    u += d["votedFor"] + d["currentTerm"] + d["role"] + d["commitIndex"] + [len(l) for l in d["logs"]]
+    for log in d["logs"]:
+        for x in range(V + 1):
+            if x < len(log):
+                u += [log[x][0], log[x][1]]
+            else:
+                u += [0, 0]
+    for r in d["matchIndex"]:
+        u += r
+    for r in d["nextIndex"]:
+        u += r
+    for r in d["pendingResponse"]:
+        u += [1 if b else 0 for b in r]
+    u += [d["electionCount"], d["restartCount"]] + list(d["valSent"]) + [len(d["msgs"])]
+    for m in d["msgs"]:
+        t = MSG_TYPES.index(m["type"])
+        rec = [t, m["src"], m["dst"], m["term"], 0, 0, 0, 0]
+        if m["type"] == "VoteReq":
+            rec[4:6] = [m["lastLogIndex"], m["lastLogTerm"]]
+        elif m["type"] == "AppendResp":
+            rec[4:6] = [m["prevLogIndex"], 1 if m["succ"] else 0]
+        elif m["type"] == "AppendReq":
+            e = m["entries"]
+            rec[4:8] = [m["prevLogIndex"], m["prevLogTerm"], m["leaderCommit"], e[0][0] * 8 + e[0][1] if e else -1]
+        u += rec
+    return u
+
+
+def unpacked_to_state(u: Sequence[int], n: int, V: int) -> dict:
+    k = 0
+
+    def take(c):
+        nonlocal k
+        r = list(u[k:k + c])
+        k += c
+        return r
+
+    d: Dict[str, object] = {}
+    d["votedFor"] = take(n)
+    d["currentTerm"] = take(n)
+    d["role"] = take(n)
+    d["commitIndex"] = take(n)
+    ll = take(n)
+    logs = []
+    for i in range(n):
+        ent = take(2 * (V + 1))
+        logs.append([[ent[2 * x], ent[2 * x + 1]] for x in range(ll[i])])
+    d["logs"] = logs
+    d["matchIndex"] = [take(n) for _ in range(n)]
+    d["nextIndex"] = [take(n) for _ in range(n)]
+    d["pendingResponse"] = [[bool(x) for x in take(n)] for _ in range(n)]
+    d["electionCount"], d["restartCount"] = take(2)
+    d["valSent"] = take(V)
+    nm = take(1)[0]
+    msgs = []
+    for _ in range(nm):
+        t, src, dst, term, x1, x2, x3, x4 = take(8)
+        m = {"type": MSG_TYPES[t], "src": src, "dst": dst, "term": term}
+        if t == 0:
+            m.update(lastLogIndex=x1, lastLogTerm=x2)
+        elif t == 3:
+            m.update(prevLogIndex=x1, succ=bool(x2))
+        elif t == 2:
+            m.update(prevLogIndex=x1, prevLogTerm=x2, leaderCommit=x3,
+                     entries=[] if x4 < 0 else [[x4 // 8, x4 % 8]])
+        msgs.append(m)
+    d["msgs"] = msgs
+    return d
+
+
+# ------------------------------------------------------------------------------ checker
+@dataclass
+class LevelStats:
+    level: int
+    status: str
+    expanded: int
+    generated: int
+    new_states: int
+    total_generated: int
+    total_distinct: int
+    queue: int
+    seconds: float
+    kernel_ms: List[float] = field(default_factory=list)
+
+
+@dataclass
+class Result:
+    status: str
+    depth: int
+    generated: int
+    distinct: int
+    queue: int
+    violated: Optional[str]
+    trace_len: int
+    seconds: float
+    levels: List[LevelStats] = field(default_factory=list)
+
+
+class ModelChecker:
+    """One GPU model-checking run (TLC's ModelChecker for myrun.sh:3)."""
+
+    def __init__(self, cfg: ModelConfig):
+        self.lib = load_library()
+        self.cfg = cfg
+        self._c = cfg.to_c()
+        h = ctypes.c_void_p()
+        rc = self.lib.rmc_create(ctypes.byref(self._c), ctypes.byref(h))
+        if rc != RMC_OK:
+            raise RmcError(f"rmc_create failed: {ERRORS.get(rc, rc)} (see stderr)")
+        self.h = h
+        self.levels: List[LevelStats] = []
+        self._inited = False
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.rmc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int) -> int:
+        if rc < 0:
+            raise RmcError(f"{ERRORS.get(rc, rc)}: {self.lib.rmc_last_error(self.h).decode()}")
+        return rc
+
+    @staticmethod
+    def _stats(s: _LevelStats) -> LevelStats:
+        return LevelStats(s.level, STATUS_NAMES.get(s.status, str(s.status)), s.expanded, s.generated,
+                          s.new_states, s.total_generated, s.total_distinct, s.queue, s.seconds,
+                          list(s.kernel_ms))
+
+    def init(self) -> LevelStats:
+        st = _LevelStats()
+        self._check(self.lib.rmc_init(self.h, ctypes.byref(st)))
+        self._inited = True
+        ls = self._stats(st)
+        self.levels.append(ls)
+        return ls
+
+    def step(self) -> LevelStats:
+        st = _LevelStats()
+        self._check(self.lib.rmc_step(self.h, ctypes.byref(st)))
+        ls = self._stats(st)
+        self.levels.append(ls)
+        return ls
+
+    def run(self) -> Result:
+        if not self._inited:
+            ls = self.init()
+            if ls.status != "ok":
+                return self.result()
+        while True:
+            ls = self.step()
+            if ls.status != "ok":
+                break
+        return self.result()
+
+    def result(self) -> Result:
+        r = _Result()
+        self._check(self.lib.rmc_get_result(self.h, ctypes.byref(r)))
+        return Result(STATUS_NAMES.get(r.status, str(r.status)), r.depth, r.generated, r.distinct, r.queue,
+                      INVARIANT_BY_BIT[r.violated] if r.violated >= 0 else None, r.trace_len, r.seconds,
+                      list(self.levels))
+
+    def trace(self) -> List[Tuple[Optional[Tuple[int, int, int]], dict]]:
+        n = ctypes.c_uint32()
+        self._check(self.lib.rmc_trace_len(self.h, ctypes.byref(n)))
+        cap = unpacked_len(self.cfg.n_servers, self.cfg.n_vals, 256)
+        buf = (ctypes.c_int32 * cap)()
+        out = []
+        for i in range(n.value):
+            a, s, w = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+            k = self._check(self.lib.rmc_trace_state(self.h, i, buf, cap, ctypes.byref(a), ctypes.byref(s),
+                                                     ctypes.byref(w)))
+            st = unpacked_to_state(list(buf[:k]), self.cfg.n_servers, self.cfg.n_vals)
+            out.append((None if a.value < 0 else (s.value, a.value, w.value), st))
+        return out
+
+    # ---- single-state hooks ------------------------------------------------------------
+    def _unpacked(self, state: dict):
+        u = state_to_unpacked(state, self.cfg.n_servers, self.cfg.n_vals)
+        return (ctypes.c_int32 * len(u))(*u)
+
+    def successors(self, state: dict, cap: int = 512):
+        """[(key(server, action, witness), successor_state, fp128)] in TLC order; raises on Assert."""
+        n, V = self.cfg.n_servers, self.cfg.n_vals
+        stride = unpacked_len(n, V, 256)
+        out = (ctypes.c_int32 * (stride * cap))()
+        keys = (ctypes.c_uint32 * cap)()
+        fps = (ctypes.c_uint64 * (2 * cap))()
+        cnt = ctypes.c_uint32()
+        rc = self._check(self.lib.rmc_successors(self.h, self._unpacked(state), out, stride, cap, keys, fps,
+                                                 ctypes.byref(cnt)))
+        if rc == RMC_ASSERT:
+            raise AssertionError("split brain")
+        res = []
+        for i in range(cnt.value):
+            k = keys[i]
+            st = unpacked_to_state(list(out[i * stride:(i + 1) * stride]), n, V)
+            res.append(((k >> 24, (k >> 16) & 0xFF, k & 0xFFFF), st, (fps[2 * i], fps[2 * i + 1])))
+        return res
+
+    def fingerprint(self, state: dict) -> Tuple[int, int]:
+        fp = (ctypes.c_uint64 * 2)()
+        self._check(self.lib.rmc_fingerprint(self.h, self._unpacked(state), fp))
+        return fp[0], fp[1]
+
+    def eval_invariant(self, state: dict, name: str) -> Optional[bool]:
+        """True / False, or None for a TLC evaluation error."""
+        bit = INVARIANT_BY_BIT.index("Inv" if name == "LeaderHasAllCommittedEntries" else name)
+        v = ctypes.c_int32()
+        rc = self.lib.rmc_eval_invariant(self.h, self._unpacked(state), bit, ctypes.byref(v))
+        if rc == RMC_EVAL_ERROR:
+            return None
+        self._check(rc)
+        return bool(v.value)

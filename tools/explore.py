@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Run one configuration level by level on the GPU and print TLC-style progress per level.
+
+usage: explore.py N V E R [--budget SECONDS] [--seeded] [--chunk G] [--seenlog2 K]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tla-raft_amd"))
+import raftmc  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("n", type=int)
+ap.add_argument("V", type=int)
+ap.add_argument("E", type=int)
+ap.add_argument("R", type=int)
+ap.add_argument("--budget", type=float, default=120)
+ap.add_argument("--seeded", action="store_true")
+ap.add_argument("--chunk", type=int, default=0)
+ap.add_argument("--seenlog2", type=int, default=0)
+ap.add_argument("--json", default="")
+a = ap.parse_args()
+cfg = raftmc.ModelConfig(n_servers=a.n, n_vals=a.V, max_election=a.E, max_restart=a.R,
+                         spec_variant=raftmc.SPEC_SEEDED if a.seeded else raftmc.SPEC_RAFT,
+                         chunk_successors=a.chunk, seen_log2=a.seenlog2)
+t0 = time.time()
+mc = raftmc.ModelChecker(cfg)
+print(f"create {time.time() - t0:.2f}s", flush=True)
+ls = mc.init()
+t1 = time.time()
+rows = []
+while ls.status == "ok" and time.time() - t1 < a.budget:
+    ls = mc.step()
+    el = time.time() - t1
+    ms = " ".join(f"{x:.1f}" for x in ls.kernel_ms)
+    print(f"L{ls.level:3d} F={ls.expanded:>11d} G={ls.generated:>12d} N={ls.new_states:>11d} "
+          f"tot={ls.total_distinct:>12d} {ls.seconds * 1e3:9.1f}ms [{ms}] el={el:.1f}s "
+          f"{ls.total_distinct / el:.3e} ds/s", flush=True)
+    rows.append(ls.__dict__)
+r = mc.result()
+print("RESULT", r.status, "generated", r.generated, "distinct", r.distinct, "depth", r.depth,
+      "seconds", round(r.seconds, 3), flush=True)
+if a.json:
+    with open(a.json, "w") as f:
+        json.dump(dict(result=r.__dict__ | {"levels": None}, levels=rows), f)
