@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""bench.py -- distinct states/sec of the MI355X model checker on BASELINE.json's workload.
+
+One "step" = one complete breadth-first exhaustion of the workload's state space from
+Init (TLC's whole myrun.sh run, minus JVM start-up): successor generation, symmetry +
+VIEW fingerprinting, seen-set dedup in TLC -workers 1 order, invariant checks.  The
+state space starts empty and every step re-explores it (rmc_reset keeps only device
+buffers; inputs = the compiled spec tables, resident in HBM).
+
+Workload at N=1: BASELINE.json configs[1] ("3 servers, 1 value, MaxTerm=2, MaxLogLen=2 on
+one MI355X") = Raft.tla with Servers={s1,s2,s3}, Vals={v1}, MaxElection=2, MaxRestart=3,
+SYMMETRY symmServers, VIEW view, INVARIANT Inv, -deadlock (MaxTerm is
+MaxElection, MaxLogLen is |Vals|+1).  configs[2]/[3] (Raft.cfg as shipped, 5 servers) do
+not fit one GPU (>2.1e9 states by BFS level 37, still growing).
+
+N>1 (torchrun, one process per GPU): each rank exhausts its own copy of the workload
+(replicas: the sharded seen-set exchange is not in this build), value = all ranks'
+distinct states / max-over-ranks time, scaling "weak".
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tla-raft_amd"))
+
+WORKLOADS = {
+    "c2": dict(n=3, V=1, E=2, R=3, desc="BASELINE configs[1]: Raft.tla, 3 servers, 1 value, MaxElection(=MaxTerm)=2, "
+                                         "MaxRestart=3, MaxLogLen=2, SYMMETRY+VIEW, INVARIANT Inv, -deadlock"),
+    "n3v2e2": dict(n=3, V=2, E=2, R=3, desc="Raft.tla, 3 servers, 2 values, MaxElection=2, MaxRestart=3 "
+                                             "(18.5M states; between configs[1] and configs[2])"),
+}
+
+# HBM peak from /opt/skills/guides/MI355X_MICROARCH.md (spec 8.0 TB/s)
+HBM_PEAK_GBS = 8000.0
+PHASES = ["expand_count", "expand_hash", "dedup", "materialize", "exchange", "other"]
+
+
+def alg_bytes(phase, F, G, N, S):
+    """Algorithmic HBM bytes of one phase (DESIGN.md "Roofline"): F parents of S-byte records,
+    G generated successors, N new states."""
+    if phase == "expand_count":
+        return F * S + F * 4                    # read parent records, write per-parent counts
+    if phase == "expand_hash":
+        return F * S + G * 16                   # read parent records, write one 128-bit fingerprint per successor
+    if phase == "dedup":
+        return G * (16 + 16 + 4) + G * (4 + 8 + 4) + G * 8   # fp + seen-set probe + slot; winner flag; scan
+    if phase == "materialize":
+        return F * S + G * 8 + N * (16 + S + 16 + 10)       # parents, flags; per new state: fp, record, seen insert, trace
+    return 0
+
+
+def cpu_baseline(w, budget_s=12.0):
+    """The C restatement (oracle/raft_oracle.c, single thread) on the same workload."""
+    so = os.path.join(ROOT, "oracle", "build", "libraft_oracle.so")
+    if not os.path.exists(so):
+        return None
+    lib = ctypes.CDLL(so)
+    lib.orc_create.restype = ctypes.c_void_p
+    lib.orc_create.argtypes = [ctypes.c_int] * 6 + [ctypes.c_uint32, ctypes.c_int]
+    lib.orc_run.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+    lib.orc_distinct.restype = ctypes.c_uint64
+    lib.orc_distinct.argtypes = [ctypes.c_void_p]
+    lib.orc_destroy.argtypes = [ctypes.c_void_p]
+    runs, states = 0, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        h = lib.orc_create(w["n"], w["V"], w["E"], w["R"], 0, 0, 1, 0)
+        lib.orc_run(h, 0)
+        states += lib.orc_distinct(h)
+        lib.orc_destroy(h)
+        runs += 1
+    dt = time.perf_counter() - t0
+    return {"value": states / dt, "unit": "distinct states/s", "cores": 1, "kind": "port",
+            "sample": f"{runs} full exhaustions of the same workload by oracle/raft_oracle.c "
+                      f"(C restatement of Raft.tla + TLC -workers 1 BFS, exact canonical forms; not TLC: "
+                      f"no JVM/tla2tools.jar on the box), {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")  # control plane only: barriers and the max-over-ranks time
+    torch.cuda.set_device(local)
+
+    import raftmc
+    w = WORKLOADS[args.workload]
+    cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
+                             invariants=("Inv",), check_deadlock=False, device=local)
+    mc = raftmc.ModelChecker(cfg)
+    res = None
+    for _ in range(args.warmup):
+        mc.reset()
+        res = mc.run()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    phase_ms = [0.0] * 6
+    launches = [0] * 6
+    Fs = Gs = Ns = 0
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        mc.reset()
+        res = mc.run()
+        for ls in res.levels:
+            for i in range(6):
+                phase_ms[i] += ls.kernel_ms[i]
+                launches[i] += ls.kernel_launches[i]
+            Fs += ls.expanded
+            Gs += ls.generated
+            Ns += ls.new_states
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert res is not None and res.status == "done", res
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * res.distinct * args.steps / elapsed
+
+    # dominant kernel phase: the one with the most device time (HIP events on the engine's stream)
+    S = record_bytes(mc)
+    dom = max(range(4), key=lambda i: phase_ms[i])
+    per_launch_ms = phase_ms[dom] / max(1, launches[dom])
+    bytes_total = alg_bytes(PHASES[dom], Fs, Gs, Ns, S)
+    achieved = bytes_total / max(1, launches[dom]) / (per_launch_ms / 1e3) / 1e9 if per_launch_ms > 0 else 0.0
+    roof = {"bound": "hbm", "kernel": PHASES[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "avg_launch_ms": round(per_launch_ms, 5), "launches": launches[dom],
+            "phase_ms_per_step": {PHASES[i]: round(phase_ms[i] / args.steps, 4) for i in range(4)}}
+    line = {
+        "metric": "distinct states/sec (whole node) + wall-time to exhaust",
+        "value": round(value, 1),
+        "unit": "distinct states/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: the state space of Raft.tla itself, generated from Init on the GPU each step",
+        "config": {"workload": w["desc"], "distinct_states": res.distinct, "states_generated": res.generated,
+                   "depth": res.depth, "verdict": "Inv holds" if res.status == "done" else res.status,
+                   "parallelism": "replicas" if world > 1 else "single-gpu"},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(w)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    mc.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def record_bytes(mc):
+    """Bytes of one packed state record (core words + message-id list), rmc_spec.h Layout."""
+    n = mc.cfg.n_servers
+    cw = (7 + 3 * n + 3) // 4 * 4
+    mcap = mc.cfg.msg_cap or (64 if n <= 3 else 128)
+    return cw * 4 + 2 * mcap
+
+
+if __name__ == "__main__":
+    main()

@@ -126,6 +126,10 @@ int rmc_init(void *ctx, rmc_level_stats *st);
  * on new states (Raft.cfg:33).  Returns RMC_OK, RMC_DONE or an error status. */
 int rmc_step(void *ctx, rmc_level_stats *st);
 
+/* Forget every explored state (seen set, levels, trace) but keep the device
+ * buffers, so the next rmc_init starts a fresh run (TLC: a new invocation). */
+int rmc_reset(void *ctx);
+
 /* Loop rmc_step until done or an error; fills the final result. */
 int rmc_run(void *ctx, rmc_result *res);
 int rmc_get_result(void *ctx, rmc_result *res);

@@ -159,8 +159,15 @@ struct rmc_ctx {
 
     // chunk buffers
     uint64_t chunk_parents = 0, Gcap = 0;
-    uint32_t *d_cnt = nullptr, *d_off = nullptr, *d_lslot = nullptr, *d_L = nullptr, *d_wflag = nullptr,
-             *d_wpos = nullptr;
+    uint32_t *d_cnt = nullptr, *d_off = nullptr, *d_lslot = nullptr, *d_wflag = nullptr, *d_wpos = nullptr;
+    unsigned long long *d_L = nullptr;  // chunk dedup table, (epoch << 32) | j
+    uint64_t Lcap_max = 0;
+    uint32_t epoch = 0;
+    unsigned long long *d_sum = nullptr, *h_sum = nullptr;  // per-chunk summary (G, W, errors, flags)
+    std::vector<hipEvent_t> evpool;
+    struct EvRec { int ph; int a, b; };
+    std::vector<EvRec> evrecs;
+    int evused = 0;
     ulonglong2 *d_fp = nullptr;
     void *d_tmp = nullptr;
     size_t tmp_bytes = 0;
@@ -418,15 +425,21 @@ struct rmc_ctx {
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 31)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^31");
         chunk_parents = Gcap / ks.maxsucc;
-        d_cnt = dmalloc<uint32_t>(chunk_parents);
+        d_cnt = dmalloc<uint32_t>(chunk_parents + 1);
         d_off = dmalloc<uint32_t>(chunk_parents + 1);
         d_fp = dmalloc<ulonglong2>(Gcap);
         d_lslot = dmalloc<uint32_t>(Gcap);
-        d_wflag = dmalloc<uint32_t>(Gcap);
+        d_wflag = dmalloc<uint32_t>(Gcap + 1);
+        HIPCHK(hipMemsetAsync(d_cnt, 0, (chunk_parents + 1) * 4, stream));
+        HIPCHK(hipMemsetAsync(d_wflag, 0, (Gcap + 1) * 4, stream));
         d_wpos = dmalloc<uint32_t>(Gcap + 1);
-        d_L = dmalloc<uint32_t>(next_pow2(2 * Gcap));
+        Lcap_max = next_pow2(2 * Gcap);
+        d_L = dmalloc<unsigned long long>(Lcap_max);
+        HIPCHK(hipMemsetAsync(d_L, 0, Lcap_max * 8, stream));
+        d_sum = dmalloc<unsigned long long>(16);
+        HIPCHK(hipHostMalloc((void **)&h_sum, 16 * 8, hipHostMallocDefault));
         size_t t1 = 0;
-        HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, t1, d_cnt, d_off + 1, (int)Gcap, stream));
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, d_cnt, d_off, (int)Gcap + 1, stream));
         tmp_bytes = t1;
         d_tmp = dmalloc<uint8_t>(tmp_bytes);
 
@@ -463,6 +476,11 @@ struct rmc_ctx {
         dfree(d_cur); dfree(d_nxt); dfree(d_cnt); dfree(d_off); dfree(d_fp); dfree(d_lslot); dfree(d_wflag);
         dfree(d_wpos); dfree(d_L); dfree(d_tmp); dfree(d_T); dfree(d_par); dfree(d_pslot); dfree(d_err);
         dfree(d_flags); dfree(d_one); dfree(d_out); dfree(d_keys); dfree(d_cnt1); dfree(d_fp1); dfree(d_inv);
+        dfree(d_sum);
+        if (h_sum) (void)hipHostFree(h_sum);
+        h_sum = nullptr;
+        for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
+        evpool.clear();
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (stream) (void)hipStreamDestroy(stream);
@@ -509,17 +527,36 @@ struct rmc_ctx {
         T_cap = nc;
     }
 
+    // Phase timing by event pairs on the engine's stream, read back at the next sync
+    // point (no extra synchronisation inside a level).
+    int ev() {
+        if (evused == (int)evpool.size()) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            evpool.push_back(e);
+        }
+        return evused++;
+    }
     template <class F>
-    void timed(rmc_level_stats *st, int ph, F &&f) {
-        if (!st) { f(); return; }
-        HIPCHK(hipEventRecord(ev0, stream));
+    void timed(int ph, F &&f) {
+        const int a = ev();
+        HIPCHK(hipEventRecord(evpool[a], stream));
         f();
-        HIPCHK(hipEventRecord(ev1, stream));
-        HIPCHK(hipEventSynchronize(ev1));
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, ev0, ev1));
-        st->kernel_ms[ph] += ms;
-        st->kernel_launches[ph] += 1;
+        const int b = ev();
+        HIPCHK(hipEventRecord(evpool[b], stream));
+        evrecs.push_back({ph, a, b});
+    }
+    void collect_times(rmc_level_stats *st) {  // call after a stream sync
+        for (const EvRec &r : evrecs) {
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, evpool[r.a], evpool[r.b]));
+            if (st) {
+                st->kernel_ms[r.ph] += ms;
+                st->kernel_launches[r.ph] += 1;
+            }
+        }
+        evrecs.clear();
+        evused = 0;
     }
 
     template <class T>
@@ -631,61 +668,53 @@ struct rmc_ctx {
         const uint64_t gid_cur = level_start[L - 1];
         const uint64_t gid_nxt = gid_cur + cur_n;
         uint64_t nxt_n = 0, level_gen = 0;
-        reset_errors();
         for (uint64_t p0 = 0; p0 < cur_n; p0 += chunk_parents) {
             const uint64_t p1 = std::min(cur_n, p0 + chunk_parents), np_ = p1 - p0;
-            KParams P = base();
-            P.front = d_cur;
-            P.p_begin = p0;
-            P.p_end = p1;
-            P.cnt = d_cnt;
-            P.off = d_off;
-            P.fp = d_fp;
-            P.wflag = d_wflag;
-            P.wpos = d_wpos;
-            P.next = d_nxt;
-            P.next_base = nxt_n;
-            P.gid_next_base = gid_nxt;
-            P.gid_parent_base = gid_cur;
-            timed(st, PH_COUNT, [&] {
-                ks.count(P, stream);
-                HIPCHK(hipMemsetAsync(d_off, 0, 4, stream));
-                HIPCHK(hipcub::DeviceScan::InclusiveSum(d_tmp, tmp_bytes, d_cnt, d_off + 1, (int)np_, stream));
+            auto params = [&] {
+                KParams Q = base();
+                Q.front = d_cur; Q.p_begin = p0; Q.p_end = p1; Q.cnt = d_cnt; Q.off = d_off; Q.fp = d_fp;
+                Q.wflag = d_wflag; Q.wpos = d_wpos; Q.next = d_nxt; Q.next_base = nxt_n;
+                Q.gid_next_base = gid_nxt; Q.gid_parent_base = gid_cur;
+                return Q;
+            };
+            const uint32_t *Gp = d_off + np_;  // device-side successor count of the chunk
+            timed(PH_COUNT, [&] {
+                ks.count(params(), stream);
+                // exclusive scan over np_+1 items: off[np_] = G (cnt[np_] is never read into it)
+                HIPCHK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, d_cnt, d_off, (int)np_ + 1, stream));
             });
-            const uint32_t G = d2h(d_off + np_);
-            uint32_t fl[4];
-            HIPCHK(hipMemcpy(fl, d_flags, sizeof fl, hipMemcpyDeviceToHost));
-            if (fl[0]) throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
-            level_gen += G;
-            uint32_t W = 0;
-            if (G) {
-                timed(st, PH_HASH, [&] { ks.hash(P, stream); });
-                const uint64_t Lcap = next_pow2(2ull * G);
-                timed(st, PH_DEDUP, [&] {
-                    HIPCHK(hipMemsetAsync(d_L, 0xFF, Lcap * 4, stream));
-                    launch_dedup(d_fp, G, d_T, T_cap - 1, d_L, Lcap - 1, d_lslot, stream);
-                    launch_winflag(d_lslot, d_L, G, d_wflag, stream);
-                    HIPCHK(hipMemsetAsync(d_wpos, 0, 4, stream));
-                    HIPCHK(hipcub::DeviceScan::InclusiveSum(d_tmp, tmp_bytes, d_wflag, d_wpos + 1, (int)G, stream));
-                });
-                W = d2h(d_wpos + G);
-                grow_records(d_nxt, nxt_cap, nxt_n, nxt_n + W);
-                grow_trace(gid_nxt + nxt_n + W);
-                grow_seen(T_count + W);
-                P = [&] {
-                    KParams Q = base();
-                    Q.front = d_cur; Q.p_begin = p0; Q.p_end = p1; Q.cnt = d_cnt; Q.off = d_off; Q.fp = d_fp;
-                    Q.wflag = d_wflag; Q.wpos = d_wpos; Q.next = d_nxt; Q.next_base = nxt_n;
-                    Q.gid_next_base = gid_nxt; Q.gid_parent_base = gid_cur;
-                    return Q;
-                }();
-                timed(st, PH_MAT, [&] { ks.materialize(P, stream); });
-                T_count += W;
+            // Small chunks run on an upper bound of G without a host round trip; large
+            // ones read G back so that the dedup/scan passes are sized exactly.
+            uint64_t Gub = np_ * (uint64_t)ks.maxsucc;
+            if (Gub > (1ull << 20)) {
+                Gub = d2h(Gp);
+                collect_times(st);
             }
-            HIPCHK(hipGetLastError());
-            unsigned long long e[ERR_NSLOTS];
-            HIPCHK(hipMemcpyAsync(e, d_err, sizeof e, hipMemcpyDeviceToHost, stream));
+            grow_records(d_nxt, nxt_cap, nxt_n, nxt_n + Gub);
+            grow_trace(gid_nxt + nxt_n + Gub);
+            grow_seen(T_count + Gub);
+            if (Gub) {
+                timed(PH_HASH, [&] { ks.hash(params(), stream); });
+                uint64_t Lcap = next_pow2(2 * Gub);
+                if (Lcap > Lcap_max) Lcap = Lcap_max;
+                ++epoch;
+                timed(PH_DEDUP, [&] {
+                    launch_dedup(d_fp, Gp, Gub, d_T, T_cap - 1, d_L, Lcap - 1, epoch, d_lslot, stream);
+                    launch_winflag(d_lslot, d_L, Gp, Gub, d_wflag, stream);
+                    HIPCHK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, d_wflag, d_wpos, (int)Gub + 1, stream));
+                });
+                timed(PH_MAT, [&] { ks.materialize(params(), stream); });
+            }
+            launch_summary(Gp, d_wpos, d_err, d_flags, d_sum, stream);
+            HIPCHK(hipMemcpyAsync(h_sum, d_sum, 8 * 8, hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
+            HIPCHK(hipGetLastError());
+            collect_times(st);
+            const uint64_t G = h_sum[0], W = Gub ? h_sum[1] : 0;
+            if (h_sum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
+            const unsigned long long *e = h_sum + 2;
+            level_gen += G;
+            T_count += W;
             int kind = -1;
             unsigned long long best = ~0ull;
             // TLC order: smaller (parent, slot) first; on a tie the Assert wins (its action's batch is discarded)
@@ -808,6 +837,23 @@ struct rmc_ctx {
         }
     }
 
+    // Forget every explored state but keep all device buffers (repeat runs, benchmarks).
+    void reset() {
+        HIPCHK(hipMemsetAsync(d_T, 0, T_cap * 16, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        T_count = 0;
+        cur_n = 0;
+        level_start.clear();
+        trace.clear();
+        inited = finished = false;
+        status = RMC_OK;
+        depth = 0;
+        total_generated = total_distinct = queue_at_end = 0;
+        violated = -1;
+        err_gid = 0;
+        seconds = 0;
+    }
+
     void result(rmc_result *r) const {
         std::memset(r, 0, sizeof *r);
         r->status = finished ? status : RMC_OK;
@@ -882,6 +928,14 @@ int rmc_run(void *ctx, rmc_result *res) {
         (void)rc;
         if (res) c->result(res);
         return c->status;
+    });
+}
+
+int rmc_reset(void *ctx) {
+    rmc_ctx *c = (rmc_ctx *)ctx;
+    return guarded(c, [&] {
+        c->reset();
+        return RMC_OK;
     });
 }
 

@@ -67,9 +67,12 @@ struct KernelSet {
 bool get_kernels(int N, int V, int msg_cap, KernelSet *ks);
 
 // generic (template-free) kernels
-void launch_dedup(const ulonglong2 *fp, uint64_t G, const ulonglong2 *T, uint64_t Tmask, uint32_t *L, uint64_t Lmask,
-                  uint32_t *lslot, hipStream_t s);
-void launch_winflag(const uint32_t *lslot, const uint32_t *L, uint64_t G, uint32_t *wflag, hipStream_t s);
+void launch_dedup(const ulonglong2 *fp, const uint32_t *Gp, uint64_t Gub, const ulonglong2 *T, uint64_t Tmask,
+                  unsigned long long *L, uint64_t Lmask, uint32_t epoch, uint32_t *lslot, hipStream_t s);
+void launch_winflag(const uint32_t *lslot, const unsigned long long *L, const uint32_t *Gp, uint64_t Gub,
+                    uint32_t *wflag, hipStream_t s);
+void launch_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned long long *err, const uint32_t *flags,
+                    unsigned long long *out, hipStream_t s);
 void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, ulonglong2 *Tnew, uint64_t new_mask, hipStream_t s);
 void launch_insert_fps(const ulonglong2 *fp, uint64_t n, ulonglong2 *T, uint64_t Tmask, hipStream_t s);
 

@@ -59,6 +59,7 @@ struct Succ {
     uint32_t nadd;
     uint32_t key;  // KEY_NONE = disabled
     uint32_t s;    // acting server (row of the structured hash that changed)
+    uint32_t lw, mirow, nirow;  // logs[s], matchIndex[s][*], nextIndex[s][*] of the successor
 };
 
 // ---- log helpers (logs[i][x], tla:97, 1-based) ---------------------------------------
@@ -233,6 +234,23 @@ __device__ __forceinline__ ulonglong2 fingerprint(const uint32_t *c, int srow, c
     return make_ulonglong2(b0 | 1ull, b1);
 }
 
+// Per-server and per-pair inputs of the structured hash, from the words of one row
+// (identical to what fingerprint() computes for row i).
+template <int N>
+__device__ __forceinline__ uint64_t own_word(uint32_t vfw, uint32_t ctw, uint32_t rolew, uint32_t ciw, uint32_t llw,
+                                             uint32_t lw, uint32_t mirow, uint32_t nirow, uint32_t i) {
+    const uint32_t vf = nib(vfw, i);
+    const uint32_t vrel = vf == VF_NONE ? 0u : (vf == i ? 1u : 2u);
+    const uint32_t own = vrel | (nib(ctw, i) << 2) | (nib(rolew, i) << 6) | (nib(ciw, i) << 10) |
+                         (nib(llw, i) << 14) | (nib(mirow, i) << 18) | (nib(nirow, i) << 22);
+    return ((uint64_t)lw << 32) | own;
+}
+__device__ __forceinline__ uint64_t pair_small(uint32_t mirow, uint32_t nirow, uint32_t vf_i, uint32_t j) {
+    return (uint64_t)(nib(mirow, j) | (nib(nirow, j) << 4) | ((vf_i == j) ? 256u : 0u));
+}
+
+constexpr int factorial(int n) { return n <= 1 ? 1 : n * factorial(n - 1); }
+
 // ---- expansion of one parent per wavefront ------------------------------------------------
 template <int N, int V, int MR>
 struct Wave {
@@ -263,6 +281,9 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
 #pragma unroll
     for (int w = 0; w < Lo::NW; w++) o.c[w] = W.c[w];
     o.s = s;
+    o.lw = W.lds[Lo::W_LOG + s];
+    o.mirow = W.lds[Lo::W_MI + s];
+    o.nirow = W.lds[Lo::W_NI + s];
     if (mt > ct) {  // UpdateTerm, first disjunct (tla:178-182)
         o.c[Lo::W_ROLE] = setnib(o.c[Lo::W_ROLE], s, FOL);
         o.c[Lo::W_CT] = setnib(o.c[Lo::W_CT], s, mt);
@@ -311,6 +332,7 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
                 if (ent) nlw |= eb << (8 * (nl - 2));
 #pragma unroll
                 for (int q = 0; q < N; q++) o.c[Lo::W_LOG + q] = ((uint32_t)q == s) ? nlw : o.c[Lo::W_LOG + q];
+                o.lw = nlw;
                 o.c[Lo::W_LL] = setnib(o.c[Lo::W_LL], s, nl);
             }
             if (!has_id(ids, W.nm, resp)) { o.add[0] = resp; o.nadd = 1; }
@@ -345,6 +367,8 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
             o.c[Lo::W_MI + q] = ((uint32_t)q == s) ? nmi : o.c[Lo::W_MI + q];
             o.c[Lo::W_NI + q] = ((uint32_t)q == s) ? nni : o.c[Lo::W_NI + q];
         }
+        o.mirow = nmi;
+        o.nirow = nni;
         o.c[Lo::W_PEND] = pend & ~(1u << pb);
         o.key = slot_key(s, HAR, k);
         return;
@@ -371,6 +395,9 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
 #pragma unroll
     for (int w = 0; w < Lo::NW; w++) o.c[w] = W.c[w];
     o.s = s;
+    o.lw = lw;
+    o.mirow = W.lds[Lo::W_MI + s];
+    o.nirow = W.lds[Lo::W_NI + s];
     if (t == 0) {  // BecomeCandidate tla:107-130
         const uint32_t ec = misc & 15u;
         if (!((int)ec < P.E)) return;
@@ -410,6 +437,8 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
             o.c[Lo::W_MI + q] = ((uint32_t)q == s) ? mirow : o.c[Lo::W_MI + q];
             o.c[Lo::W_NI + q] = ((uint32_t)q == s) ? nirow : o.c[Lo::W_NI + q];
         }
+        o.mirow = mirow;
+        o.nirow = nirow;
         o.c[Lo::W_PEND] = W.c[Lo::W_PEND] & ~(((1u << N) - 1u) << (s * N));
         o.c[Lo::W_ROLE] = setnib(o.c[Lo::W_ROLE], s, LEA);
         o.key = slot_key(s, BL, 0);
@@ -427,6 +456,8 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
             o.c[Lo::W_LOG + q] = ((uint32_t)q == s) ? nlw : o.c[Lo::W_LOG + q];
             o.c[Lo::W_MI + q] = ((uint32_t)q == s) ? mirow : o.c[Lo::W_MI + q];
         }
+        o.lw = nlw;
+        o.mirow = mirow;
         o.c[Lo::W_LL] = setnib(o.c[Lo::W_LL], s, ll + 1);
         o.key = slot_key(s, CR, v);
         return;
@@ -600,7 +631,26 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
     __shared__ uint16_t ids[S::MCAP];
     __shared__ uint64_t M0[N * N], M1[N * N];
     __shared__ uint32_t pcore[Lo::NW + N];
+    constexpr int NPM = SUMS ? factorial(N) : 1;        // |Permutations(Servers)| (tla:21)
+    constexpr int MAXS = SUMS ? S::MCAP + N * S::SLOTS_PER_SERVER : 1;
+    __shared__ uint64_t Rt[2][NPM * N], Tt[2][NPM];     // parent row terms / totals per permutation
+    __shared__ uint64_t sdS[2][N], sdP[2][N * N];       // position seeds
+    __shared__ uint8_t pimg[NPM * N];                   // permutation images
+    __shared__ uint64_t sU[MAXS], sX[2][MAXS * N];      // compacted successor rows
+    __shared__ uint32_t sS[MAXS];
     const int lane = threadIdx.x;
+    if (SUMS) {
+        for (int i = lane; i < P.t.np * N; i += 64) pimg[i] = P.t.perms[(i / N) * MAXN + (i % N)];
+        if (lane < N) {
+            sdS[0][lane] = P.t.seeds[lane];
+            sdS[1][lane] = P.t.seeds[MAXN + MAXN * MAXN + lane];
+        }
+        if (lane < N * N) {
+            const int k = lane / N, l = lane % N;
+            sdP[0][lane] = P.t.seeds[MAXN + k * MAXN + l];
+            sdP[1][lane] = P.t.seeds[2 * MAXN + MAXN * MAXN + k * MAXN + l];
+        }
+    }
     for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
         const uint32_t *rec = P.front + p * (uint64_t)S::RECW;
         Wave<N, V, MR> W;
@@ -655,14 +705,87 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
             continue;
         }
         if (MODE == M_HASH || MODE == M_SINGLE) {
-            const uint64_t base = (MODE == M_HASH) ? P.off[pl] : 0;
+            // (a) parent row terms Rt[f][p][s] = Z_f(pi(s), U[s]) + sum_j Z_f(pi(s), pi(j), X_f[s][j])
+            //     and their per-permutation totals Tt[f][p]  (structured hash, rmc_spec.h)
+            const int np = P.t.np;
+            for (int idx = lane; idx < np * N; idx += 64) {
+                const int pp = idx / N;
+                const uint32_t sv = (uint32_t)(idx - pp * N);
+                const uint32_t imgs = pimg[idx];
+                const uint32_t mirow = pcore[Lo::W_MI + sv], nirow = pcore[Lo::W_NI + sv];
+                const uint64_t u = own_word<N>(W.c[Lo::W_VF], W.c[Lo::W_CT], W.c[Lo::W_ROLE], W.c[Lo::W_CI],
+                                               W.c[Lo::W_LL], pcore[Lo::W_LOG + sv], mirow, nirow, sv);
+                uint64_t r0 = mix64(u ^ sdS[0][imgs]), r1 = mix64(u ^ sdS[1][imgs]);
+                const uint32_t vfs = nib(W.c[Lo::W_VF], sv);
+#pragma unroll
+                for (int j = 0; j < N; j++) {
+                    if ((uint32_t)j == sv) continue;
+                    const uint64_t sm = pair_small(mirow, nirow, vfs, j);
+                    const uint32_t q = imgs * N + pimg[pp * N + j];
+                    r0 += mix64((M0[sv * N + j] ^ (sm * PAIR_K0)) ^ sdP[0][q]);
+                    r1 += mix64((M1[sv * N + j] ^ (sm * PAIR_K1)) ^ sdP[1][q]);
+                }
+                Rt[0][idx] = r0;
+                Rt[1][idx] = r1;
+            }
+            // (b) every enabled successor writes its acting row to LDS slot rank
 #pragma unroll
             for (int r = 0; r <= MR; r++) {
-                if (cand[r].key != KEY_NONE) {
-                    uint64_t row0[N], row1[N];
-                    succ_row<N, V, MR>(P, cand[r], M0, M1, row0, row1);
-                    P.fp[base + rank[r]] = fingerprint<N, V>(cand[r].c, (int)cand[r].s, row0, row1, M0, M1, P.t);
+                if (cand[r].key == KEY_NONE) continue;
+                const Succ<N, V, MR> &o = cand[r];
+                const uint32_t sl = rank[r];
+                uint64_t row0[N], row1[N];
+                succ_row<N, V, MR>(P, o, M0, M1, row0, row1);
+                const uint32_t vfs = nib(o.c[Lo::W_VF], o.s);
+                sU[sl] = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI], o.c[Lo::W_LL],
+                                     o.lw, o.mirow, o.nirow, o.s);
+#pragma unroll
+                for (int j = 0; j < N; j++) {
+                    const uint64_t sm = pair_small(o.mirow, o.nirow, vfs, j);
+                    sX[0][sl * N + j] = row0[j] ^ (sm * PAIR_K0);
+                    sX[1][sl * N + j] = row1[j] ^ (sm * PAIR_K1);
                 }
+                sS[sl] = o.s;
+            }
+            __syncthreads();
+            for (int pp = lane; pp < np; pp += 64) {
+                uint64_t t0 = 0, t1 = 0;
+#pragma unroll
+                for (int q = 0; q < N; q++) { t0 += Rt[0][pp * N + q]; t1 += Rt[1][pp * N + q]; }
+                Tt[0][pp] = t0;
+                Tt[1][pp] = t1;
+            }
+            __syncthreads();
+            // (c) one lane per successor: min over permutations of (parent total - old row + new row)
+            const uint64_t base = (MODE == M_HASH) ? P.off[pl] : 0;
+            for (uint32_t b = 0; b < total; b += 64) {
+                const uint32_t l = b + lane;
+                if (l >= total) break;
+                const uint32_t sv = sS[l];
+                const uint64_t u = sU[l];
+                uint64_t x0[N], x1[N];
+#pragma unroll
+                for (int j = 0; j < N; j++) { x0[j] = sX[0][l * N + j]; x1[j] = sX[1][l * N + j]; }
+                uint64_t b0 = ~0ull, b1 = ~0ull;
+                for (int pp = 0; pp < np; pp++) {
+                    uint32_t img[N];
+#pragma unroll
+                    for (int j = 0; j < N; j++) img[j] = pimg[pp * N + j];
+                    uint32_t imgs = img[0];
+#pragma unroll
+                    for (int j = 1; j < N; j++) imgs = ((uint32_t)j == sv) ? img[j] : imgs;
+                    uint64_t h0 = Tt[0][pp] - Rt[0][pp * N + sv] + mix64(u ^ sdS[0][imgs]);
+                    uint64_t h1 = Tt[1][pp] - Rt[1][pp * N + sv] + mix64(u ^ sdS[1][imgs]);
+#pragma unroll
+                    for (int j = 0; j < N; j++) {
+                        if ((uint32_t)j == sv) continue;
+                        const uint32_t q = imgs * N + img[j];
+                        h0 += mix64(x0[j] ^ sdP[0][q]);
+                        h1 += mix64(x1[j] ^ sdP[1][q]);
+                    }
+                    if (h1 < b1 || (h1 == b1 && h0 < b0)) { b1 = h1; b0 = h0; }
+                }
+                P.fp[base + l] = make_ulonglong2(b0 | 1ull, b1);
             }
         }
         if (MODE == M_HASH) continue;
@@ -794,9 +917,15 @@ bool get_kernels(int N, int V, int msg_cap, KernelSet *ks) {
 // Probe the global seen set T (read-only in this launch) and, for fingerprints not in
 // it, elect the first successor in TLC order per fingerprint in the chunk table L
 // (slots hold chunk-local successor indices; index order == TLC order).
-__global__ __launch_bounds__(256) void k_dedup(const ulonglong2 *__restrict__ fp, uint64_t G,
-                                               const ulonglong2 *__restrict__ T, uint64_t Tmask, uint32_t *L,
-                                               uint64_t Lmask, uint32_t *lslot) {
+__global__ __launch_bounds__(256) void k_dedup(const ulonglong2 *__restrict__ fp, const uint32_t *__restrict__ Gp,
+                                               const ulonglong2 *__restrict__ T, uint64_t Tmask,
+                                               unsigned long long *L, uint64_t Lmask, uint32_t epoch,
+                                               uint32_t *lslot) {
+    // L slots hold (epoch << 32) | j; a slot whose epoch is not this chunk's is empty, so
+    // the table never needs clearing.  atomicMin on the packed word keeps the smallest j
+    // (= first in TLC order) per fingerprint.
+    const uint64_t G = *Gp;
+    const unsigned long long tag = (unsigned long long)epoch << 32;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < G; j += (uint64_t)gridDim.x * blockDim.x) {
         const ulonglong2 f = fp[j];
         uint64_t h = t_index(f, Tmask);
@@ -809,27 +938,56 @@ __global__ __launch_bounds__(256) void k_dedup(const ulonglong2 *__restrict__ fp
         }
         if (old) { lslot[j] = 0xFFFFFFFFu; continue; }
         uint64_t g = (f.x ^ (f.x >> 31) ^ (f.y >> 7)) & Lmask;
+        const unsigned long long mine = tag | (unsigned long long)j;
         for (;;) {
-            uint32_t v = __hip_atomic_load(&L[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (v == 0xFFFFFFFFu) {
-                const uint32_t prev = atomicCAS(&L[g], 0xFFFFFFFFu, (uint32_t)j);
-                if (prev == 0xFFFFFFFFu) break;
+            unsigned long long v = __hip_atomic_load(&L[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((v >> 32) != epoch) {
+                const unsigned long long prev = atomicCAS(&L[g], v, mine);
+                if (prev == v) break;
                 v = prev;
             }
-            const ulonglong2 o = fp[v];
-            if (o.x == f.x && o.y == f.y) { atomicMin(&L[g], (uint32_t)j); break; }
+            if ((v >> 32) == epoch) {
+                const ulonglong2 o = fp[(uint32_t)v];
+                if (o.x == f.x && o.y == f.y) { atomicMin(&L[g], mine); break; }
+            }
             g = (g + 1) & Lmask;
         }
         lslot[j] = (uint32_t)g;
     }
 }
 
-__global__ __launch_bounds__(256) void k_winflag(const uint32_t *__restrict__ lslot, const uint32_t *__restrict__ L,
-                                                 uint64_t G, uint32_t *__restrict__ w) {
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < G; j += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t g = lslot[j];
-        w[j] = (g != 0xFFFFFFFFu && L[g] == (uint32_t)j) ? 1u : 0u;
+__global__ __launch_bounds__(256) void k_winflag(const uint32_t *__restrict__ lslot,
+                                                 const unsigned long long *__restrict__ L,
+                                                 const uint32_t *__restrict__ Gp, uint64_t Gub,
+                                                 uint32_t *__restrict__ w) {
+    const uint64_t G = *Gp;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < Gub;
+         j += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t win = 0;
+        if (j < G) {
+            const uint32_t g = lslot[j];
+            win = (g != 0xFFFFFFFFu && (uint32_t)L[g] == (uint32_t)j) ? 1u : 0u;
+        }
+        w[j] = win;
     }
+}
+
+// one copy-back per chunk: G, W, error keys, flags
+__global__ void k_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned long long *err,
+                          const uint32_t *flags, unsigned long long *out) {
+    if (threadIdx.x == 0) {
+        const uint32_t G = *Gp;
+        out[0] = G;
+        out[1] = wpos[G];
+        for (int i = 0; i < ERR_NSLOTS; i++) out[2 + i] = err[i];
+        out[2 + ERR_NSLOTS] = flags[0];
+    }
+}
+
+// reset the error words for the next chunk (after k_summary has copied them)
+__global__ void k_clear_err(unsigned long long *err, uint32_t *flags) {
+    if (threadIdx.x < ERR_NSLOTS) err[threadIdx.x] = ~0ull;
+    if (threadIdx.x == 0) flags[0] = 0;
 }
 
 __global__ __launch_bounds__(256) void k_rehash(const ulonglong2 *__restrict__ Told, uint64_t old_cap, ulonglong2 *Tn,
@@ -852,12 +1010,19 @@ static inline unsigned grid256(uint64_t n) {
     return (unsigned)(b < cap ? (b ? b : 1) : cap);
 }
 
-void launch_dedup(const ulonglong2 *fp, uint64_t G, const ulonglong2 *T, uint64_t Tmask, uint32_t *L, uint64_t Lmask,
-                  uint32_t *lslot, hipStream_t s) {
-    hipLaunchKernelGGL(k_dedup, dim3(grid256(G)), dim3(256), 0, s, fp, G, T, Tmask, L, Lmask, lslot);
+void launch_dedup(const ulonglong2 *fp, const uint32_t *Gp, uint64_t Gub, const ulonglong2 *T, uint64_t Tmask,
+                  unsigned long long *L, uint64_t Lmask, uint32_t epoch, uint32_t *lslot, hipStream_t s) {
+    hipLaunchKernelGGL(k_dedup, dim3(grid256(Gub)), dim3(256), 0, s, fp, Gp, T, Tmask, L, Lmask, epoch, lslot);
 }
-void launch_winflag(const uint32_t *lslot, const uint32_t *L, uint64_t G, uint32_t *wflag, hipStream_t s) {
-    hipLaunchKernelGGL(k_winflag, dim3(grid256(G)), dim3(256), 0, s, lslot, L, G, wflag);
+void launch_winflag(const uint32_t *lslot, const unsigned long long *L, const uint32_t *Gp, uint64_t Gub,
+                    uint32_t *wflag, hipStream_t s) {
+    hipLaunchKernelGGL(k_winflag, dim3(grid256(Gub)), dim3(256), 0, s, lslot, L, Gp, Gub, wflag);
+}
+void launch_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned long long *err, const uint32_t *flags,
+                    unsigned long long *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_summary, dim3(1), dim3(64), 0, s, Gp, wpos, err, flags, out);
+    hipLaunchKernelGGL(k_clear_err, dim3(1), dim3(64), 0, s, const_cast<unsigned long long *>(err),
+                       const_cast<uint32_t *>(flags));
 }
 void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, ulonglong2 *Tnew, uint64_t new_mask, hipStream_t s) {
     hipLaunchKernelGGL(k_rehash, dim3(grid256(old_cap)), dim3(256), 0, s, Told, old_cap, Tnew, new_mask);

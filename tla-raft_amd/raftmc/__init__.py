@@ -85,6 +85,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.rmc_init.argtypes = [vp, P(_LevelStats)]
     lib.rmc_step.argtypes = [vp, P(_LevelStats)]
     lib.rmc_run.argtypes = [vp, P(_Result)]
+    lib.rmc_reset.argtypes = [vp]
     lib.rmc_get_result.argtypes = [vp, P(_Result)]
     lib.rmc_trace_len.argtypes = [vp, P(u32)]
     lib.rmc_trace_state.argtypes = [vp, u32, P(i32), ctypes.c_size_t, P(i32), P(i32), P(i32)]
@@ -244,6 +245,7 @@ class LevelStats:
     queue: int
     seconds: float
     kernel_ms: List[float] = field(default_factory=list)
+    kernel_launches: List[int] = field(default_factory=list)
 
 
 @dataclass
@@ -300,7 +302,7 @@ class ModelChecker:
     def _stats(s: _LevelStats) -> LevelStats:
         return LevelStats(s.level, STATUS_NAMES.get(s.status, str(s.status)), s.expanded, s.generated,
                           s.new_states, s.total_generated, s.total_distinct, s.queue, s.seconds,
-                          list(s.kernel_ms))
+                          list(s.kernel_ms), list(s.kernel_launches))
 
     def init(self) -> LevelStats:
         st = _LevelStats()
@@ -309,6 +311,12 @@ class ModelChecker:
         ls = self._stats(st)
         self.levels.append(ls)
         return ls
+
+    def reset(self) -> None:
+        """Start over from Init on the next run(), keeping the device buffers."""
+        self._check(self.lib.rmc_reset(self.h))
+        self.levels = []
+        self._inited = False
 
     def step(self) -> LevelStats:
         st = _LevelStats()
