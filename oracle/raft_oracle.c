@@ -62,6 +62,8 @@ typedef struct {
     int check_deadlock; /* 0 = -deadlock (run:3) */
     uint32_t inv_mask;  /* bit I_* : checked invariants, in bit order */
     int record_trace;
+    int order;          /* 0 = TLC -workers 1 order; 1 = reversed; 2 = seeded shuffle (order-sensitivity probe) */
+    uint64_t seed;
 } ocfg_t;
 
 typedef struct {
@@ -682,6 +684,12 @@ void *orc_create(int n, int V, int E, int R, int seeded, int check_deadlock, uin
     return O;
 }
 
+void orc_set_order(void *h, int order, uint64_t seed) {
+    orc_t *O = (orc_t *)h;
+    O->c.order = order;
+    O->c.seed = seed;
+}
+
 void orc_destroy(void *h) {
     orc_t *O = (orc_t *)h;
     if (!O) return;
@@ -727,8 +735,20 @@ int orc_run(void *h, uint64_t max_states) {
     for (int lvl = 1; cur.n > 0; lvl++) {
         if (lvl >= MAXLEVELS) { O->verdict = V_CAPACITY; goto done; }
         uint64_t nxt_base = O->distinct;
+        uint64_t *perm = NULL;
+        if (c->order) {  /* order-sensitivity probe: visit this level's states in another order */
+            perm = (uint64_t *)malloc(cur.n * sizeof(uint64_t));
+            for (uint64_t i = 0; i < cur.n; i++) perm[i] = c->order == 1 ? cur.n - 1 - i : i;
+            if (c->order == 2) {
+                uint64_t x = c->seed + (uint64_t)lvl * 0x9e3779b97f4a7c15ULL;
+                for (uint64_t i = cur.n; i > 1; i--) {
+                    x = mix64(x + 0x9e3779b97f4a7c15ULL);
+                    uint64_t j = x % i, t = perm[i - 1]; perm[i - 1] = perm[j]; perm[j] = t;
+                }
+            }
+        }
         for (uint64_t i = 0; i < cur.n; i++) {
-            ar_get(&cur, i, ps);
+            ar_get(&cur, perm ? perm[i] : i, ps);
             if (ps->nm > O->max_nm) O->max_nm = ps->nm;
             int nsucc = 0;
             for (int s = 0; s < c->n; s++) {
@@ -744,7 +764,8 @@ int orc_run(void *h, uint64_t max_states) {
                     O->generated += (uint64_t)b.n;
                     O->lvl_generated[lvl - 1] += (uint64_t)b.n;
                     nsucc += b.n;
-                    for (int j = 0; j < b.n; j++) {
+                    for (int jj = 0; jj < b.n; jj++) {
+                        const int j = c->order == 1 ? b.n - 1 - jj : jj;
                         st_t *t = &b.buf[j];
                         canon_hash(c, &O->P, t, h2);
                         if (!fps_put(&S, h2)) continue;
@@ -770,6 +791,7 @@ int orc_run(void *h, uint64_t max_states) {
                 goto done;
             }
         }
+        free(perm);
         arena_t tmp = cur; cur = nxt; nxt = tmp; ar_clear(&nxt);
         cur_base = nxt_base;
     }
@@ -822,7 +844,7 @@ int orc_trace_state(void *h, int idx, int32_t *out, int cap_ints, uint32_t *key)
 /* successors of an unpacked state in TLC order; returns count, -1 on Assert, -2 on capacity */
 int orc_successors(int n, int V, int E, int R, int seeded, const int32_t *in, int32_t *out, int stride_ints,
                    int cap_states, uint32_t *keys) {
-    ocfg_t c = {n, V, E, R, seeded, 0, 1, 0};
+    ocfg_t c = {n, V, E, R, seeded, 0, 1, 0, 0, 0};
     st_t *st = (st_t *)malloc(sizeof(st_t));
     batch_t b; b.buf = (st_t *)malloc(sizeof(st_t) * BATCH_CAP); b.w = (int32_t *)malloc(sizeof(int32_t) * BATCH_CAP); b.cap = BATCH_CAP;
     int cnt = 0, ret = 0;
@@ -846,7 +868,7 @@ out:
 }
 
 int orc_canon_hash(int n, int V, const int32_t *in, uint64_t *out2) {
-    ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0};
+    ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0, 0, 0};
     perms_t *P = (perms_t *)malloc(sizeof(perms_t));
     make_perms(n, P);
     st_t *st = (st_t *)malloc(sizeof(st_t));
@@ -857,7 +879,7 @@ int orc_canon_hash(int n, int V, const int32_t *in, uint64_t *out2) {
 }
 
 int orc_inv(int n, int V, const int32_t *in, int inv_id) {
-    ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0};
+    ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0, 0, 0};
     st_t *st = (st_t *)malloc(sizeof(st_t));
     int r = pack_from(&c, in, st);
     if (r >= 0) r = inv_eval(&c, st, inv_id);
@@ -870,9 +892,10 @@ int orc_inv(int n, int V, const int32_t *in, int inv_id) {
 int main(int argc, char **argv) {
     int n = 3, V = 2, E = 3, R = 3, seeded = 0;
     uint32_t mask = 1;
-    int trace = 1;
+    int trace = 1, order = 0;
     for (int i = 1; i < argc; i++) {
         if (!strcmp(argv[i], "-notrace")) trace = 0;
+        else if (!strcmp(argv[i], "-order")) order = atoi(argv[++i]);
         if (!strcmp(argv[i], "-n")) n = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-V")) V = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-E")) E = atoi(argv[++i]);
@@ -881,6 +904,7 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "-inv")) mask = (uint32_t)strtoul(argv[++i], 0, 0);
     }
     void *h = orc_create(n, V, E, R, seeded, 0, mask, trace);
+    orc_set_order(h, order, 12345);
     int v = orc_run(h, 0);
     uint64_t d[MAXLEVELS], g[MAXLEVELS];
     int L = orc_levels(h, d, g, MAXLEVELS);

@@ -12,7 +12,8 @@ so every fixture here comes from the CPU restatements in oracle/:
 * traces.json      counterexamples: the seeded commit bug, debug invariants that
                    are FALSE early, and a deadlock trace (check_deadlock on) -- Python oracle.
 
-Usage: python tests/golden/make_golden.py [--big]   (--big adds the 18.5M-state n3/V2/E2 config)
+Usage: python tests/golden/make_golden.py [--big]
+  (--big adds n3/V2/E2 = 18.5M states and n3/V1/E3 = 60.2M states: ~25 min of C-oracle time)
 """
 import argparse
 import ctypes
@@ -85,7 +86,7 @@ def main():
     both = [(3, 1, 1, 3), (3, 2, 1, 3), (2, 1, 2, 3), (4, 1, 1, 3), (3, 1, 2, 3)]
     c_only = [(2, 2, 3, 3), (3, 3, 1, 3), (5, 1, 1, 3), (3, 1, 2, 1), (2, 1, 3, 2)]
     if args.big:
-        c_only.append((3, 2, 2, 3))
+        c_only += [(3, 2, 2, 3), (3, 1, 3, 3)]
     levels = {}
     for (n, V, E, Rr) in both + c_only:
         name = f"n{n}_v{V}_e{E}_r{Rr}"
