@@ -77,7 +77,9 @@ typedef struct rmc_config {
     uint64_t chunk_successors; /* successors per device chunk (0 = auto) */
     /* multi-GPU (one process per GPU): world_size 1 = single GPU */
     int32_t rank, world_size;  /* world_size 0 or 1 = single GPU */
-    const void *comm_unique_id; /* 128-byte RCCL unique id, identical on every rank */
+    const void *comm_unique_id; /* 128-byte RCCL unique id (rmc_comm_unique_id on rank 0), same on every rank */
+    int32_t virtual_shards;    /* > 1: run that many fingerprint-owner shards in this process on one device
+                                  (the multi-GPU partition/exchange logic with device copies for transport) */
 } rmc_config;
 
 /* Statistics of one BFS level (what TLC's progress line reports). */
@@ -106,6 +108,11 @@ typedef struct rmc_result {
 } rmc_result;
 
 int rmc_abi_version(void);
+
+/* RCCL unique id for a multi-GPU run (call on rank 0, broadcast the 128 bytes to every
+ * rank, pass as rmc_config.comm_unique_id).  Replaces nothing in the reference: TLC runs
+ * in one JVM; this is the seen-set sharding of SURVEY.md 8(e). */
+int rmc_comm_unique_id(void *out128);
 
 /* Parse Raft.cfg text (replaces TLC's ModelConfig for the subset Raft.cfg uses,
  * Raft.cfg:1-34) and validate Raft.tla text by content (replaces SANY; only

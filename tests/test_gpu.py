@@ -146,3 +146,39 @@ def test_seeded_trace_independent_of_chunking():
     mc, res = run_cfg(g, chunk_successors=6000, seen_log2=10)
     check_levels(g, res)
     mc.close()
+
+
+# ---- sharded BFS (fingerprint-owner shards), run as virtual shards on one GPU ----
+SHARDED = ["n3_v1_e1_r3", "n3_v2_e1_r3", "n2_v2_e3_r3", "n4_v1_e1_r3", "n3_v1_e2_r3", "n5_v1_e1_r3", "n3_v3_e1_r3"]
+
+
+@pytest.mark.parametrize("shards", [2, 3, 8])
+@pytest.mark.parametrize("name", SHARDED)
+def test_sharded_bfs_matches_golden(name, shards):
+    """Owner-sharded exploration (order: chunk, source shard, TLC order) reaches the same
+    distinct/generated counts, depth and per-level sizes as TLC's -workers 1 order."""
+    g = LEVELS[name]
+    mc, res = run_cfg(g, virtual_shards=shards, chunk_successors=20000)
+    check_levels(g, res)
+    mc.close()
+
+
+@pytest.mark.parametrize("name", ["seeded_n3_v1_e2_r3", "seeded_n3_v2_e2_r3", "deadlock_n3_v1_e1_r3",
+                                  "exist_lc_n3_v1_e2_r3"])
+def test_sharded_counterexample_is_valid_and_shortest(name):
+    g = LEVELS[name]
+    cfg = R.Config(n=g["n"], V=g["V"], max_election=g["E"], max_restart=g["R"], seeded=g["seeded"],
+                   invariants=tuple(g["invariants"]), check_deadlock=g["check_deadlock"])
+    mc, res = run_cfg(g, virtual_shards=4, chunk_successors=20000)
+    assert res.status == {"ok": "done"}.get(g["verdict"], g["verdict"])
+    assert res.trace_len == g["trace_len"]          # BFS: shortest counterexample, same length as TLC
+    tr = mc.trace()
+    for (k1, a), (k2, b) in zip(tr, tr[1:]):
+        succ = R.successors(cfg, R.state_from_json(a))
+        assert (tuple(k2), R.state_from_json(b)) in [(k, t) for k, t in succ]
+    last = R.state_from_json(tr[-1][1])
+    if g["verdict"] == "invariant":
+        assert not all(R.INV_FUNCS[i](cfg, last) for i in g["invariants"])
+    if g["verdict"] == "deadlock":
+        assert R.successors(cfg, last) == []
+    mc.close()

@@ -25,6 +25,10 @@
 #include "rmc_kernels.h"
 #include "rmc_spec.h"
 
+#ifdef RMC_WITH_RCCL
+#include <rccl/rccl.h>
+#endif
+
 using namespace rmc;
 
 namespace {
@@ -137,6 +141,48 @@ struct TraceStep {
 
 }  // namespace
 
+
+// Per-shard device state.  One shard per GPU (RCCL rank) -- or several "virtual"
+// shards in one process on one device, which runs the identical partition/exchange
+// logic with device copies instead of RCCL (the multi-GPU parity tests use it).
+struct Shard {
+    int id = 0;  // global shard index = owner id
+    // frontier: current and next level, packed records
+    uint32_t *cur = nullptr, *nxt = nullptr;
+    uint64_t cur_n = 0, cur_cap = 0, nxt_n = 0, nxt_cap = 0;
+    // seen-set shard
+    ulonglong2 *T = nullptr;
+    uint64_t T_cap = 0, T_count = 0;
+    // trace: parent reference (shard << 48 | local gid) + slot key, per local gid
+    uint64_t *par = nullptr;
+    uint16_t *pslot = nullptr;
+    uint64_t trace_cap = 0;
+    std::vector<uint64_t> level_start;  // local gid of the first state of each level
+    // chunk buffers (source side)
+    uint32_t *cnt = nullptr, *off = nullptr, *lslot = nullptr, *wflag = nullptr, *wpos = nullptr;
+    ulonglong2 *fp = nullptr;
+    unsigned long long *L = nullptr;
+    uint32_t epoch = 0;
+    void *tmp = nullptr;
+    size_t tmp_bytes = 0;
+    // exchange buffers (W > 1)
+    uint32_t *okey = nullptr, *okey2 = nullptr, *iota = nullptr, *perm = nullptr, *sflag = nullptr, *spos = nullptr;
+    ulonglong2 *sfp = nullptr;
+    unsigned long long *ocnt = nullptr;
+    ulonglong2 *rfp = nullptr;
+    uint32_t *rlslot = nullptr, *rflag = nullptr, *rpos = nullptr, *rcount = nullptr;
+    uint64_t rcap = 0;
+    uint32_t *sx = nullptr, *rx = nullptr;
+    uint64_t sx_cap = 0, rx_cap = 0;
+    uint64_t *pick_idx = nullptr;
+    // errors, summary
+    unsigned long long *err = nullptr, *sum = nullptr, *hsum = nullptr;
+    uint32_t *flags = nullptr;
+    // per-chunk host bookkeeping (sharded path)
+    uint64_t p0 = 0, np = 0, G = 0;
+    std::vector<uint64_t> scnt, soff, rcnt, roff, swin, swoff, rwin, rwoff;
+};
+
 struct rmc_ctx {
     rmc_config cfg{};
     KernelSet ks{};
@@ -144,6 +190,11 @@ struct rmc_ctx {
     std::string err;
     hipStream_t stream = nullptr;
     int N = 0, V = 0, RECW = 0;
+    int W = 1, rank = 0;  // shards in the run, this process's first shard
+    bool virt = false;    // all W shards live in this process
+#ifdef RMC_WITH_RCCL
+    ncclComm_t comm = nullptr;
+#endif
 
     // device tables
     uint32_t *d_info = nullptr;
@@ -153,43 +204,21 @@ struct rmc_ctx {
     uint64_t *d_seeds = nullptr;
     int np = 0;
 
-    // frontier
-    uint32_t *d_cur = nullptr, *d_nxt = nullptr;
-    uint64_t cur_n = 0, cur_cap = 0, nxt_cap = 0;
+    std::vector<Shard> sh;
+    uint64_t chunk_parents = 0, Gcap = 0, Lcap_max = 0;
 
-    // chunk buffers
-    uint64_t chunk_parents = 0, Gcap = 0;
-    uint32_t *d_cnt = nullptr, *d_off = nullptr, *d_lslot = nullptr, *d_wflag = nullptr, *d_wpos = nullptr;
-    unsigned long long *d_L = nullptr;  // chunk dedup table, (epoch << 32) | j
-    uint64_t Lcap_max = 0;
-    uint32_t epoch = 0;
-    unsigned long long *d_sum = nullptr, *h_sum = nullptr;  // per-chunk summary (G, W, errors, flags)
     std::vector<hipEvent_t> evpool;
     struct EvRec { int ph; int a, b; };
     std::vector<EvRec> evrecs;
     int evused = 0;
-    ulonglong2 *d_fp = nullptr;
-    void *d_tmp = nullptr;
-    size_t tmp_bytes = 0;
-
-    // seen set
-    ulonglong2 *d_T = nullptr;
-    uint64_t T_cap = 0, T_count = 0;
-
-    // trace
-    uint64_t *d_par = nullptr;
-    uint16_t *d_pslot = nullptr;
-    uint64_t trace_cap = 0;
-    std::vector<uint64_t> level_start;  // gid of each level's first state
-
-    // errors / flags
-    unsigned long long *d_err = nullptr;
-    uint32_t *d_flags = nullptr;
 
     // scratch for single-state hooks
     uint32_t *d_one = nullptr, *d_out = nullptr, *d_keys = nullptr, *d_cnt1 = nullptr;
     ulonglong2 *d_fp1 = nullptr;
     int32_t *d_inv = nullptr;
+    unsigned long long *d_err1 = nullptr;
+    uint32_t *d_flags1 = nullptr;
+    unsigned long long *d_red = nullptr, *h_red = nullptr;  // collective scratch
 
     // progress
     bool inited = false, finished = false;
@@ -197,13 +226,12 @@ struct rmc_ctx {
     int depth = 0;
     uint64_t total_generated = 0, total_distinct = 0, queue_at_end = 0;
     int violated = -1;
-    uint64_t err_gid = 0;  // state whose trace is reported
+    uint64_t err_ref = 0;  // state whose trace is reported: shard << 48 | local gid
+    uint32_t err_last_slot = KEY_NONE;  // sharded: slot of the violating successor (not stored anywhere)
     std::vector<TraceStep> trace;
     double seconds = 0;
 
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-
-    KParams base() const {
+    KParams base(const Shard &s) const {
         KParams P{};
         P.d = U.d;
         P.E = cfg.max_election;
@@ -217,12 +245,12 @@ struct rmc_ctx {
         P.t.perms = d_perms;
         P.t.seeds = d_seeds;
         P.t.np = np;
-        P.T = d_T;
-        P.Tmask = T_cap - 1;
-        P.err = d_err;
-        P.flags = d_flags;
-        P.par = d_par;
-        P.pslot = d_pslot;
+        P.T = s.T;
+        P.Tmask = s.T_cap - 1;
+        P.err = s.err;
+        P.flags = s.flags;
+        P.par = s.par;
+        P.pslot = s.pslot;
         return P;
     }
 
@@ -362,6 +390,7 @@ struct rmc_ctx {
         return rec;
     }
 
+
     // ---- allocation -----------------------------------------------------------------
     void setup() {
         if (cfg.n_servers < 1 || cfg.n_servers > MAXN) throw Fail(RMC_E_ARG, "n_servers must be 1..5");
@@ -370,7 +399,13 @@ struct rmc_ctx {
         if (cfg.max_restart < 0 || cfg.max_restart > 15) throw Fail(RMC_E_ARG, "max_restart must be 0..15");
         if (cfg.invariants & RMC_INV_NO_ALL_COMMIT) throw Fail(RMC_E_ARG, "invariant NoAllCommit is not compiled");
         if (cfg.invariants & ~0x7Fu) throw Fail(RMC_E_ARG, "unknown invariant bits");
-        if (cfg.world_size > 1) throw Fail(RMC_E_ARG, "multi-GPU sharding is driven by rmc_create on each rank: not in this build");
+        const int ws = cfg.world_size > 1 ? cfg.world_size : 1;
+        if (cfg.virtual_shards > 1 && ws > 1) throw Fail(RMC_E_ARG, "virtual_shards and world_size > 1 are exclusive");
+        if (cfg.virtual_shards > 64 || ws > 64) throw Fail(RMC_E_ARG, "at most 64 shards");
+        virt = cfg.virtual_shards > 1;
+        W = virt ? cfg.virtual_shards : ws;
+        rank = virt ? 0 : (ws > 1 ? cfg.rank : 0);
+        if (rank < 0 || rank >= W) throw Fail(RMC_E_ARG, "rank out of range");
         N = cfg.n_servers;
         V = cfg.n_vals;
         int cap = cfg.msg_cap ? cfg.msg_cap : (N <= 3 ? 64 : 128);
@@ -389,8 +424,16 @@ struct rmc_ctx {
         if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
             throw Fail(RMC_E_DEVICE, std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950");
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        HIPCHK(hipEventCreate(&ev0));
-        HIPCHK(hipEventCreate(&ev1));
+        if (W > 1 && !virt) {
+#ifdef RMC_WITH_RCCL
+            if (!cfg.comm_unique_id) throw Fail(RMC_E_ARG, "world_size > 1 needs comm_unique_id (rmc_comm_unique_id)");
+            ncclUniqueId id;
+            std::memcpy(&id, cfg.comm_unique_id, sizeof id);
+            if (ncclCommInitRank(&comm, W, id, rank) != ncclSuccess) throw Fail(RMC_E_COMM, "ncclCommInitRank failed");
+#else
+            throw Fail(RMC_E_COMM, "built without RCCL");
+#endif
+        }
 
         U.build(N, V, cfg.max_election);
         d_info = dmalloc<uint32_t>(U.info.size());
@@ -421,41 +464,14 @@ struct rmc_ctx {
         d_seeds = dmalloc<uint64_t>(seeds.size());
         HIPCHK(hipMemcpy(d_seeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
 
-        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (1ull << 26);
+        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (virt ? (1ull << 23) : (1ull << 26));
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 31)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^31");
         chunk_parents = Gcap / ks.maxsucc;
-        d_cnt = dmalloc<uint32_t>(chunk_parents + 1);
-        d_off = dmalloc<uint32_t>(chunk_parents + 1);
-        d_fp = dmalloc<ulonglong2>(Gcap);
-        d_lslot = dmalloc<uint32_t>(Gcap);
-        d_wflag = dmalloc<uint32_t>(Gcap + 1);
-        HIPCHK(hipMemsetAsync(d_cnt, 0, (chunk_parents + 1) * 4, stream));
-        HIPCHK(hipMemsetAsync(d_wflag, 0, (Gcap + 1) * 4, stream));
-        d_wpos = dmalloc<uint32_t>(Gcap + 1);
         Lcap_max = next_pow2(2 * Gcap);
-        d_L = dmalloc<unsigned long long>(Lcap_max);
-        HIPCHK(hipMemsetAsync(d_L, 0, Lcap_max * 8, stream));
-        d_sum = dmalloc<unsigned long long>(16);
-        HIPCHK(hipHostMalloc((void **)&h_sum, 16 * 8, hipHostMallocDefault));
-        size_t t1 = 0;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, d_cnt, d_off, (int)Gcap + 1, stream));
-        tmp_bytes = t1;
-        d_tmp = dmalloc<uint8_t>(tmp_bytes);
 
-        T_cap = 1ull << (cfg.seen_log2 ? cfg.seen_log2 : 22);
-        d_T = dmalloc<ulonglong2>(T_cap);
-        HIPCHK(hipMemsetAsync(d_T, 0, T_cap * 16, stream));
-        d_err = dmalloc<unsigned long long>(ERR_NSLOTS);
-        d_flags = dmalloc<uint32_t>(4);
-        reset_errors();
-
-        cur_cap = nxt_cap = 1 << 16;
-        d_cur = dmalloc<uint32_t>(cur_cap * RECW);
-        d_nxt = dmalloc<uint32_t>(nxt_cap * RECW);
-        trace_cap = 1 << 20;
-        d_par = dmalloc<uint64_t>(trace_cap);
-        d_pslot = dmalloc<uint16_t>(trace_cap);
+        sh.resize(virt ? W : 1);
+        for (size_t i = 0; i < sh.size(); i++) alloc_shard(sh[i], virt ? (int)i : rank);
 
         d_one = dmalloc<uint32_t>(RECW);
         d_out = dmalloc<uint32_t>((size_t)ks.maxsucc * RECW);
@@ -463,68 +479,148 @@ struct rmc_ctx {
         d_cnt1 = dmalloc<uint32_t>(4);
         d_fp1 = dmalloc<ulonglong2>(ks.maxsucc + 1);
         d_inv = dmalloc<int32_t>(7);
+        d_err1 = dmalloc<unsigned long long>(ERR_NSLOTS);
+        d_flags1 = dmalloc<uint32_t>(4);
+        d_red = dmalloc<unsigned long long>(4 * 64 + 8);
+        HIPCHK(hipHostMalloc((void **)&h_red, (4 * 64 + 8) * 8, hipHostMallocDefault));
         HIPCHK(hipStreamSynchronize(stream));
     }
 
-    void reset_errors() {
-        HIPCHK(hipMemsetAsync(d_err, 0xFF, ERR_NSLOTS * 8, stream));
-        HIPCHK(hipMemsetAsync(d_flags, 0, 16, stream));
+    void alloc_shard(Shard &s, int id) {
+        s.id = id;
+        s.cnt = dmalloc<uint32_t>(chunk_parents + 1);
+        s.off = dmalloc<uint32_t>(chunk_parents + 1);
+        s.fp = dmalloc<ulonglong2>(Gcap);
+        s.lslot = dmalloc<uint32_t>(Gcap);
+        s.wflag = dmalloc<uint32_t>(Gcap + 1);
+        s.wpos = dmalloc<uint32_t>(Gcap + 1);
+        HIPCHK(hipMemsetAsync(s.cnt, 0, (chunk_parents + 1) * 4, stream));
+        HIPCHK(hipMemsetAsync(s.wflag, 0, (Gcap + 1) * 4, stream));
+        s.L = dmalloc<unsigned long long>(Lcap_max);
+        HIPCHK(hipMemsetAsync(s.L, 0, Lcap_max * 8, stream));
+        size_t t1 = 0, t2 = 0;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, s.cnt, s.off, (int)Gcap + 1, stream));
+        if (W > 1) {
+            s.okey = dmalloc<uint32_t>(Gcap);
+            s.okey2 = dmalloc<uint32_t>(Gcap);
+            s.iota = dmalloc<uint32_t>(Gcap);
+            s.perm = dmalloc<uint32_t>(Gcap);
+            s.sflag = dmalloc<uint32_t>(Gcap + 1);
+            s.spos = dmalloc<uint32_t>(Gcap + 1);
+            s.sfp = dmalloc<ulonglong2>(Gcap);
+            s.ocnt = dmalloc<unsigned long long>(64);
+            s.pick_idx = dmalloc<uint64_t>(2 * 65);
+            int bits = 0;
+            while ((1 << bits) < W) bits++;
+            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, s.okey, s.okey2, s.iota, s.perm, (int)Gcap, 0,
+                                                      std::max(bits, 1), stream));
+        }
+        s.tmp_bytes = std::max(t1, t2);
+        s.tmp = dmalloc<uint8_t>(s.tmp_bytes);
+        s.T_cap = 1ull << (cfg.seen_log2 ? cfg.seen_log2 : 22);
+        s.T = dmalloc<ulonglong2>(s.T_cap);
+        HIPCHK(hipMemsetAsync(s.T, 0, s.T_cap * 16, stream));
+        s.err = dmalloc<unsigned long long>(ERR_NSLOTS);
+        s.flags = dmalloc<uint32_t>(4);
+        HIPCHK(hipMemsetAsync(s.err, 0xFF, ERR_NSLOTS * 8, stream));
+        HIPCHK(hipMemsetAsync(s.flags, 0, 16, stream));
+        s.sum = dmalloc<unsigned long long>(160);
+        HIPCHK(hipHostMalloc((void **)&s.hsum, 160 * 8, hipHostMallocDefault));
+        s.cur_cap = s.nxt_cap = 1 << 16;
+        s.cur = dmalloc<uint32_t>(s.cur_cap * RECW);
+        s.nxt = dmalloc<uint32_t>(s.nxt_cap * RECW);
+        s.trace_cap = 1 << 20;
+        s.par = dmalloc<uint64_t>(s.trace_cap);
+        s.pslot = dmalloc<uint16_t>(s.trace_cap);
+    }
+
+    void free_shard(Shard &s) {
+        dfree(s.cur); dfree(s.nxt); dfree(s.T); dfree(s.par); dfree(s.pslot); dfree(s.cnt); dfree(s.off);
+        dfree(s.lslot); dfree(s.wflag); dfree(s.wpos); dfree(s.fp); dfree(s.L); dfree(s.tmp); dfree(s.okey);
+        dfree(s.okey2); dfree(s.iota); dfree(s.perm); dfree(s.sflag); dfree(s.spos); dfree(s.sfp); dfree(s.ocnt);
+        dfree(s.rfp); dfree(s.rlslot); dfree(s.rflag); dfree(s.rpos); dfree(s.rcount); dfree(s.sx); dfree(s.rx);
+        dfree(s.pick_idx); dfree(s.err); dfree(s.sum); dfree(s.flags);
+        if (s.hsum) (void)hipHostFree(s.hsum);
+        s.hsum = nullptr;
     }
 
     void release() {
+        for (Shard &s : sh) free_shard(s);
+        sh.clear();
         dfree(d_info); dfree(d_nat2id); dfree(d_gmsg); dfree(d_perms); dfree(d_seeds);
-        dfree(d_cur); dfree(d_nxt); dfree(d_cnt); dfree(d_off); dfree(d_fp); dfree(d_lslot); dfree(d_wflag);
-        dfree(d_wpos); dfree(d_L); dfree(d_tmp); dfree(d_T); dfree(d_par); dfree(d_pslot); dfree(d_err);
-        dfree(d_flags); dfree(d_one); dfree(d_out); dfree(d_keys); dfree(d_cnt1); dfree(d_fp1); dfree(d_inv);
-        dfree(d_sum);
-        if (h_sum) (void)hipHostFree(h_sum);
-        h_sum = nullptr;
+        dfree(d_one); dfree(d_out); dfree(d_keys); dfree(d_cnt1); dfree(d_fp1); dfree(d_inv); dfree(d_err1);
+        dfree(d_flags1); dfree(d_red);
+        if (h_red) (void)hipHostFree(h_red);
+        h_red = nullptr;
         for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
         evpool.clear();
-        if (ev0) (void)hipEventDestroy(ev0);
-        if (ev1) (void)hipEventDestroy(ev1);
+#ifdef RMC_WITH_RCCL
+        if (comm) (void)ncclCommDestroy(comm);
+        comm = nullptr;
+#endif
         if (stream) (void)hipStreamDestroy(stream);
-        ev0 = ev1 = nullptr;
         stream = nullptr;
     }
 
-    void grow_records(uint32_t *&buf, uint64_t &cap, uint64_t used, uint64_t need) {
+    void grow_records(uint32_t *&buf, uint64_t &cap, uint64_t used, uint64_t need, uint64_t recw) {
         if (need <= cap) return;
         uint64_t nc = std::max<uint64_t>(need + need / 2, cap * 2);
-        uint32_t *nb = dmalloc<uint32_t>(nc * RECW);
-        if (used) HIPCHK(hipMemcpyAsync(nb, buf, used * RECW * 4, hipMemcpyDeviceToDevice, stream));
+        uint32_t *nb = dmalloc<uint32_t>(nc * recw);
+        if (used) HIPCHK(hipMemcpyAsync(nb, buf, used * recw * 4, hipMemcpyDeviceToDevice, stream));
         HIPCHK(hipStreamSynchronize(stream));
         dfree(buf);
         buf = nb;
         cap = nc;
     }
 
-    void grow_trace(uint64_t need) {
-        if (need <= trace_cap) return;
-        uint64_t nc = std::max<uint64_t>(need + need / 2, trace_cap * 2);
+    void grow_trace(Shard &s, uint64_t need) {
+        if (need <= s.trace_cap) return;
+        uint64_t nc = std::max<uint64_t>(need + need / 2, s.trace_cap * 2);
         uint64_t *np_ = dmalloc<uint64_t>(nc);
         uint16_t *ns = dmalloc<uint16_t>(nc);
-        HIPCHK(hipMemcpyAsync(np_, d_par, trace_cap * 8, hipMemcpyDeviceToDevice, stream));
-        HIPCHK(hipMemcpyAsync(ns, d_pslot, trace_cap * 2, hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipMemcpyAsync(np_, s.par, s.trace_cap * 8, hipMemcpyDeviceToDevice, stream));
+        HIPCHK(hipMemcpyAsync(ns, s.pslot, s.trace_cap * 2, hipMemcpyDeviceToDevice, stream));
         HIPCHK(hipStreamSynchronize(stream));
-        dfree(d_par);
-        dfree(d_pslot);
-        d_par = np_;
-        d_pslot = ns;
-        trace_cap = nc;
+        dfree(s.par);
+        dfree(s.pslot);
+        s.par = np_;
+        s.pslot = ns;
+        s.trace_cap = nc;
     }
 
-    void grow_seen(uint64_t need) {
-        if (need * 2 <= T_cap) return;  // keep the load factor <= 1/2
-        uint64_t nc = T_cap;
+    void grow_seen(Shard &s, uint64_t need) {
+        if (need * 2 <= s.T_cap) return;  // keep the load factor <= 1/2
+        uint64_t nc = s.T_cap;
         while (need * 2 > nc) nc *= 4;
         ulonglong2 *nT = dmalloc<ulonglong2>(nc);
         HIPCHK(hipMemsetAsync(nT, 0, nc * 16, stream));
-        launch_rehash(d_T, T_cap, nT, nc - 1, stream);
+        launch_rehash(s.T, s.T_cap, nT, nc - 1, stream);
         HIPCHK(hipStreamSynchronize(stream));
-        dfree(d_T);
-        d_T = nT;
-        T_cap = nc;
+        dfree(s.T);
+        s.T = nT;
+        s.T_cap = nc;
+    }
+
+    template <class T>
+    void grow_plain(T *&p, uint64_t &cap, uint64_t need) {
+        if (need <= cap) return;
+        uint64_t nc = std::max<uint64_t>(need + need / 2, 1024);
+        dfree(p);
+        p = dmalloc<T>(nc);
+        cap = nc;
+    }
+
+    void grow_recv(Shard &s, uint64_t need) {
+        if (need + 1 <= s.rcap) return;
+        uint64_t nc = std::max<uint64_t>(need + need / 2 + 1, 1024);
+        dfree(s.rfp); dfree(s.rlslot); dfree(s.rflag); dfree(s.rpos);
+        s.rfp = dmalloc<ulonglong2>(nc);
+        s.rlslot = dmalloc<uint32_t>(nc);
+        s.rflag = dmalloc<uint32_t>(nc);
+        s.rpos = dmalloc<uint32_t>(nc);
+        HIPCHK(hipMemsetAsync(s.rflag, 0, nc * 4, stream));
+        s.rcap = nc;
+        if (!s.rcount) s.rcount = dmalloc<uint32_t>(4);
     }
 
     // Phase timing by event pairs on the engine's stream, read back at the next sync
@@ -567,11 +663,79 @@ struct rmc_ctx {
         return v;
     }
 
+    // ---- collectives over shards --------------------------------------------------------
+    // Every host value handed to these is this process's contribution (virtual mode: the
+    // sum/max over all local shards already IS the global value).
+    void allreduce(uint64_t *v, int n, bool is_max) {
+        if (W == 1 || virt) return;
+#ifdef RMC_WITH_RCCL
+        for (int i = 0; i < n; i++) h_red[i] = v[i];
+        HIPCHK(hipMemcpyAsync(d_red, h_red, n * 8, hipMemcpyHostToDevice, stream));
+        if (ncclAllReduce(d_red, d_red, n, ncclUint64, is_max ? ncclMax : ncclSum, comm, stream) != ncclSuccess)
+            throw Fail(RMC_E_COMM, "ncclAllReduce failed");
+        HIPCHK(hipMemcpyAsync(h_red, d_red, n * 8, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        for (int i = 0; i < n; i++) v[i] = h_red[i];
+#endif
+    }
+
+    // counts: c_out[local d][s] = c_in[local s][d]
+    void exchange_counts(const std::vector<std::vector<uint64_t>> &in, std::vector<std::vector<uint64_t>> &out) {
+        out.assign(sh.size(), std::vector<uint64_t>(W, 0));
+        if (virt || W == 1) {
+            for (int s = 0; s < W && s < (int)in.size(); s++)
+                for (int d = 0; d < (int)sh.size(); d++) out[d][s] = in[s][d];
+            return;
+        }
+#ifdef RMC_WITH_RCCL
+        for (int d = 0; d < W; d++) h_red[d] = in[0][d];
+        HIPCHK(hipMemcpyAsync(d_red, h_red, W * 8, hipMemcpyHostToDevice, stream));
+        if (ncclAllToAll(d_red, d_red + 64, 1, ncclUint64, comm, stream) != ncclSuccess)
+            throw Fail(RMC_E_COMM, "ncclAllToAll failed");
+        HIPCHK(hipMemcpyAsync(h_red, d_red + 64, W * 8, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        for (int s = 0; s < W; s++) out[0][s] = h_red[s];
+#endif
+    }
+
+    // alltoallv of fixed-size items: send[local s] segment d (cnt scnt[s][d] at soff[s][d]) ->
+    // recv[local d] segment s (at roff[d][s]).
+    void exchange_items(const std::vector<const void *> &send, const std::vector<std::vector<uint64_t>> &scnt,
+                        const std::vector<std::vector<uint64_t>> &soff, const std::vector<void *> &recv,
+                        const std::vector<std::vector<uint64_t>> &roff, size_t elem) {
+        if (virt || W == 1) {
+            for (int s = 0; s < W; s++)
+                for (int d = 0; d < W; d++) {
+                    const uint64_t n = scnt[s][d];
+                    if (!n) continue;
+                    HIPCHK(hipMemcpyAsync((char *)recv[d] + roff[d][s] * elem, (const char *)send[s] + soff[s][d] * elem,
+                                          n * elem, hipMemcpyDeviceToDevice, stream));
+                }
+            return;
+        }
+#ifdef RMC_WITH_RCCL
+        // recv counts are the transposed send counts, known to the caller through roff
+        if (ncclGroupStart() != ncclSuccess) throw Fail(RMC_E_COMM, "ncclGroupStart failed");
+        for (int peer = 0; peer < W; peer++) {
+            const uint64_t ns = scnt[0][peer];
+            const uint64_t nr = roff[0][peer + 1] - roff[0][peer];
+            if (ns && ncclSend((const char *)send[0] + soff[0][peer] * elem, ns * elem, ncclUint8, peer, comm, stream) != ncclSuccess)
+                throw Fail(RMC_E_COMM, "ncclSend failed");
+            if (nr && ncclRecv((char *)recv[0] + roff[0][peer] * elem, nr * elem, ncclUint8, peer, comm, stream) != ncclSuccess)
+                throw Fail(RMC_E_COMM, "ncclRecv failed");
+        }
+        if (ncclGroupEnd() != ncclSuccess) throw Fail(RMC_E_COMM, "ncclGroupEnd failed");
+#endif
+    }
+
     // successors of one record already in d_one: keys + records in d_out
     uint32_t expand_one(std::vector<uint32_t> *keys, std::vector<uint32_t> *recs, std::vector<ulonglong2> *fps,
                         bool *assert_fail) {
-        reset_errors();
-        KParams P = base();
+        HIPCHK(hipMemsetAsync(d_err1, 0xFF, ERR_NSLOTS * 8, stream));
+        HIPCHK(hipMemsetAsync(d_flags1, 0, 16, stream));
+        KParams P = base(sh[0]);
+        P.err = d_err1;
+        P.flags = d_flags1;
         P.front = d_one;
         P.p_begin = 0;
         P.p_end = 1;
@@ -585,8 +749,8 @@ struct rmc_ctx {
         const uint32_t cnt = d2h(d_cnt1);
         unsigned long long e[ERR_NSLOTS];
         uint32_t fl[4];
-        HIPCHK(hipMemcpy(e, d_err, sizeof e, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(fl, d_flags, sizeof fl, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(e, d_err1, sizeof e, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(fl, d_flags1, sizeof fl, hipMemcpyDeviceToHost));
         if (fl[0]) throw Fail(RMC_E_CAPACITY, "a successor exceeds msg_cap messages");
         *assert_fail = e[ERR_ASSERT] != ~0ull;
         if (keys) {
@@ -609,21 +773,32 @@ struct rmc_ctx {
         if (inited) throw Fail(RMC_E_STATE, "rmc_init called twice");
         auto t0 = std::chrono::steady_clock::now();
         std::vector<uint32_t> rec = init_record();
-        HIPCHK(hipMemcpy(d_cur, rec.data(), RECW * 4, hipMemcpyHostToDevice));
-        cur_n = 1;
-        KParams P = base();
-        P.front = d_cur;
+        HIPCHK(hipMemcpy(d_one, rec.data(), RECW * 4, hipMemcpyHostToDevice));
+        KParams P = base(sh[0]);
+        P.front = d_one;
         P.fp = d_fp1;
         ks.fp_states(P, 1, stream);
-        launch_insert_fps(d_fp1, 1, d_T, T_cap - 1, stream);
         ks.inv_states(P, 1, d_inv, stream);
+        uint32_t owner = 0;
+        if (W > 1) {
+            launch_owner_of(d_fp1, (uint32_t)W, d_cnt1, stream);
+            owner = d2h(d_cnt1);
+        }
         int32_t iv[7];
         HIPCHK(hipMemcpyAsync(iv, d_inv, sizeof iv, hipMemcpyDeviceToHost, stream));
-        const uint64_t none = ~0ull;
-        HIPCHK(hipMemcpyAsync(d_par, &none, 8, hipMemcpyHostToDevice, stream));
         HIPCHK(hipStreamSynchronize(stream));
-        T_count = 1;
-        level_start = {0};
+        const uint64_t none = ~0ull;
+        for (Shard &s : sh) {
+            s.level_start = {0};
+            s.cur_n = 0;
+            if ((uint32_t)s.id != owner) continue;
+            HIPCHK(hipMemcpyAsync(s.cur, d_one, RECW * 4, hipMemcpyDeviceToDevice, stream));
+            launch_insert_fps(d_fp1, 1, s.T, s.T_cap - 1, stream);
+            HIPCHK(hipMemcpyAsync(s.par, &none, 8, hipMemcpyHostToDevice, stream));
+            s.cur_n = 1;
+            s.T_count = 1;
+        }
+        HIPCHK(hipStreamSynchronize(stream));
         total_generated = 1;  // TLC counts the initial state as generated
         total_distinct = 1;
         depth = 1;
@@ -634,7 +809,8 @@ struct rmc_ctx {
             if (iv[b] != 1) {
                 status = iv[b] == 0 ? RMC_VIOLATION : RMC_EVAL_ERROR;
                 violated = b;
-                err_gid = 0;
+                err_ref = ((uint64_t)owner << 48);
+                err_last_slot = KEY_NONE;
                 queue_at_end = 0;
                 finished = true;
                 build_trace();
@@ -650,6 +826,7 @@ struct rmc_ctx {
             st->total_distinct = total_distinct;
             st->queue = finished ? 0 : 1;
             st->new_states = 1;
+            st->expanded = 0;
             st->seconds = seconds;
         }
         return status;
@@ -658,30 +835,49 @@ struct rmc_ctx {
     int step(rmc_level_stats *st) {
         if (!inited) throw Fail(RMC_E_STATE, "rmc_step before rmc_init");
         if (finished) return status == RMC_OK ? RMC_DONE : status;
-        auto t0 = std::chrono::steady_clock::now();
         rmc_level_stats local;
         if (!st) st = &local;
         std::memset(st, 0, sizeof *st);
-        const int L = (int)level_start.size();  // expanding level L (1-based)
+        return W == 1 ? step_single(st) : step_sharded(st);
+    }
+
+    // First error in TLC order among the error slots: smaller (parent, slot) first; on a
+    // tie the Assert wins (its sub-action's batch is discarded).
+    static int first_error(const unsigned long long *e, unsigned long long *best) {
+        int kind = -1;
+        *best = ~0ull;
+        const int order[4] = {ERR_ASSERT, ERR_DEADLOCK, ERR_INV, ERR_EVAL};
+        for (int q = 0; q < 4; q++) {
+            const int kk = order[q];
+            if (e[kk] == ~0ull) continue;
+            if (kind < 0 || (e[kk] >> 8) < (*best >> 8)) { kind = kk; *best = e[kk]; }
+        }
+        return kind;
+    }
+
+    int step_single(rmc_level_stats *st) {
+        auto t0 = std::chrono::steady_clock::now();
+        Shard &s = sh[0];
+        const int L = (int)s.level_start.size();  // expanding level L (1-based)
         st->level = L;
-        st->expanded = cur_n;
-        const uint64_t gid_cur = level_start[L - 1];
-        const uint64_t gid_nxt = gid_cur + cur_n;
+        st->expanded = s.cur_n;
+        const uint64_t gid_cur = s.level_start[L - 1];
+        const uint64_t gid_nxt = gid_cur + s.cur_n;
         uint64_t nxt_n = 0, level_gen = 0;
-        for (uint64_t p0 = 0; p0 < cur_n; p0 += chunk_parents) {
-            const uint64_t p1 = std::min(cur_n, p0 + chunk_parents), np_ = p1 - p0;
+        for (uint64_t p0 = 0; p0 < s.cur_n; p0 += chunk_parents) {
+            const uint64_t p1 = std::min(s.cur_n, p0 + chunk_parents), np_ = p1 - p0;
             auto params = [&] {
-                KParams Q = base();
-                Q.front = d_cur; Q.p_begin = p0; Q.p_end = p1; Q.cnt = d_cnt; Q.off = d_off; Q.fp = d_fp;
-                Q.wflag = d_wflag; Q.wpos = d_wpos; Q.next = d_nxt; Q.next_base = nxt_n;
+                KParams Q = base(s);
+                Q.front = s.cur; Q.p_begin = p0; Q.p_end = p1; Q.cnt = s.cnt; Q.off = s.off; Q.fp = s.fp;
+                Q.wflag = s.wflag; Q.wpos = s.wpos; Q.next = s.nxt; Q.next_base = nxt_n;
                 Q.gid_next_base = gid_nxt; Q.gid_parent_base = gid_cur;
                 return Q;
             };
-            const uint32_t *Gp = d_off + np_;  // device-side successor count of the chunk
+            const uint32_t *Gp = s.off + np_;  // device-side successor count of the chunk
             timed(PH_COUNT, [&] {
                 ks.count(params(), stream);
                 // exclusive scan over np_+1 items: off[np_] = G (cnt[np_] is never read into it)
-                HIPCHK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, d_cnt, d_off, (int)np_ + 1, stream));
+                HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.cnt, s.off, (int)np_ + 1, stream));
             });
             // Small chunks run on an upper bound of G without a host round trip; large
             // ones read G back so that the dedup/scan passes are sized exactly.
@@ -690,57 +886,49 @@ struct rmc_ctx {
                 Gub = d2h(Gp);
                 collect_times(st);
             }
-            grow_records(d_nxt, nxt_cap, nxt_n, nxt_n + Gub);
-            grow_trace(gid_nxt + nxt_n + Gub);
-            grow_seen(T_count + Gub);
+            grow_records(s.nxt, s.nxt_cap, nxt_n, nxt_n + Gub, RECW);
+            grow_trace(s, gid_nxt + nxt_n + Gub);
+            grow_seen(s, s.T_count + Gub);
             if (Gub) {
                 timed(PH_HASH, [&] { ks.hash(params(), stream); });
                 uint64_t Lcap = next_pow2(2 * Gub);
                 if (Lcap > Lcap_max) Lcap = Lcap_max;
-                ++epoch;
+                ++s.epoch;
                 timed(PH_DEDUP, [&] {
-                    launch_dedup(d_fp, Gp, Gub, d_T, T_cap - 1, d_L, Lcap - 1, epoch, d_lslot, stream);
-                    launch_winflag(d_lslot, d_L, Gp, Gub, d_wflag, stream);
-                    HIPCHK(hipcub::DeviceScan::ExclusiveSum(d_tmp, tmp_bytes, d_wflag, d_wpos, (int)Gub + 1, stream));
+                    launch_dedup(s.fp, Gp, Gub, s.T, s.T_cap - 1, s.L, Lcap - 1, s.epoch, s.lslot, stream);
+                    launch_winflag(s.lslot, s.L, Gp, Gub, s.wflag, stream);
+                    HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.wflag, s.wpos, (int)Gub + 1, stream));
                 });
                 timed(PH_MAT, [&] { ks.materialize(params(), stream); });
             }
-            launch_summary(Gp, d_wpos, d_err, d_flags, d_sum, stream);
-            HIPCHK(hipMemcpyAsync(h_sum, d_sum, 8 * 8, hipMemcpyDeviceToHost, stream));
+            launch_summary(Gp, s.wpos, s.err, s.flags, s.sum, stream);
+            HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
             HIPCHK(hipGetLastError());
             collect_times(st);
-            const uint64_t G = h_sum[0], W = Gub ? h_sum[1] : 0;
-            if (h_sum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
-            const unsigned long long *e = h_sum + 2;
+            const uint64_t G = s.hsum[0], Wn = Gub ? s.hsum[1] : 0;
+            if (s.hsum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
             level_gen += G;
-            T_count += W;
-            int kind = -1;
-            unsigned long long best = ~0ull;
-            // TLC order: smaller (parent, slot) first; on a tie the Assert wins (its action's batch is discarded)
-            const int order[4] = {ERR_ASSERT, ERR_DEADLOCK, ERR_INV, ERR_EVAL};
-            for (int q = 0; q < 4; q++) {
-                const int kk = order[q];
-                if (e[kk] == ~0ull) continue;
-                if (kind < 0 || (e[kk] >> 8) < (best >> 8)) { kind = kk; best = e[kk]; }
-            }
+            s.T_count += Wn;
+            unsigned long long best;
+            const int kind = first_error(s.hsum + 2, &best);
             if (kind >= 0) {
                 stop_on_error(kind, best, p0, nxt_n, gid_cur, gid_nxt, level_gen - G, st);
                 st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
                 seconds += st->seconds;
                 return status;
             }
-            nxt_n += W;
+            nxt_n += Wn;
         }
         total_generated += level_gen;
         total_distinct += nxt_n;
         st->generated = level_gen;
         st->new_states = nxt_n;
-        std::swap(d_cur, d_nxt);
-        std::swap(cur_cap, nxt_cap);
-        cur_n = nxt_n;
-        if (cur_n) {
-            level_start.push_back(gid_nxt);
+        std::swap(s.cur, s.nxt);
+        std::swap(s.cur_cap, s.nxt_cap);
+        s.cur_n = nxt_n;
+        if (s.cur_n) {
+            s.level_start.push_back(gid_nxt);
             depth = L + 1;
         } else {
             finished = true;
@@ -749,7 +937,7 @@ struct rmc_ctx {
         }
         st->total_generated = total_generated;
         st->total_distinct = total_distinct;
-        st->queue = cur_n;
+        st->queue = s.cur_n;
         st->status = finished ? RMC_DONE : RMC_OK;
         st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         seconds += st->seconds;
@@ -759,12 +947,13 @@ struct rmc_ctx {
     // TLC's counters at the moment the first error (in -workers 1 order) is reported.
     void stop_on_error(int kind, unsigned long long ek, uint64_t p0, uint64_t nxt_before, uint64_t gid_cur,
                        uint64_t gid_nxt, uint64_t gen_before_chunk, rmc_level_stats *st) {
+        Shard &s = sh[0];
         const uint64_t p = ek >> 24;                       // level-local parent
         const uint32_t slot = (uint32_t)((ek >> 8) & 0xFFFF);
         const int which = (int)(ek & 0xFF);
-        const uint32_t off_p = d2h(d_off + (p - p0));
+        const uint32_t off_p = d2h(s.off + (p - p0));
         // successors of p, in order, to find the sub-action batch boundaries
-        HIPCHK(hipMemcpy(d_one, d_cur + p * RECW, RECW * 4, hipMemcpyDeviceToDevice));
+        HIPCHK(hipMemcpy(d_one, s.cur + p * RECW, RECW * 4, hipMemcpyDeviceToDevice));
         std::vector<uint32_t> keys;
         bool af = false;
         expand_one(&keys, nullptr, nullptr, &af);
@@ -778,26 +967,27 @@ struct rmc_ctx {
         uint64_t winners_before;
         if (kind == ERR_INV || kind == ERR_EVAL) {
             gen += batch_end;  // TLC adds the whole sub-action's batch before fingerprinting it
-            uint32_t rank = 0;
-            for (uint32_t k : keys) rank += k < slot;
-            const uint32_t j = off_p + rank;
-            winners_before = d2h(d_wpos + j);
-            err_gid = gid_nxt + nxt_before + winners_before;
+            uint32_t rank_ = 0;
+            for (uint32_t k : keys) rank_ += k < slot;
+            const uint32_t j = off_p + rank_;
+            winners_before = d2h(s.wpos + j);
+            err_ref = gid_nxt + nxt_before + winners_before;
             total_distinct += nxt_before + winners_before + 1;
-            queue_at_end = (cur_n - p - 1) + nxt_before + winners_before;
+            queue_at_end = (s.cur_n - p - 1) + nxt_before + winners_before;
             status = kind == ERR_INV ? RMC_VIOLATION : RMC_EVAL_ERROR;
             violated = which;
-            depth = (int)level_start.size() + 1;
+            depth = (int)s.level_start.size() + 1;
         } else {
             if (kind == ERR_ASSERT) gen += cut;  // the failing sub-action's batch is never counted
             const uint32_t jcut = off_p + (kind == ERR_ASSERT ? cut : 0);
-            winners_before = d2h(d_wpos + jcut);
-            err_gid = gid_cur + p;
+            winners_before = d2h(s.wpos + jcut);
+            err_ref = gid_cur + p;
             total_distinct += nxt_before + winners_before;
-            queue_at_end = (cur_n - p - 1) + nxt_before + winners_before;
+            queue_at_end = (s.cur_n - p - 1) + nxt_before + winners_before;
             status = kind == ERR_ASSERT ? RMC_ASSERT : RMC_DEADLOCK;
-            if (winners_before + nxt_before > 0) depth = (int)level_start.size() + 1;
+            if (winners_before + nxt_before > 0) depth = (int)s.level_start.size() + 1;
         }
+        err_last_slot = KEY_NONE;
         total_generated += gen;
         st->generated = gen;
         st->new_states = nxt_before + winners_before + ((kind == ERR_INV || kind == ERR_EVAL) ? 1 : 0);
@@ -809,13 +999,271 @@ struct rmc_ctx {
         build_trace();
     }
 
-    // Walk parent pointers from err_gid to Init, then replay the slots from Init.
+    // ---- sharded level (W > 1): fingerprint-owner partition, exchange, owner election --
+    // Order: chunk c of every shard's frontier, then source shard, then TLC order within
+    // the source's chunk.  Identical to TLC -workers 1 order when W == 1.
+    int step_sharded(rmc_level_stats *st) {
+        auto t0 = std::chrono::steady_clock::now();
+        const int L = (int)sh[0].level_start.size();
+        st->level = L;
+        uint64_t agg[2] = {0, 0};
+        for (Shard &s : sh) agg[0] = std::max<uint64_t>(agg[0], (s.cur_n + chunk_parents - 1) / chunk_parents);
+        for (Shard &s : sh) { st->expanded += s.cur_n; s.nxt_n = 0; }
+        allreduce(agg, 1, true);
+        const uint64_t nchunks = agg[0];
+        const size_t NL = sh.size();
+        uint64_t level_gen = 0, level_new = 0;
+        std::vector<std::vector<uint64_t>> scnt(W, std::vector<uint64_t>(W, 0)), soff(W, std::vector<uint64_t>(W + 1, 0)),
+            rcnt, roff(W, std::vector<uint64_t>(W + 1, 0)), swin(W, std::vector<uint64_t>(W, 0)),
+            swoff(W, std::vector<uint64_t>(W + 1, 0)), rwin, rwoff(W, std::vector<uint64_t>(W + 1, 0));
+        std::vector<const void *> sendp(W);
+        std::vector<void *> recvp(W);
+        const uint64_t XW = (uint64_t)RECW + 4;
+        for (uint64_t c = 0; c < nchunks; c++) {
+            // (A) expand, fingerprint, partition by owner -- every local shard as a source
+            for (size_t li = 0; li < NL; li++) {
+                Shard &s = sh[li];
+                const uint64_t gid_cur = s.level_start[L - 1];
+                s.p0 = c * chunk_parents;
+                s.np = s.cur_n > s.p0 ? std::min<uint64_t>(chunk_parents, s.cur_n - s.p0) : 0;
+                s.G = 0;
+                std::fill(scnt[li].begin(), scnt[li].end(), 0);
+                if (!s.np) continue;
+                KParams Q = base(s);
+                Q.front = s.cur; Q.p_begin = s.p0; Q.p_end = s.p0 + s.np; Q.cnt = s.cnt; Q.off = s.off; Q.fp = s.fp;
+                Q.gid_parent_base = gid_cur;
+                timed(PH_COUNT, [&] {
+                    ks.count(Q, stream);
+                    HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.cnt, s.off, (int)s.np + 1, stream));
+                });
+                s.G = d2h(s.off + s.np);
+                collect_times(st);
+                if (!s.G) continue;
+                int bits = 0;
+                while ((1 << bits) < W) bits++;
+                timed(PH_HASH, [&] { ks.hash(Q, stream); });
+                timed(PH_XCHG, [&] {
+                    HIPCHK(hipMemsetAsync(s.ocnt, 0, 64 * 8, stream));
+                    launch_owner_keys(s.fp, s.G, (uint32_t)W, s.okey, s.iota, s.ocnt, stream);
+                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(s.tmp, s.tmp_bytes, s.okey, s.okey2, s.iota, s.perm,
+                                                              (int)s.G, 0, bits, stream));
+                    launch_gather_fp(s.fp, s.perm, s.G, s.sfp, stream);
+                });
+                HIPCHK(hipMemcpyAsync(s.hsum, s.ocnt, W * 8, hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipStreamSynchronize(stream));
+                collect_times(st);
+                for (int d = 0; d < W; d++) scnt[li][d] = s.hsum[d];
+                level_gen += s.G;
+            }
+            for (size_t li = 0; li < NL; li++) {
+                soff[li][0] = 0;
+                for (int d = 0; d < W; d++) soff[li][d + 1] = soff[li][d] + scnt[li][d];
+            }
+            exchange_counts(scnt, rcnt);
+            for (size_t li = 0; li < NL; li++) {
+                roff[li][0] = 0;
+                for (int q = 0; q < W; q++) roff[li][q + 1] = roff[li][q] + rcnt[li][q];
+                grow_recv(sh[li], roff[li][W]);
+                sendp[li] = sh[li].sfp;
+                recvp[li] = sh[li].rfp;
+            }
+            timed(PH_XCHG, [&] { exchange_items(sendp, scnt, soff, recvp, roff, 16); });
+            // (B) owners: seen-set probe + election of the first (source, j) per fingerprint
+            for (size_t li = 0; li < NL; li++) {
+                Shard &o = sh[li];
+                const uint64_t R = roff[li][W];
+                if (!R) continue;
+                uint32_t Rv = (uint32_t)R;
+                HIPCHK(hipMemcpyAsync(o.rcount, &Rv, 4, hipMemcpyHostToDevice, stream));
+                uint64_t Lcap = std::min(next_pow2(2 * R), Lcap_max);
+                if (R * 2 > Lcap_max) throw Fail(RMC_E_CAPACITY, "owner receive batch exceeds the election table");
+                ++o.epoch;
+                timed(PH_DEDUP, [&] {
+                    launch_dedup(o.rfp, o.rcount, R, o.T, o.T_cap - 1, o.L, Lcap - 1, o.epoch, o.rlslot, stream);
+                    launch_recv_flags(o.rlslot, o.L, R, o.rflag, stream);
+                });
+                HIPCHK(hipStreamSynchronize(stream));
+            }
+            // flags back to the sources (reverse exchange)
+            for (size_t li = 0; li < NL; li++) { sendp[li] = sh[li].rflag; recvp[li] = sh[li].sflag; }
+            {
+                std::vector<std::vector<uint64_t>> rev(W, std::vector<uint64_t>(W, 0));
+                for (size_t li = 0; li < NL; li++)
+                    for (int q = 0; q < W; q++) rev[li][q] = rcnt[li][q];
+                timed(PH_XCHG, [&] { exchange_items(sendp, rev, roff, recvp, soff, 4); });
+            }
+            // (C) sources: winner positions in owner-grouped order, materialize into exchange records
+            for (size_t li = 0; li < NL; li++) {
+                Shard &s = sh[li];
+                std::fill(swin[li].begin(), swin[li].end(), 0);
+                if (!s.G) { std::fill(swoff[li].begin(), swoff[li].end(), 0); continue; }
+                HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.sflag, s.spos, (int)s.G + 1, stream));
+                std::vector<uint64_t> idx(W + 1);
+                for (int d = 0; d <= W; d++) idx[d] = soff[li][d];
+                HIPCHK(hipMemcpyAsync(s.pick_idx, idx.data(), (W + 1) * 8, hipMemcpyHostToDevice, stream));
+                launch_pick(s.spos, s.pick_idx, W + 1, s.sum, stream);
+                HIPCHK(hipMemcpyAsync(s.hsum, s.sum, (W + 1) * 8, hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipStreamSynchronize(stream));
+                for (int d = 0; d <= W; d++) swoff[li][d] = s.hsum[d];
+                for (int d = 0; d < W; d++) swin[li][d] = swoff[li][d + 1] - swoff[li][d];
+                grow_plain(s.sx, s.sx_cap, swoff[li][W] * XW + 1);
+                launch_scatter_flags(s.perm, s.sflag, s.spos, s.G, s.wflag, s.wpos, stream);
+                KParams Q = base(s);
+                Q.front = s.cur; Q.p_begin = s.p0; Q.p_end = s.p0 + s.np; Q.cnt = s.cnt; Q.off = s.off; Q.fp = s.fp;
+                Q.wflag = s.wflag; Q.wpos = s.wpos; Q.xrec = s.sx; Q.gid_parent_base = s.level_start[L - 1];
+                timed(PH_MAT, [&] { ks.materialize(Q, stream); });
+            }
+            exchange_counts(swin, rwin);
+            for (size_t li = 0; li < NL; li++) {
+                rwoff[li][0] = 0;
+                for (int q = 0; q < W; q++) rwoff[li][q + 1] = rwoff[li][q] + rwin[li][q];
+                grow_plain(sh[li].rx, sh[li].rx_cap, rwoff[li][W] * XW + 1);
+                sendp[li] = sh[li].sx;
+                recvp[li] = sh[li].rx;
+            }
+            timed(PH_XCHG, [&] { exchange_items(sendp, swin, swoff, recvp, rwoff, XW * 4); });
+            // (D) owners: append winners (source-major) to the next level, seen-set insert
+            for (size_t li = 0; li < NL; li++) {
+                Shard &o = sh[li];
+                const uint64_t n = rwoff[li][W];
+                const uint64_t gid_nxt = o.level_start[L - 1] + o.cur_n;
+                if (n) {
+                    grow_records(o.nxt, o.nxt_cap, o.nxt_n, o.nxt_n + n, RECW);
+                    grow_trace(o, gid_nxt + o.nxt_n + n);
+                    grow_seen(o, o.T_count + n);
+                    timed(PH_OTHER, [&] {
+                        for (int q = 0; q < W; q++) {
+                            const uint64_t k = rwin[li][q];
+                            if (!k) continue;
+                            launch_accept(o.rx + rwoff[li][q] * XW, k, (uint32_t)RECW, o.nxt + (o.nxt_n + rwoff[li][q]) * RECW,
+                                          o.par + gid_nxt + o.nxt_n + rwoff[li][q], o.pslot + gid_nxt + o.nxt_n + rwoff[li][q],
+                                          (uint64_t)q << 48, stream);
+                        }
+                        launch_insert_flagged(o.rfp, o.rflag, roff[li][W], o.T, o.T_cap - 1, stream);
+                    });
+                    o.nxt_n += n;
+                    o.T_count += n;
+                    level_new += n;
+                }
+            }
+            // errors: first in (source shard, parent, slot) order
+            std::vector<uint64_t> ebuf(2 * W, ~0ull);
+            for (size_t li = 0; li < NL; li++) {
+                Shard &s = sh[li];
+                HIPCHK(hipMemcpyAsync(s.hsum, s.err, ERR_NSLOTS * 8, hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipMemcpyAsync(s.hsum + 8, s.flags, 4, hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipStreamSynchronize(stream));
+                if ((uint32_t)s.hsum[8]) throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
+                unsigned long long best;
+                const int kind = first_error(s.hsum, &best);
+                if (kind >= 0) { ebuf[2 * s.id] = (uint64_t)kind; ebuf[2 * s.id + 1] = best; }
+                HIPCHK(hipMemsetAsync(s.err, 0xFF, ERR_NSLOTS * 8, stream));
+            }
+            if (!virt && W > 1) {
+                // gather every rank's (kind, key): ranks contribute only their own slots
+                std::vector<uint64_t> g(2 * W, 0);
+                for (int q = 0; q < 2 * W; q++) g[q] = (q / 2 == rank) ? ebuf[q] + 1 : 0;  // +1: ~0 -> 0
+                allreduce(g.data(), 2 * W, false);
+                for (int q = 0; q < 2 * W; q++) ebuf[q] = g[q] - 1;
+            }
+            for (int q = 0; q < W; q++) {
+                if (ebuf[2 * q] == ~0ull) continue;
+                uint64_t glob[2] = {level_gen, level_new};
+                allreduce(glob, 2, false);
+                stop_sharded(q, (int)ebuf[2 * q], ebuf[2 * q + 1], L, glob[0], glob[1], st);
+                st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                seconds += st->seconds;
+                return status;
+            }
+        }
+        uint64_t glob[2] = {level_gen, level_new};
+        allreduce(glob, 2, false);
+        total_generated += glob[0];
+        total_distinct += glob[1];
+        st->generated = glob[0];
+        st->new_states = glob[1];
+        for (Shard &s : sh) {
+            const uint64_t gid_nxt = s.level_start[L - 1] + s.cur_n;
+            std::swap(s.cur, s.nxt);
+            std::swap(s.cur_cap, s.nxt_cap);
+            s.cur_n = s.nxt_n;
+            s.nxt_n = 0;
+            s.level_start.push_back(gid_nxt);
+        }
+        if (glob[1]) {
+            depth = L + 1;
+        } else {
+            finished = true;
+            status = RMC_DONE;
+            queue_at_end = 0;
+        }
+        st->total_generated = total_generated;
+        st->total_distinct = total_distinct;
+        st->queue = glob[1];
+        st->status = finished ? RMC_DONE : RMC_OK;
+        st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        seconds += st->seconds;
+        return st->status;
+    }
+
+    // Sharded stop: the error's shard q, kind, key (parent in q's level, slot).  Counters are
+    // those at the end of the chunk (every chunk is processed by all shards together).
+    void stop_sharded(int q, int kind, unsigned long long ek, int L, uint64_t gen, uint64_t nw, rmc_level_stats *st) {
+        const uint64_t p = ek >> 24;
+        const uint32_t slot = (uint32_t)((ek >> 8) & 0xFFFF);
+        total_generated += gen;
+        total_distinct += nw;
+        uint64_t gid_cur = 0;
+        for (Shard &s : sh)
+            if (s.id == q) gid_cur = s.level_start[L - 1];
+        uint64_t g[1] = {virt ? gid_cur : (q == rank ? gid_cur : 0)};
+        allreduce(g, 1, false);
+        err_ref = ((uint64_t)q << 48) | (g[0] + p);
+        if (kind == ERR_INV || kind == ERR_EVAL) {
+            status = kind == ERR_INV ? RMC_VIOLATION : RMC_EVAL_ERROR;
+            violated = (int)(ek & 0xFF);
+            err_last_slot = slot;
+            depth = L + 1;
+        } else {
+            status = kind == ERR_ASSERT ? RMC_ASSERT : RMC_DEADLOCK;
+            err_last_slot = KEY_NONE;
+        }
+        queue_at_end = 0;
+        st->generated = gen;
+        st->new_states = nw;
+        st->total_generated = total_generated;
+        st->total_distinct = total_distinct;
+        st->status = status;
+        finished = true;
+        build_trace();
+    }
+
+    // parent reference and slot of a state (shard << 48 | local gid), from whichever rank holds it
+    void fetch_par(uint64_t ref, uint64_t *par, uint16_t *slot) {
+        const int q = (int)(ref >> 48);
+        const uint64_t gid = ref & ((1ull << 48) - 1);
+        uint64_t v[2] = {0, 0};
+        for (Shard &s : sh)
+            if (s.id == q) {
+                v[0] = d2h(s.par + gid) + 1;  // +1: the Init sentinel ~0 travels as 0
+                v[1] = d2h(s.pslot + gid);
+            }
+        allreduce(v, 2, false);
+        *par = v[0] - 1;
+        *slot = (uint16_t)v[1];
+    }
+
+    // Walk parent pointers from err_ref to Init, then replay the slots from Init.
     void build_trace() {
         std::vector<uint16_t> slots;
-        uint64_t g = err_gid;
-        while (g != 0) {
-            const uint64_t par = d2h(d_par + g);
-            slots.push_back(d2h(d_pslot + g));
+        if (err_last_slot != KEY_NONE) slots.push_back((uint16_t)err_last_slot);
+        uint64_t g = err_ref;
+        for (;;) {
+            uint64_t par;
+            uint16_t sl;
+            fetch_par(g, &par, &sl);
+            if (par == ~0ull) break;
+            slots.push_back(sl);
             g = par;
             if (slots.size() > 100000) throw Fail(RMC_E_STATE, "corrupt parent chain");
         }
@@ -839,18 +1287,21 @@ struct rmc_ctx {
 
     // Forget every explored state but keep all device buffers (repeat runs, benchmarks).
     void reset() {
-        HIPCHK(hipMemsetAsync(d_T, 0, T_cap * 16, stream));
+        for (Shard &s : sh) {
+            HIPCHK(hipMemsetAsync(s.T, 0, s.T_cap * 16, stream));
+            s.T_count = 0;
+            s.cur_n = s.nxt_n = 0;
+            s.level_start.clear();
+        }
         HIPCHK(hipStreamSynchronize(stream));
-        T_count = 0;
-        cur_n = 0;
-        level_start.clear();
         trace.clear();
         inited = finished = false;
         status = RMC_OK;
         depth = 0;
         total_generated = total_distinct = queue_at_end = 0;
         violated = -1;
-        err_gid = 0;
+        err_ref = 0;
+        err_last_slot = KEY_NONE;
         seconds = 0;
     }
 
@@ -860,7 +1311,9 @@ struct rmc_ctx {
         r->depth = depth;
         r->generated = total_generated;
         r->distinct = total_distinct;
-        r->queue = finished ? queue_at_end : cur_n;
+        uint64_t q = 0;
+        for (const Shard &s : sh) q += s.cur_n;
+        r->queue = finished ? queue_at_end : q;
         r->violated = violated;
         r->trace_len = (uint32_t)trace.size();
         r->seconds = seconds;
@@ -887,6 +1340,20 @@ static int guarded(rmc_ctx *c, F &&f) {
 extern "C" {
 
 int rmc_abi_version(void) { return RMC_ABI_VERSION; }
+
+int rmc_comm_unique_id(void *out128) {
+    if (!out128) return RMC_E_ARG;
+#ifdef RMC_WITH_RCCL
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return RMC_E_COMM;
+    static_assert(sizeof(id) <= 128, "ncclUniqueId larger than 128 bytes");
+    std::memset(out128, 0, 128);
+    std::memcpy(out128, &id, sizeof id);
+    return RMC_OK;
+#else
+    return RMC_E_COMM;
+#endif
+}
 
 int rmc_create(const rmc_config *cfg, void **out) {
     if (!cfg || !out) return RMC_E_ARG;
@@ -1020,7 +1487,7 @@ int rmc_fingerprint(void *ctx, const int32_t *unpacked, uint64_t fp[2]) {
         std::vector<uint32_t> rec(c->RECW);
         c->pack(unpacked, rec.data());
         HIPCHK(hipMemcpy(c->d_one, rec.data(), c->RECW * 4, hipMemcpyHostToDevice));
-        KParams P = c->base();
+        KParams P = c->base(c->sh[0]);
         P.front = c->d_one;
         P.fp = c->d_fp1;
         c->ks.fp_states(P, 1, c->stream);
@@ -1038,7 +1505,7 @@ int rmc_eval_invariant(void *ctx, const int32_t *unpacked, uint32_t bit, int32_t
         std::vector<uint32_t> rec(c->RECW);
         c->pack(unpacked, rec.data());
         HIPCHK(hipMemcpy(c->d_one, rec.data(), c->RECW * 4, hipMemcpyHostToDevice));
-        KParams P = c->base();
+        KParams P = c->base(c->sh[0]);
         P.front = c->d_one;
         c->ks.inv_states(P, 1, c->d_inv, c->stream);
         int32_t iv[7];

@@ -48,6 +48,8 @@ struct KParams {
     // errors: atomicMin keys (p << 16 | slot), level-local p
     unsigned long long *err;
     uint32_t *flags;           // [0] msg-cap overflow, [1] violated invariant bit, [2] eval-error invariant bit
+    // sharded mode: winners go to owner-grouped exchange records (RECW + 4 words each)
+    uint32_t *xrec;
     // single-state hook outputs
     uint32_t *out_keys;
     uint32_t *out_count;
@@ -73,6 +75,18 @@ void launch_winflag(const uint32_t *lslot, const unsigned long long *L, const ui
                     uint32_t *wflag, hipStream_t s);
 void launch_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned long long *err, const uint32_t *flags,
                     unsigned long long *out, hipStream_t s);
+void launch_owner_keys(const ulonglong2 *fp, uint64_t G, uint32_t W, uint32_t *key, uint32_t *iota,
+                       unsigned long long *cnt, hipStream_t s);
+void launch_gather_fp(const ulonglong2 *fp, const uint32_t *perm, uint64_t G, ulonglong2 *out, hipStream_t s);
+void launch_recv_flags(const uint32_t *lslot, const unsigned long long *L, uint64_t R, uint32_t *flag, hipStream_t s);
+void launch_scatter_flags(const uint32_t *perm, const uint32_t *sflag, const uint32_t *spos, uint64_t G,
+                          uint32_t *wflag, uint32_t *wpos, hipStream_t s);
+void launch_accept(const uint32_t *xrec, uint64_t n, uint32_t recw, uint32_t *next, uint64_t *par, uint16_t *pslot,
+                   uint64_t src_tag, hipStream_t s);
+void launch_insert_flagged(const ulonglong2 *fp, const uint32_t *flag, uint64_t n, ulonglong2 *T, uint64_t mask,
+                           hipStream_t s);
+void launch_pick(const uint32_t *a, const uint64_t *idx, int n, unsigned long long *out, hipStream_t s);
+void launch_owner_of(const ulonglong2 *fp, uint32_t W, uint32_t *out, hipStream_t s);
 void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, ulonglong2 *Tnew, uint64_t new_mask, hipStream_t s);
 void launch_insert_fps(const ulonglong2 *fp, uint64_t n, ulonglong2 *T, uint64_t Tmask, hipStream_t s);
 

@@ -799,6 +799,29 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
                     win = true;
                     out = rank[r];
                     P.out_keys[out] = cand[r].key;
+                } else if (P.xrec) {
+                    // sharded: the winner goes to its owner's exchange slot with a sidecar
+                    // (parent reference, slot key); the owner inserts it into its seen set
+                    const uint64_t j = P.off[pl] + rank[r];
+                    win = P.wflag[j] != 0;
+                    if (win) {
+                        out = P.wpos[j];
+                        uint32_t *side = P.xrec + out * (uint64_t)(S::RECW + 4) + S::RECW;
+                        {
+                            const uint64_t pref = P.gid_parent_base + p;
+                            side[0] = (uint32_t)pref;
+                            side[1] = (uint32_t)(pref >> 32);
+                            side[2] = cand[r].key;
+                            side[3] = 0;
+                        }
+                        int which = 0;
+                        const int iv = check_invs<N, V>(cand[r].c, P.inv_mask, &which);
+                        if (iv != 1) {
+                            const unsigned long long ek =
+                                ((((unsigned long long)p << 16) | cand[r].key) << 8) | (unsigned long long)which;
+                            atomicMin(&P.err[iv == 0 ? ERR_INV : ERR_EVAL], ek);
+                        }
+                    }
                 } else {
                     const uint64_t j = P.off[pl] + rank[r];
                     win = P.wflag[j] != 0;
@@ -818,10 +841,12 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
                     }
                 }
             }
+            const uint64_t stride = P.xrec ? (uint64_t)(S::RECW + 4) : (uint64_t)S::RECW;
+            uint32_t *dst = P.xrec ? P.xrec : P.next;
             for (uint64_t m = __ballot(win); m; m &= m - 1) {
                 const int t = __ffsll((unsigned long long)m) - 1;
                 const uint64_t ot = rdlane64(out, t);
-                write_record<N, V, MR>(W, cand[r], t, lane, P.next + ot * (uint64_t)S::RECW);
+                write_record<N, V, MR>(W, cand[r], t, lane, dst + ot * stride);
             }
         }
         if (MODE == M_SINGLE && lane == 0) *P.out_count = total;
@@ -1029,6 +1054,115 @@ void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, ulonglong2 *Tnew, u
 }
 void launch_insert_fps(const ulonglong2 *fp, uint64_t n, ulonglong2 *T, uint64_t Tmask, hipStream_t s) {
     hipLaunchKernelGGL(k_insert, dim3(grid256(n)), dim3(256), 0, s, fp, n, T, Tmask);
+}
+
+// ---- sharded exchange helpers (one GPU per owner shard) -------------------------------------
+// owner(fp) = hi bits of fp mod W -- independent of the seen-set index bits
+__device__ __forceinline__ uint32_t fp_owner(const ulonglong2 f, uint32_t W) {
+    return (uint32_t)((f.y >> 40) % W);
+}
+
+__global__ __launch_bounds__(256) void k_owner_keys(const ulonglong2 *__restrict__ fp, uint64_t G, uint32_t W,
+                                                    uint32_t *__restrict__ key, uint32_t *__restrict__ iota,
+                                                    unsigned long long *__restrict__ cnt) {
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < G; j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t o = fp_owner(fp[j], W);
+        key[j] = o;
+        iota[j] = (uint32_t)j;
+        atomicAdd(&cnt[o], 1ull);
+    }
+}
+
+// gather fingerprints into owner-grouped order (perm from a stable radix sort by owner)
+__global__ __launch_bounds__(256) void k_gather_fp(const ulonglong2 *__restrict__ fp, const uint32_t *__restrict__ perm,
+                                                   uint64_t G, ulonglong2 *__restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = fp[perm[i]];
+}
+
+// owner: winner flags of the received items (plain u32 0/1), from the chunk election table
+__global__ __launch_bounds__(256) void k_recv_flags(const uint32_t *__restrict__ lslot,
+                                                    const unsigned long long *__restrict__ L, uint64_t R,
+                                                    uint32_t *__restrict__ flag) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t g = lslot[i];
+        flag[i] = (g != 0xFFFFFFFFu && (uint32_t)L[g] == (uint32_t)i) ? 1u : 0u;
+    }
+}
+
+// source: flags/positions in owner-grouped order -> per successor j (TLC order within the chunk)
+__global__ __launch_bounds__(256) void k_scatter_flags(const uint32_t *__restrict__ perm,
+                                                       const uint32_t *__restrict__ sflag,
+                                                       const uint32_t *__restrict__ spos, uint64_t G,
+                                                       uint32_t *__restrict__ wflag, uint32_t *__restrict__ wpos) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t j = perm[i];
+        wflag[j] = sflag[i];
+        wpos[j] = spos[i];
+    }
+}
+
+// owner: append received winner records (record + 4-word sidecar) to the next level,
+// parent pointers to the trace arrays, fingerprints to the seen set
+__global__ __launch_bounds__(256) void k_accept(const uint32_t *__restrict__ xrec, uint64_t n, uint32_t recw,
+                                                uint32_t *__restrict__ next, uint64_t *__restrict__ par,
+                                                uint16_t *__restrict__ pslot, uint64_t src_tag) {
+    const uint64_t total = n * recw;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t q = i / recw, w = i - q * recw;
+        next[i] = xrec[q * (recw + 4) + w];
+        if (w == 0) {
+            const uint32_t *side = xrec + q * (recw + 4) + recw;
+            par[q] = src_tag | ((uint64_t)side[0] | ((uint64_t)side[1] << 32));
+            pslot[q] = (uint16_t)side[2];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_insert_flagged(const ulonglong2 *__restrict__ fp,
+                                                        const uint32_t *__restrict__ flag, uint64_t n, ulonglong2 *T,
+                                                        uint64_t mask) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        if (flag[i]) t_insert(T, mask, fp[i]);
+}
+
+// values at a list of indices (segment boundaries of scans) -> out
+__global__ void k_pick(const uint32_t *__restrict__ a, const uint64_t *__restrict__ idx, int n,
+                       unsigned long long *__restrict__ out) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = a[idx[i]];
+}
+
+__global__ void k_owner_of(const ulonglong2 *__restrict__ fp, uint32_t W, uint32_t *out) {
+    if (threadIdx.x == 0) out[0] = fp_owner(fp[0], W);
+}
+
+void launch_owner_keys(const ulonglong2 *fp, uint64_t G, uint32_t W, uint32_t *key, uint32_t *iota,
+                       unsigned long long *cnt, hipStream_t s) {
+    hipLaunchKernelGGL(k_owner_keys, dim3(grid256(G)), dim3(256), 0, s, fp, G, W, key, iota, cnt);
+}
+void launch_gather_fp(const ulonglong2 *fp, const uint32_t *perm, uint64_t G, ulonglong2 *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_gather_fp, dim3(grid256(G)), dim3(256), 0, s, fp, perm, G, out);
+}
+void launch_recv_flags(const uint32_t *lslot, const unsigned long long *L, uint64_t R, uint32_t *flag, hipStream_t s) {
+    hipLaunchKernelGGL(k_recv_flags, dim3(grid256(R)), dim3(256), 0, s, lslot, L, R, flag);
+}
+void launch_scatter_flags(const uint32_t *perm, const uint32_t *sflag, const uint32_t *spos, uint64_t G,
+                          uint32_t *wflag, uint32_t *wpos, hipStream_t s) {
+    hipLaunchKernelGGL(k_scatter_flags, dim3(grid256(G)), dim3(256), 0, s, perm, sflag, spos, G, wflag, wpos);
+}
+void launch_accept(const uint32_t *xrec, uint64_t n, uint32_t recw, uint32_t *next, uint64_t *par, uint16_t *pslot,
+                   uint64_t src_tag, hipStream_t s) {
+    hipLaunchKernelGGL(k_accept, dim3(grid256(n * recw)), dim3(256), 0, s, xrec, n, recw, next, par, pslot, src_tag);
+}
+void launch_insert_flagged(const ulonglong2 *fp, const uint32_t *flag, uint64_t n, ulonglong2 *T, uint64_t mask,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_insert_flagged, dim3(grid256(n)), dim3(256), 0, s, fp, flag, n, T, mask);
+}
+void launch_pick(const uint32_t *a, const uint64_t *idx, int n, unsigned long long *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_pick, dim3(1), dim3(256), 0, s, a, idx, n, out);
+}
+void launch_owner_of(const ulonglong2 *fp, uint32_t W, uint32_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_owner_of, dim3(1), dim3(64), 0, s, fp, W, out);
 }
 
 }  // namespace rmc

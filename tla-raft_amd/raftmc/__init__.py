@@ -46,6 +46,7 @@ class _Config(ctypes.Structure):
         ("spec_variant", ctypes.c_int32), ("device", ctypes.c_int32), ("msg_cap", ctypes.c_int32),
         ("seen_log2", ctypes.c_int32), ("no_symmetry", ctypes.c_int32), ("chunk_successors", ctypes.c_uint64),
         ("rank", ctypes.c_int32), ("world_size", ctypes.c_int32), ("comm_unique_id", ctypes.c_void_p),
+        ("virtual_shards", ctypes.c_int32),
     ]
 
 
@@ -86,6 +87,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.rmc_step.argtypes = [vp, P(_LevelStats)]
     lib.rmc_run.argtypes = [vp, P(_Result)]
     lib.rmc_reset.argtypes = [vp]
+    lib.rmc_comm_unique_id.argtypes = [vp]
     lib.rmc_get_result.argtypes = [vp, P(_Result)]
     lib.rmc_trace_len.argtypes = [vp, P(u32)]
     lib.rmc_trace_state.argtypes = [vp, u32, P(i32), ctypes.c_size_t, P(i32), P(i32), P(i32)]
@@ -116,6 +118,10 @@ class ModelConfig:
     msg_cap: int = 0
     seen_log2: int = 0
     chunk_successors: int = 0
+    virtual_shards: int = 0          # >1: that many fingerprint-owner shards on one device
+    rank: int = 0                    # multi-GPU: this process's rank
+    world_size: int = 1              # multi-GPU: ranks (one process per GPU)
+    comm_unique_id: Optional[bytes] = None  # 128 bytes from comm_unique_id() on rank 0
 
     def to_c(self) -> _Config:
         c = _Config()
@@ -132,7 +138,11 @@ class ModelConfig:
         c.seen_log2 = self.seen_log2
         c.no_symmetry = 0 if self.symmetry else 1
         c.chunk_successors = self.chunk_successors
-        c.rank, c.world_size = 0, 1
+        c.rank, c.world_size = self.rank, self.world_size
+        c.virtual_shards = self.virtual_shards
+        if self.comm_unique_id is not None:
+            self._idbuf = ctypes.create_string_buffer(bytes(self.comm_unique_id), 128)
+            c.comm_unique_id = ctypes.cast(self._idbuf, ctypes.c_void_p)
         return c
 
 
@@ -149,6 +159,16 @@ def parse_config(cfg_text: str, tla_text: Optional[str] = None) -> ModelConfig:
     return ModelConfig(n_servers=c.n_servers, n_vals=c.n_vals, max_election=c.max_election,
                        max_restart=c.max_restart, invariants=invs, check_deadlock=bool(c.check_deadlock),
                        spec_variant=c.spec_variant, symmetry=not c.no_symmetry)
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id for a multi-GPU run (rank 0 creates it, every rank passes it in)."""
+    lib = load_library()
+    buf = ctypes.create_string_buffer(128)
+    rc = lib.rmc_comm_unique_id(buf)
+    if rc != RMC_OK:
+        raise RmcError(f"rmc_comm_unique_id failed: {ERRORS.get(rc, rc)}")
+    return buf.raw
 
 
 # ------------------------------------------------------------------------------ unpacked states
