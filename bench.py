@@ -13,9 +13,12 @@ SYMMETRY symmServers, VIEW view, INVARIANT Inv, -deadlock (Max
 MaxElection, MaxLogLen is |Vals|+1).  configs[2]/[3] (Raft.cfg as shipped, 5 servers) do
 not fit one GPU (>2.1e9 states by BFS level 37, still growing).
 
-N>1 (torchrun, one process per GPU): each rank exhausts its own copy of the workload
-(replicas: the sharded seen-set exchange is not in this build), value = all ranks'
-distinct states / max-over-ranks time, scaling "weak".
+N>1 (torchrun, one process per GPU): the same workload is exhausted ONCE by all ranks
+together -- seen set and frontier sharded by fingerprint owner, one RCCL exchange of
+fingerprints / winner flags / winner records per chunk; value =
+distinct states of the whole run / max-over-ranks time, scaling "strong" (total work
+fixed).  If the RCCL path fails to initialise, each rank exhausts its own copy instead
+and the line says "replicas" with the error.
 """
 import argparse
 import ctypes
@@ -100,9 +103,38 @@ def main():
 
     import raftmc
     w = WORKLOADS[args.workload]
+    # HIP-event timing of the fingerprint kernel only (the dominant one; events on every phase
+    # would add host API calls to each BFS level of this latency-bound workload)
     cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
-                             invariants=("Inv",), check_deadlock=False, device=local)
-    mc = raftmc.ModelChecker(cfg)
+                             invariants=("Inv",), check_deadlock=False, device=local,
+                             timing_phases=1 << PHASES.index("expand_hash"))
+    parallelism = "single-gpu"
+    if world > 1:
+        # rank 0 creates the RCCL id; the control-plane group (gloo) broadcasts it
+        idt = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            idt = torch.tensor(list(raftmc.comm_unique_id()), dtype=torch.uint8)
+        dist.broadcast(idt, 0)
+        cfg.rank, cfg.world_size, cfg.comm_unique_id = rank, world, bytes(idt.tolist())
+        parallelism = f"sharded-rccl-{world}"
+    mc, err = None, ""
+    try:
+        mc = raftmc.ModelChecker(cfg)
+    except raftmc.RmcError as e:
+        if world == 1:
+            raise
+        err = str(e)
+    if world > 1:
+        ok = torch.tensor([0 if mc is None else 1], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same mode
+        if int(ok.item()) == 0:
+            print(f"rank {rank}: sharded RCCL path unavailable ({err or 'another rank failed'}); running replicas",
+                  file=sys.stderr, flush=True)
+            if mc is not None:
+                mc.close()
+            cfg.rank, cfg.world_size, cfg.comm_unique_id = 0, 1, None
+            mc = raftmc.ModelChecker(cfg)
+            parallelism = f"replicas (sharded RCCL init failed: {err or 'on another rank'})"
     res = None
     for _ in range(args.warmup):
         mc.reset()
@@ -137,7 +169,8 @@ def main():
         elapsed = float(t.item())
     assert res is not None and res.status == "done", res
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * res.distinct * args.steps / elapsed
+    units = res.distinct * (world if parallelism.startswith("replicas") else 1)
+    value = units * args.steps / elapsed
 
     # dominant kernel phase: the one with the most device time (HIP events on the engine's stream)
     S = record_bytes(mc)
@@ -158,13 +191,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if parallelism.startswith("replicas") else "strong",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic: the state space of Raft.tla itself, generated from Init on the GPU each step",
         "config": {"workload": w["desc"], "distinct_states": res.distinct, "states_generated": res.generated,
                    "depth": res.depth, "verdict": "Inv holds" if res.status == "done" else res.status,
-                   "parallelism": "replicas" if world > 1 else "single-gpu"},
+                   "parallelism": parallelism},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -80,6 +80,7 @@ typedef struct rmc_config {
     const void *comm_unique_id; /* 128-byte RCCL unique id (rmc_comm_unique_id on rank 0), same on every rank */
     int32_t virtual_shards;    /* > 1: run that many fingerprint-owner shards in this process on one device
                                   (the multi-GPU partition/exchange logic with device copies for transport) */
+    uint32_t timing_phases;    /* bit i: HIP-event time phase i into rmc_level_stats.kernel_ms (0 = all) */
 } rmc_config;
 
 /* Statistics of one BFS level (what TLC's progress line reports). */
@@ -140,6 +141,10 @@ int rmc_reset(void *ctx);
 /* Loop rmc_step until done or an error; fills the final result. */
 int rmc_run(void *ctx, rmc_result *res);
 int rmc_get_result(void *ctx, rmc_result *res);
+
+/* rmc_init + rmc_step until done inside the library (no per-level host round trip of the
+ * caller); per-level statistics go to levels[0..*n_levels) (as many as fit in cap). */
+int rmc_run_levels(void *ctx, rmc_level_stats *levels, uint32_t cap, uint32_t *n_levels, rmc_result *res);
 
 /* Counterexample (TLC's "The behavior up to this point is"): states 1..len from
  * Init to the error state.  Unpacked layout below.  action/server/witness

@@ -132,6 +132,8 @@ uint64_t next_pow2(uint64_t x) {
     return p;
 }
 
+constexpr uint64_t SMALL_SCAN = 1u << 12;  // one-workgroup scans below this size (one CU: tiny chunks only)
+
 enum Phase { PH_COUNT = 0, PH_HASH = 1, PH_DEDUP = 2, PH_MAT = 3, PH_XCHG = 4, PH_OTHER = 5 };
 
 struct TraceStep {
@@ -635,6 +637,7 @@ struct rmc_ctx {
     }
     template <class F>
     void timed(int ph, F &&f) {
+        if (cfg.timing_phases && !(cfg.timing_phases & (1u << ph))) { f(); return; }
         const int a = ev();
         HIPCHK(hipEventRecord(evpool[a], stream));
         f();
@@ -876,8 +879,11 @@ struct rmc_ctx {
             const uint32_t *Gp = s.off + np_;  // device-side successor count of the chunk
             timed(PH_COUNT, [&] {
                 ks.count(params(), stream);
-                // exclusive scan over np_+1 items: off[np_] = G (cnt[np_] is never read into it)
-                HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.cnt, s.off, (int)np_ + 1, stream));
+                // exclusive scan: off[np_] = G
+                if (np_ <= SMALL_SCAN)
+                    launch_scan_small(s.cnt, np_, s.off, stream);
+                else
+                    HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.cnt, s.off, (int)np_ + 1, stream));
             });
             // Small chunks run on an upper bound of G without a host round trip; large
             // ones read G back so that the dedup/scan passes are sized exactly.
@@ -896,8 +902,12 @@ struct rmc_ctx {
                 ++s.epoch;
                 timed(PH_DEDUP, [&] {
                     launch_dedup(s.fp, Gp, Gub, s.T, s.T_cap - 1, s.L, Lcap - 1, s.epoch, s.lslot, stream);
-                    launch_winflag(s.lslot, s.L, Gp, Gub, s.wflag, stream);
-                    HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.wflag, s.wpos, (int)Gub + 1, stream));
+                    if (Gub <= SMALL_SCAN) {
+                        launch_winscan_small(s.lslot, s.L, Gp, Gub, s.wflag, s.wpos, stream);
+                    } else {
+                        launch_winflag(s.lslot, s.L, Gp, Gub, s.wflag, stream);
+                        HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.wflag, s.wpos, (int)Gub + 1, stream));
+                    }
                 });
                 timed(PH_MAT, [&] { ks.materialize(params(), stream); });
             }
@@ -1403,6 +1413,25 @@ int rmc_reset(void *ctx) {
     return guarded(c, [&] {
         c->reset();
         return RMC_OK;
+    });
+}
+
+int rmc_run_levels(void *ctx, rmc_level_stats *levels, uint32_t cap, uint32_t *n_levels, rmc_result *res) {
+    rmc_ctx *c = (rmc_ctx *)ctx;
+    return guarded(c, [&] {
+        uint32_t n = 0;
+        rmc_level_stats tmp;
+        if (!c->inited) {
+            c->init(n < cap && levels ? &levels[n] : &tmp);
+            n++;
+        }
+        while (!c->finished) {
+            c->step(n < cap && levels ? &levels[n] : &tmp);
+            n++;
+        }
+        if (n_levels) *n_levels = n < cap ? n : cap;
+        if (res) c->result(res);
+        return c->status;
     });
 }
 

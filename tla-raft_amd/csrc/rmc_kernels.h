@@ -75,6 +75,9 @@ void launch_winflag(const uint32_t *lslot, const unsigned long long *L, const ui
                     uint32_t *wflag, hipStream_t s);
 void launch_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned long long *err, const uint32_t *flags,
                     unsigned long long *out, hipStream_t s);
+void launch_scan_small(const uint32_t *in, uint64_t n, uint32_t *out, hipStream_t s);
+void launch_winscan_small(const uint32_t *lslot, const unsigned long long *L, const uint32_t *Gp, uint64_t Gub,
+                          uint32_t *wflag, uint32_t *wpos, hipStream_t s);
 void launch_owner_keys(const ulonglong2 *fp, uint64_t G, uint32_t W, uint32_t *key, uint32_t *iota,
                        unsigned long long *cnt, hipStream_t s);
 void launch_gather_fp(const ulonglong2 *fp, const uint32_t *perm, uint64_t G, ulonglong2 *out, hipStream_t s);

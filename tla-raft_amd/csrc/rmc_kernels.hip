@@ -998,21 +998,66 @@ __global__ __launch_bounds__(256) void k_winflag(const uint32_t *__restrict__ ls
 }
 
 // one copy-back per chunk: G, W, error keys, flags
-__global__ void k_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned long long *err,
-                          const uint32_t *flags, unsigned long long *out) {
+__global__ void k_summary(const uint32_t *Gp, const uint32_t *wpos, unsigned long long *err, uint32_t *flags,
+                          unsigned long long *out) {
     if (threadIdx.x == 0) {
         const uint32_t G = *Gp;
         out[0] = G;
         out[1] = wpos[G];
-        for (int i = 0; i < ERR_NSLOTS; i++) out[2 + i] = err[i];
+        for (int i = 0; i < ERR_NSLOTS; i++) {
+            out[2 + i] = err[i];
+            err[i] = ~0ull;  // reset for the next chunk
+        }
         out[2 + ERR_NSLOTS] = flags[0];
+        flags[0] = 0;
     }
 }
 
-// reset the error words for the next chunk (after k_summary has copied them)
-__global__ void k_clear_err(unsigned long long *err, uint32_t *flags) {
-    if (threadIdx.x < ERR_NSLOTS) err[threadIdx.x] = ~0ull;
-    if (threadIdx.x == 0) flags[0] = 0;
+// One-workgroup exclusive scan for small chunks (n <= 64K): out[i] = sum in[0..i), out[n] = total.
+// WIN = true computes the winner flags inline (flag_j = L[lslot[j]] == j, k_winflag) and
+// also stores them, replacing the flag kernel + a two-kernel library scan.
+template <bool WIN>
+__global__ __launch_bounds__(1024) void k_scan_small(const uint32_t *__restrict__ in, const uint32_t *__restrict__ Gp,
+                                                     uint64_t nmax, const uint32_t *__restrict__ lslot,
+                                                     const unsigned long long *__restrict__ L,
+                                                     uint32_t *__restrict__ flags_out, uint32_t *__restrict__ out) {
+    __shared__ uint32_t wsum[16];
+    const uint32_t n = WIN ? *Gp : (uint32_t)nmax;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t per = (n + 1023) / 1024;
+    const uint32_t b = tid * per, e = min(n, b + per);
+    uint32_t local = 0;
+    for (uint32_t i = b; i < e; i++) {
+        uint32_t v;
+        if (WIN) {
+            const uint32_t g = lslot[i];
+            v = (g != 0xFFFFFFFFu && (uint32_t)L[g] == i) ? 1u : 0u;
+            flags_out[i] = v;
+        } else {
+            v = in[i];
+        }
+        local += v;
+    }
+    // exclusive scan of the 1024 thread sums: in-wave shuffles, then across the 16 waves
+    uint32_t x = local;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (uint32_t k = 0; k < wv; k++) wbase += wsum[k];
+    uint32_t run = wbase + x - local;
+    for (uint32_t i = b; i < e; i++) {
+        out[i] = run;
+        run += WIN ? flags_out[i] : in[i];
+    }
+    if (tid == 1023) out[n] = wbase + x;
+    if (WIN) {  // flags past the chunk's G stay zero for scans sized on an upper bound
+        for (uint64_t i = n + tid; i < nmax; i += 1024) flags_out[i] = 0;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_rehash(const ulonglong2 *__restrict__ Told, uint64_t old_cap, ulonglong2 *Tn,
@@ -1045,9 +1090,17 @@ void launch_winflag(const uint32_t *lslot, const unsigned long long *L, const ui
 }
 void launch_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned long long *err, const uint32_t *flags,
                     unsigned long long *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_summary, dim3(1), dim3(64), 0, s, Gp, wpos, err, flags, out);
-    hipLaunchKernelGGL(k_clear_err, dim3(1), dim3(64), 0, s, const_cast<unsigned long long *>(err),
-                       const_cast<uint32_t *>(flags));
+    hipLaunchKernelGGL(k_summary, dim3(1), dim3(64), 0, s, Gp, wpos, const_cast<unsigned long long *>(err),
+                       const_cast<uint32_t *>(flags), out);
+}
+void launch_scan_small(const uint32_t *in, uint64_t n, uint32_t *out, hipStream_t s) {
+    hipLaunchKernelGGL((k_scan_small<false>), dim3(1), dim3(1024), 0, s, in, (const uint32_t *)nullptr, n,
+                       (const uint32_t *)nullptr, (const unsigned long long *)nullptr, (uint32_t *)nullptr, out);
+}
+void launch_winscan_small(const uint32_t *lslot, const unsigned long long *L, const uint32_t *Gp, uint64_t Gub,
+                          uint32_t *wflag, uint32_t *wpos, hipStream_t s) {
+    hipLaunchKernelGGL((k_scan_small<true>), dim3(1), dim3(1024), 0, s, (const uint32_t *)nullptr, Gp, Gub, lslot, L,
+                       wflag, wpos);
 }
 void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, ulonglong2 *Tnew, uint64_t new_mask, hipStream_t s) {
     hipLaunchKernelGGL(k_rehash, dim3(grid256(old_cap)), dim3(256), 0, s, Told, old_cap, Tnew, new_mask);

@@ -46,7 +46,7 @@ class _Config(ctypes.Structure):
         ("spec_variant", ctypes.c_int32), ("device", ctypes.c_int32), ("msg_cap", ctypes.c_int32),
         ("seen_log2", ctypes.c_int32), ("no_symmetry", ctypes.c_int32), ("chunk_successors", ctypes.c_uint64),
         ("rank", ctypes.c_int32), ("world_size", ctypes.c_int32), ("comm_unique_id", ctypes.c_void_p),
-        ("virtual_shards", ctypes.c_int32),
+        ("virtual_shards", ctypes.c_int32), ("timing_phases", ctypes.c_uint32),
     ]
 
 
@@ -87,6 +87,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.rmc_step.argtypes = [vp, P(_LevelStats)]
     lib.rmc_run.argtypes = [vp, P(_Result)]
     lib.rmc_reset.argtypes = [vp]
+    lib.rmc_run_levels.argtypes = [vp, P(_LevelStats), u32, P(u32), P(_Result)]
     lib.rmc_comm_unique_id.argtypes = [vp]
     lib.rmc_get_result.argtypes = [vp, P(_Result)]
     lib.rmc_trace_len.argtypes = [vp, P(u32)]
@@ -122,6 +123,7 @@ class ModelConfig:
     rank: int = 0                    # multi-GPU: this process's rank
     world_size: int = 1              # multi-GPU: ranks (one process per GPU)
     comm_unique_id: Optional[bytes] = None  # 128 bytes from comm_unique_id() on rank 0
+    timing_phases: int = 0           # bit i: time phase i with HIP events (0 = all phases)
 
     def to_c(self) -> _Config:
         c = _Config()
@@ -140,6 +142,7 @@ class ModelConfig:
         c.chunk_successors = self.chunk_successors
         c.rank, c.world_size = self.rank, self.world_size
         c.virtual_shards = self.virtual_shards
+        c.timing_phases = self.timing_phases
         if self.comm_unique_id is not None:
             self._idbuf = ctypes.create_string_buffer(bytes(self.comm_unique_id), 128)
             c.comm_unique_id = ctypes.cast(self._idbuf, ctypes.c_void_p)
@@ -346,14 +349,13 @@ class ModelChecker:
         return ls
 
     def run(self) -> Result:
-        if not self._inited:
-            ls = self.init()
-            if ls.status != "ok":
-                return self.result()
-        while True:
-            ls = self.step()
-            if ls.status != "ok":
-                break
+        """Exhaust the state space (or stop at the first error) inside the library."""
+        cap = 4096
+        buf = (_LevelStats * cap)()
+        n = ctypes.c_uint32()
+        self._check(self.lib.rmc_run_levels(self.h, buf, cap, ctypes.byref(n), None))
+        self._inited = True
+        self.levels.extend(self._stats(buf[i]) for i in range(n.value))
         return self.result()
 
     def result(self) -> Result:
