@@ -178,8 +178,11 @@ def main():
     per_launch_ms = phase_ms[dom] / max(1, launches[dom])
     bytes_total = alg_bytes(PHASES[dom], Fs, Gs, Ns, S)
     achieved = bytes_total / max(1, launches[dom]) / (per_launch_ms / 1e3) / 1e9 if per_launch_ms > 0 else 0.0
+    traffic, pmc_src = pmc_traffic(mc, PHASES[dom], args.workload)
     roof = {"bound": "hbm", "kernel": PHASES[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+            "traffic_source": pmc_src,
+            "algorithmic_bytes_per_launch": round(bytes_total / max(1, launches[dom])),
             "avg_launch_ms": round(per_launch_ms, 5), "launches": launches[dom],
             "phase_ms_per_step": {PHASES[i]: round(phase_ms[i] / args.steps, 4) for i in range(4)}}
     line = {
@@ -207,6 +210,26 @@ def main():
     mc.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+KERNEL_MODE = {"expand_count": 0, "expand_hash": 1, "materialize": 2}
+
+
+def pmc_traffic(mc, phase, workload):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
+    (tools/pmc.sh + tools/pmc_summary.py, FETCH_SIZE x2 correction per MI355X_MICROARCH.md)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}.json")))
+    if not files or phase not in KERNEL_MODE:
+        return None, None
+    n, V = mc.cfg.n_servers, mc.cfg.n_vals
+    mr = 1 if (mc.cfg.msg_cap or (64 if n <= 3 else 128)) <= 64 else 2
+    name = f"void rmc::k_expand<{n}, {V}, {mr}, {KERNEL_MODE[phase]}>(rmc::KParams)"
+    d = json.load(open(files[-1]))
+    e = d.get(name)
+    if not e or "hbm_bytes_per_dispatch" not in e:
+        return None, None
+    return round(e["hbm_bytes_per_dispatch"]), os.path.relpath(files[-1], ROOT)
 
 
 def record_bytes(mc):
