@@ -42,17 +42,15 @@ HBM_PEAK_GBS = 8000.0
 PHASES = ["expand_count", "expand_hash", "dedup", "materialize", "exchange", "other"]
 
 
-def alg_bytes(phase, F, G, N, S):
-    """Algorithmic HBM bytes of one phase (DESIGN.md "Roofline"): F parents of S-byte records,
-    G generated successors, N new states."""
-    if phase == "expand_count":
-        return F * S + F * 4                    # read parent records, write per-parent counts
-    if phase == "expand_hash":
-        return F * S + G * 16                   # read parent records, write one 128-bit fingerprint per successor
-    if phase == "dedup":
-        return G * (16 + 16 + 4) + G * (4 + 8 + 4) + G * 8   # fp + seen-set probe + slot; winner flag; scan
-    if phase == "materialize":
-        return F * S + G * 8 + N * (16 + S + 16 + 10)       # parents, flags; per new state: fp, record, seen insert, trace
+def alg_bytes(phase, F, G, N, S, CWB):
+    """Algorithmic HBM bytes of one phase of the fused single-GPU level (DESIGN.md "Kernels"):
+    F parents of S-byte records, G generated successors, N new states, CWB core bytes."""
+    if phase == "expand_hash":   # k_expand<FUSED>: parents in; per successor: staged core + aux + fp + slot, one seen-set probe
+        return F * S + F * 8 + G * (CWB + 16 + 16 + 4) + G * 16
+    if phase == "dedup":         # k_elect + k_wincount + scan: fp, slot, election word per successor; counts per parent
+        return G * (4 + 16 + 8 + 4 + 8) + F * (4 + 4 + 8)
+    if phase == "materialize":   # k_commit: per parent wpos/cnt + parent ids; per new state: staging in, record out,
+        return F * (8 + 4) + F * (S - CWB) + N * (CWB + 16 + 4 + 8 + 16 + S + 16 + 10)  # seen insert, trace
     return 0
 
 
@@ -173,10 +171,10 @@ def main():
     value = units * args.steps / elapsed
 
     # dominant kernel phase: the one with the most device time (HIP events on the engine's stream)
-    S = record_bytes(mc)
+    S, CWB = record_bytes(mc)
     dom = max(range(4), key=lambda i: phase_ms[i])
     per_launch_ms = phase_ms[dom] / max(1, launches[dom])
-    bytes_total = alg_bytes(PHASES[dom], Fs, Gs, Ns, S)
+    bytes_total = alg_bytes(PHASES[dom], Fs, Gs, Ns, S, CWB)
     achieved = bytes_total / max(1, launches[dom]) / (per_launch_ms / 1e3) / 1e9 if per_launch_ms > 0 else 0.0
     traffic, pmc_src = pmc_traffic(mc, PHASES[dom], args.workload)
     roof = {"bound": "hbm", "kernel": PHASES[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -212,7 +210,8 @@ def main():
         dist.destroy_process_group()
 
 
-KERNEL_MODE = {"expand_count": 0, "expand_hash": 1, "materialize": 2}
+KERNEL_NAME = {"expand_hash": "void rmc::k_expand<{n}, {V}, {mr}, 4>(rmc::KParams)",
+               "materialize": "void rmc::k_commit<{n}, {V}, {mr}>(rmc::KParams)"}
 
 
 def pmc_traffic(mc, phase, workload):
@@ -220,11 +219,11 @@ def pmc_traffic(mc, phase, workload):
     (tools/pmc.sh + tools/pmc_summary.py, FETCH_SIZE x2 correction per MI355X_MICROARCH.md)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}.json")))
-    if not files or phase not in KERNEL_MODE:
+    if not files or phase not in KERNEL_NAME:
         return None, None
     n, V = mc.cfg.n_servers, mc.cfg.n_vals
     mr = 1 if (mc.cfg.msg_cap or (64 if n <= 3 else 128)) <= 64 else 2
-    name = f"void rmc::k_expand<{n}, {V}, {mr}, {KERNEL_MODE[phase]}>(rmc::KParams)"
+    name = KERNEL_NAME[phase].format(n=n, V=V, mr=mr)
     d = json.load(open(files[-1]))
     e = d.get(name)
     if not e or "hbm_bytes_per_dispatch" not in e:
@@ -233,11 +232,11 @@ def pmc_traffic(mc, phase, workload):
 
 
 def record_bytes(mc):
-    """Bytes of one packed state record (core words + message-id list), rmc_spec.h Layout."""
+    """(bytes of one packed state record, bytes of its core words), rmc_spec.h Layout."""
     n = mc.cfg.n_servers
     cw = (7 + 3 * n + 3) // 4 * 4
     mcap = mc.cfg.msg_cap or (64 if n <= 3 else 128)
-    return cw * 4 + 2 * mcap
+    return cw * 4 + 2 * mcap, cw * 4
 
 
 if __name__ == "__main__":

@@ -165,6 +165,10 @@ struct Shard {
     ulonglong2 *fp = nullptr;
     unsigned long long *L = nullptr;
     uint32_t epoch = 0;
+    // fused single-shard level: sparse successor staging (slot q = chunk parent * maxsucc + rank)
+    uint4 *score = nullptr, *saux = nullptr;
+    uint32_t *wcnt = nullptr;
+    unsigned long long *gsum = nullptr;
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
     // exchange buffers (W > 1)
@@ -466,7 +470,9 @@ struct rmc_ctx {
         d_seeds = dmalloc<uint64_t>(seeds.size());
         HIPCHK(hipMemcpy(d_seeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
 
-        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (virt ? (1ull << 23) : (1ull << 26));
+        // successor slots per chunk: dense for the sharded path, sparse (parents x maxsucc) for
+        // the fused single-GPU path, whose staging holds CW*4 + 36 bytes per slot
+        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (W > 1 ? (virt ? (1ull << 23) : (1ull << 26)) : (1ull << 25));
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 31)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^31");
         chunk_parents = Gcap / ks.maxsucc;
@@ -500,6 +506,12 @@ struct rmc_ctx {
         HIPCHK(hipMemsetAsync(s.wflag, 0, (Gcap + 1) * 4, stream));
         s.L = dmalloc<unsigned long long>(Lcap_max);
         HIPCHK(hipMemsetAsync(s.L, 0, Lcap_max * 8, stream));
+        if (W == 1) {
+            s.score = dmalloc<uint4>(Gcap * (uint64_t)(ks.CW / 4));
+            s.saux = dmalloc<uint4>(Gcap);
+            s.wcnt = dmalloc<uint32_t>(chunk_parents + 1);
+            s.gsum = dmalloc<unsigned long long>(WC_BLOCKS);
+        }
         size_t t1 = 0, t2 = 0;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, s.cnt, s.off, (int)Gcap + 1, stream));
         if (W > 1) {
@@ -542,6 +554,7 @@ struct rmc_ctx {
         dfree(s.okey2); dfree(s.iota); dfree(s.perm); dfree(s.sflag); dfree(s.spos); dfree(s.sfp); dfree(s.ocnt);
         dfree(s.rfp); dfree(s.rlslot); dfree(s.rflag); dfree(s.rpos); dfree(s.rcount); dfree(s.sx); dfree(s.rx);
         dfree(s.pick_idx); dfree(s.err); dfree(s.sum); dfree(s.flags);
+        dfree(s.score); dfree(s.saux); dfree(s.wcnt); dfree(s.gsum);
         if (s.hsum) (void)hipHostFree(s.hsum);
         s.hsum = nullptr;
     }
@@ -869,54 +882,50 @@ struct rmc_ctx {
         uint64_t nxt_n = 0, level_gen = 0;
         for (uint64_t p0 = 0; p0 < s.cur_n; p0 += chunk_parents) {
             const uint64_t p1 = std::min(s.cur_n, p0 + chunk_parents), np_ = p1 - p0;
+            // Small chunks size the next level, trace and seen set on the successor upper bound
+            // without a host round trip; large ones read the winner count back before commit.
+            const uint64_t Gub = np_ * (uint64_t)ks.maxsucc;
+            const bool small = Gub <= (1ull << 23);
+            if (small) {
+                grow_records(s.nxt, s.nxt_cap, nxt_n, nxt_n + Gub, RECW);
+                grow_trace(s, gid_nxt + nxt_n + Gub);
+                grow_seen(s, s.T_count + Gub);
+            }
+            const uint64_t Lcap = std::min(next_pow2(2 * Gub), Lcap_max);
+            ++s.epoch;
             auto params = [&] {
                 KParams Q = base(s);
-                Q.front = s.cur; Q.p_begin = p0; Q.p_end = p1; Q.cnt = s.cnt; Q.off = s.off; Q.fp = s.fp;
-                Q.wflag = s.wflag; Q.wpos = s.wpos; Q.next = s.nxt; Q.next_base = nxt_n;
+                Q.front = s.cur; Q.p_begin = p0; Q.p_end = p1; Q.cnt = s.cnt; Q.fp = s.fp;
+                Q.wpos = s.wpos; Q.wcnt = s.wcnt; Q.gsum = s.gsum; Q.next = s.nxt; Q.next_base = nxt_n;
                 Q.gid_next_base = gid_nxt; Q.gid_parent_base = gid_cur;
+                Q.score = s.score; Q.saux = s.saux; Q.lslot = s.lslot; Q.L = s.L; Q.Lmask = Lcap - 1;
+                Q.epoch = s.epoch;
                 return Q;
             };
-            const uint32_t *Gp = s.off + np_;  // device-side successor count of the chunk
-            timed(PH_COUNT, [&] {
-                ks.count(params(), stream);
-                // exclusive scan: off[np_] = G
+            // expand + fingerprint + seen-set probe + staging, one evaluation per parent
+            timed(PH_HASH, [&] { ks.fused(params(), stream); });
+            timed(PH_DEDUP, [&] {
+                ks.elect(params(), np_, stream);
+                ks.wincount(params(), np_, stream);
                 if (np_ <= SMALL_SCAN)
-                    launch_scan_small(s.cnt, np_, s.off, stream);
+                    launch_scan_small(s.wcnt, np_, s.wpos, stream);
                 else
-                    HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.cnt, s.off, (int)np_ + 1, stream));
+                    HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.wcnt, s.wpos, (int)np_ + 1, stream));
             });
-            // Small chunks run on an upper bound of G without a host round trip; large
-            // ones read G back so that the dedup/scan passes are sized exactly.
-            uint64_t Gub = np_ * (uint64_t)ks.maxsucc;
-            if (Gub > (1ull << 20)) {
-                Gub = d2h(Gp);
+            if (!small) {
+                const uint64_t Wub = d2h(s.wpos + np_);
                 collect_times(st);
+                grow_records(s.nxt, s.nxt_cap, nxt_n, nxt_n + Wub, RECW);
+                grow_trace(s, gid_nxt + nxt_n + Wub);
+                grow_seen(s, s.T_count + Wub);
             }
-            grow_records(s.nxt, s.nxt_cap, nxt_n, nxt_n + Gub, RECW);
-            grow_trace(s, gid_nxt + nxt_n + Gub);
-            grow_seen(s, s.T_count + Gub);
-            if (Gub) {
-                timed(PH_HASH, [&] { ks.hash(params(), stream); });
-                uint64_t Lcap = next_pow2(2 * Gub);
-                if (Lcap > Lcap_max) Lcap = Lcap_max;
-                ++s.epoch;
-                timed(PH_DEDUP, [&] {
-                    launch_dedup(s.fp, Gp, Gub, s.T, s.T_cap - 1, s.L, Lcap - 1, s.epoch, s.lslot, stream);
-                    if (Gub <= SMALL_SCAN) {
-                        launch_winscan_small(s.lslot, s.L, Gp, Gub, s.wflag, s.wpos, stream);
-                    } else {
-                        launch_winflag(s.lslot, s.L, Gp, Gub, s.wflag, stream);
-                        HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.wflag, s.wpos, (int)Gub + 1, stream));
-                    }
-                });
-                timed(PH_MAT, [&] { ks.materialize(params(), stream); });
-            }
-            launch_summary(Gp, s.wpos, s.err, s.flags, s.sum, stream);
+            timed(PH_MAT, [&] { ks.commit(params(), stream); });
+            launch_summary_fused(s.gsum, wincount_blocks(np_), s.wpos + np_, s.err, s.flags, s.sum, stream);
             HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
             HIPCHK(hipGetLastError());
             collect_times(st);
-            const uint64_t G = s.hsum[0], Wn = Gub ? s.hsum[1] : 0;
+            const uint64_t G = s.hsum[0], Wn = s.hsum[1];
             if (s.hsum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
             level_gen += G;
             s.T_count += Wn;
@@ -961,7 +970,25 @@ struct rmc_ctx {
         const uint64_t p = ek >> 24;                       // level-local parent
         const uint32_t slot = (uint32_t)((ek >> 8) & 0xFFFF);
         const int which = (int)(ek & 0xFF);
-        const uint32_t off_p = d2h(s.off + (p - p0));
+        const uint64_t pl = p - p0;
+        // successors of the chunk's parents before p, and winners before p
+        uint64_t off_p = 0;
+        if (pl) {
+            std::vector<uint32_t> cn(pl);
+            HIPCHK(hipMemcpy(cn.data(), s.cnt, pl * 4, hipMemcpyDeviceToHost));
+            for (uint32_t x : cn) off_p += x;
+        }
+        const uint64_t wbase = d2h(s.wpos + pl);
+        // winners among p's first `upto` successor slots (election table of this chunk)
+        auto winners_in = [&](uint32_t upto) -> uint64_t {
+            if (!upto) return 0;
+            std::vector<uint32_t> ls(upto);
+            HIPCHK(hipMemcpy(ls.data(), s.lslot + pl * ks.maxsucc, upto * 4, hipMemcpyDeviceToHost));
+            uint64_t w = 0;
+            for (uint32_t r = 0; r < upto; r++)
+                if (ls[r] < LS_ELECT && (uint32_t)d2h(s.L + ls[r]) == (uint32_t)(pl * ks.maxsucc + r)) w++;
+            return w;
+        };
         // successors of p, in order, to find the sub-action batch boundaries
         HIPCHK(hipMemcpy(d_one, s.cur + p * RECW, RECW * 4, hipMemcpyDeviceToDevice));
         std::vector<uint32_t> keys;
@@ -979,8 +1006,7 @@ struct rmc_ctx {
             gen += batch_end;  // TLC adds the whole sub-action's batch before fingerprinting it
             uint32_t rank_ = 0;
             for (uint32_t k : keys) rank_ += k < slot;
-            const uint32_t j = off_p + rank_;
-            winners_before = d2h(s.wpos + j);
+            winners_before = wbase + winners_in(rank_);
             err_ref = gid_nxt + nxt_before + winners_before;
             total_distinct += nxt_before + winners_before + 1;
             queue_at_end = (s.cur_n - p - 1) + nxt_before + winners_before;
@@ -989,8 +1015,7 @@ struct rmc_ctx {
             depth = (int)s.level_start.size() + 1;
         } else {
             if (kind == ERR_ASSERT) gen += cut;  // the failing sub-action's batch is never counted
-            const uint32_t jcut = off_p + (kind == ERR_ASSERT ? cut : 0);
-            winners_before = d2h(s.wpos + jcut);
+            winners_before = wbase + (kind == ERR_ASSERT ? winners_in(cut) : 0);
             err_ref = gid_cur + p;
             total_distinct += nxt_before + winners_before;
             queue_at_end = (s.cur_n - p - 1) + nxt_before + winners_before;

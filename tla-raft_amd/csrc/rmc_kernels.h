@@ -50,6 +50,19 @@ struct KParams {
     uint32_t *flags;           // [0] msg-cap overflow, [1] violated invariant bit, [2] eval-error invariant bit
     // sharded mode: winners go to owner-grouped exchange records (RECW + 4 words each)
     uint32_t *xrec;
+    // fused single-shard level: expand (+hash, +seen-set probe, +staging) -> elect -> wincount
+    // -> scan -> commit.  Successor slot q = (p - p_begin) * maxsucc + rank is sparse and
+    // increases in TLC order; it indexes fp, lslot, score (core words, CW/4 uint4 each) and
+    // saux {key | nadd << 16, add0 | add1 << 16, add2 | add3 << 16, 0}.  wpos is then the
+    // exclusive scan of wcnt (winners per parent).
+    uint4 *score;
+    uint4 *saux;
+    uint32_t *lslot;           // LS_SEEN, LS_ELECT, or the election slot in L
+    unsigned long long *L;     // chunk election table, (epoch << 32) | q
+    uint64_t Lmask;
+    uint32_t epoch;
+    uint32_t *wcnt;            // winners per parent (chunk-local), [np] = 0
+    unsigned long long *gsum;  // successors generated in the chunk
     // single-state hook outputs
     uint32_t *out_keys;
     uint32_t *out_count;
@@ -61,6 +74,10 @@ struct KernelSet {
     void (*hash)(const KParams &, hipStream_t);
     void (*materialize)(const KParams &, hipStream_t);
     void (*single)(const KParams &, hipStream_t);           // all successors of front[0] -> next, fp, out_keys
+    void (*fused)(const KParams &, hipStream_t);            // expand + hash + probe + staging (one pass)
+    void (*elect)(const KParams &, uint64_t np, hipStream_t);     // first-in-TLC-order election per fingerprint
+    void (*wincount)(const KParams &, uint64_t np, hipStream_t);  // winners per parent, successors generated
+    void (*commit)(const KParams &, hipStream_t);           // winners -> next level, seen set, trace, invariants
     void (*fp_states)(const KParams &, uint64_t n, hipStream_t);  // fp of front[0..n) -> fp
     void (*inv_states)(const KParams &, uint64_t n, int32_t *out, hipStream_t); // per state: 1/0/-1 for inv_mask bits
 };
@@ -75,6 +92,16 @@ void launch_winflag(const uint32_t *lslot, const unsigned long long *L, const ui
                     uint32_t *wflag, hipStream_t s);
 void launch_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned long long *err, const uint32_t *flags,
                     unsigned long long *out, hipStream_t s);
+// fused level: summary = {successors generated (sum of the wincount blocks' partial sums),
+// winners (wpos[np]), error keys (then reset), flags (then reset)}
+void launch_summary_fused(const unsigned long long *gsum, unsigned nblocks, const uint32_t *wtotal,
+                          unsigned long long *err, uint32_t *flags, unsigned long long *out, hipStream_t s);
+constexpr uint32_t LS_SEEN = 0xFFFFFFFFu, LS_ELECT = 0xFFFFFFFEu;
+constexpr unsigned WC_BLOCKS = 1024;  // max blocks of the wincount pass (= partial sums in gsum)
+inline unsigned wincount_blocks(uint64_t np) {
+    const uint64_t b = (np + 255) / 256;
+    return (unsigned)(b < WC_BLOCKS ? (b ? b : 1) : WC_BLOCKS);
+}
 void launch_scan_small(const uint32_t *in, uint64_t n, uint32_t *out, hipStream_t s);
 void launch_winscan_small(const uint32_t *lslot, const unsigned long long *L, const uint32_t *Gp, uint64_t Gub,
                           uint32_t *wflag, uint32_t *wpos, hipStream_t s);

@@ -23,7 +23,7 @@
 
 namespace rmc {
 
-enum Mode { M_COUNT = 0, M_HASH = 1, M_MAT = 2, M_SINGLE = 3 };
+enum Mode { M_COUNT = 0, M_HASH = 1, M_MAT = 2, M_SINGLE = 3, M_FUSED = 4 };
 
 template <int N>
 __device__ __forceinline__ uint32_t sel(const uint32_t *a, int i) {
@@ -49,6 +49,8 @@ struct Spec {
     static constexpr int NADD = (N > 1) ? N - 1 : 1;
     static constexpr int SLOTS_PER_SERVER = 4 + V + (N - 1);  // BC BL CR*V LAE*(N-1) LCC RS
     static_assert(N * SLOTS_PER_SERVER <= 64, "non-message slots must fit one wave");
+    static constexpr int MAXS = MCAP + N * SLOTS_PER_SERVER;  // successor slots per parent (sparse stride)
+    static constexpr int CW4 = CW / 4;                         // core words as uint4
 };
 
 // per-lane successor candidate
@@ -614,6 +616,20 @@ __device__ __forceinline__ uint64_t t_index(const ulonglong2 f, uint64_t mask) {
     return (f.y ^ (f.y >> 29) ^ (f.x >> 23)) & mask;
 }
 
+__device__ __forceinline__ bool t_contains(const ulonglong2 *T, uint64_t mask, ulonglong2 f) {
+    uint64_t h = t_index(f, mask);
+    for (;;) {
+        const ulonglong2 e = T[h];
+        if (e.x == 0ull) return false;
+        if (e.x == f.x && e.y == f.y) return true;
+        h = (h + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ uint64_t l_index(const ulonglong2 f, uint64_t mask) {
+    return (f.x ^ (f.x >> 31) ^ (f.y >> 7)) & mask;
+}
+
 __device__ __forceinline__ void t_insert(ulonglong2 *T, uint64_t mask, ulonglong2 f) {
     uint64_t h = t_index(f, mask);
     for (;;) {
@@ -627,8 +643,9 @@ template <int N, int V, int MR, int MODE>
 __global__ __launch_bounds__(64) void k_expand(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
-    constexpr bool SUMS = (MODE == M_HASH || MODE == M_SINGLE);
+    constexpr bool SUMS = (MODE == M_HASH || MODE == M_SINGLE || MODE == M_FUSED);
     __shared__ uint16_t ids[S::MCAP];
+    __shared__ ulonglong2 sPart[SUMS ? 64 : 1];         // partial minima per (successor, permutation block)
     __shared__ uint64_t M0[N * N], M1[N * N];
     __shared__ uint32_t pcore[Lo::NW + N];
     constexpr int NPM = SUMS ? factorial(N) : 1;        // |Permutations(Servers)| (tla:21)
@@ -682,7 +699,7 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
         }
         const uint64_t pl = p - P.p_begin;  // chunk-local parent index
         uint64_t am = 0;
-        if (MODE == M_COUNT || MODE == M_SINGLE) {
+        if (MODE == M_COUNT || MODE == M_SINGLE || MODE == M_FUSED) {
             bool ovf = false;
 #pragma unroll
             for (int r = 0; r <= MR; r++) ovf |= cand[r].key != KEY_NONE && W.nm + cand[r].nadd > (uint32_t)S::MCAP;
@@ -697,14 +714,37 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
                 if (lane == 0) atomicMin(&P.err[ERR_ASSERT], (((unsigned long long)p << 16) | best) << 8);
             }
         }
-        if (MODE == M_COUNT) {
+        if (MODE == M_COUNT || MODE == M_FUSED) {
             if (lane == 0) {
                 P.cnt[pl] = total;
                 if (total == 0 && !am && P.check_deadlock) atomicMin(&P.err[ERR_DEADLOCK], ((unsigned long long)p << 16) << 8);
             }
-            continue;
+            if (MODE == M_COUNT) continue;
         }
-        if (MODE == M_HASH || MODE == M_SINGLE) {
+        if (MODE == M_FUSED) {
+            // stage every enabled successor at its slot q: core words (|msgs| already updated)
+            // and the message ids it adds -- commit merges them into the parent's id list
+#pragma unroll
+            for (int r = 0; r <= MR; r++) {
+                if (cand[r].key == KEY_NONE) continue;
+                const Succ<N, V, MR> &o = cand[r];
+                const uint64_t q = pl * (uint64_t)S::MAXS + rank[r];
+                uint32_t cw[S::CW];
+#pragma unroll
+                for (int w = 0; w < S::CW; w++) {
+                    if (w < Lo::NW) cw[w] = o.c[w]; else cw[w] = 0u;
+                }
+                cw[Lo::W_MISC] = (cw[Lo::W_MISC] & ~0xFF0000u) | ((W.nm + o.nadd) << 16);
+                uint4 *dst = P.score + q * (uint64_t)S::CW4;
+#pragma unroll
+                for (int k = 0; k < S::CW4; k++) dst[k] = make_uint4(cw[4 * k], cw[4 * k + 1], cw[4 * k + 2], cw[4 * k + 3]);
+                uint32_t a[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int k = 0; k < S::NADD; k++) a[k] = o.add[k];
+                P.saux[q] = make_uint4(o.key | (o.nadd << 16), a[0] | (a[1] << 16), a[2] | (a[3] << 16), 0u);
+            }
+        }
+        if (SUMS) {
             // (a) parent row terms Rt[f][p][s] = Z_f(pi(s), U[s]) + sum_j Z_f(pi(s), pi(j), X_f[s][j])
             //     and their per-permutation totals Tt[f][p]  (structured hash, rmc_spec.h)
             const int np = P.t.np;
@@ -756,39 +796,66 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
                 Tt[1][pp] = t1;
             }
             __syncthreads();
-            // (c) one lane per successor: min over permutations of (parent total - old row + new row)
-            const uint64_t base = (MODE == M_HASH) ? P.off[pl] : 0;
-            for (uint32_t b = 0; b < total; b += 64) {
-                const uint32_t l = b + lane;
-                if (l >= total) break;
-                const uint32_t sv = sS[l];
-                const uint64_t u = sU[l];
-                uint64_t x0[N], x1[N];
+            // (c) one (successor l, permutation block b) task per lane: the lane takes the minimum
+            //     over permutations b, b + PB, ... of (parent total - old row + new row), and the PB
+            //     partial minima of a successor meet in LDS.  PB = 64 / total (at most |perms|)
+            //     keeps all 64 lanes busy when a parent has few successors -- the common case.
+            const uint32_t npu = (uint32_t)np;
+            uint32_t PB = 1;
+            if (total > 0 && total < 64) PB = min(64u / total, npu);
+            const uint32_t SB = 64u / PB;  // successors per round
+            const uint32_t li = (uint32_t)lane / PB, blk = (uint32_t)lane - li * PB;
+            for (uint32_t b0 = 0; b0 < total; b0 += SB) {
+                const uint32_t l = b0 + li;
+                uint64_t m0 = ~0ull, m1 = ~0ull;
+                if (li < SB && l < total) {
+                    const uint32_t sv = sS[l];
+                    const uint64_t u = sU[l];
+                    uint64_t x0[N], x1[N];
 #pragma unroll
-                for (int j = 0; j < N; j++) { x0[j] = sX[0][l * N + j]; x1[j] = sX[1][l * N + j]; }
-                uint64_t b0 = ~0ull, b1 = ~0ull;
-                for (int pp = 0; pp < np; pp++) {
-                    uint32_t img[N];
+                    for (int j = 0; j < N; j++) { x0[j] = sX[0][l * N + j]; x1[j] = sX[1][l * N + j]; }
+                    for (uint32_t pp = blk; pp < npu; pp += PB) {
+                        uint32_t img[N];
 #pragma unroll
-                    for (int j = 0; j < N; j++) img[j] = pimg[pp * N + j];
-                    uint32_t imgs = img[0];
+                        for (int j = 0; j < N; j++) img[j] = pimg[pp * N + j];
+                        uint32_t imgs = img[0];
 #pragma unroll
-                    for (int j = 1; j < N; j++) imgs = ((uint32_t)j == sv) ? img[j] : imgs;
-                    uint64_t h0 = Tt[0][pp] - Rt[0][pp * N + sv] + mix64(u ^ sdS[0][imgs]);
-                    uint64_t h1 = Tt[1][pp] - Rt[1][pp * N + sv] + mix64(u ^ sdS[1][imgs]);
+                        for (int j = 1; j < N; j++) imgs = ((uint32_t)j == sv) ? img[j] : imgs;
+                        uint64_t h0 = Tt[0][pp] - Rt[0][pp * N + sv] + mix64(u ^ sdS[0][imgs]);
+                        uint64_t h1 = Tt[1][pp] - Rt[1][pp * N + sv] + mix64(u ^ sdS[1][imgs]);
 #pragma unroll
-                    for (int j = 0; j < N; j++) {
-                        if ((uint32_t)j == sv) continue;
-                        const uint32_t q = imgs * N + img[j];
-                        h0 += mix64(x0[j] ^ sdP[0][q]);
-                        h1 += mix64(x1[j] ^ sdP[1][q]);
+                        for (int j = 0; j < N; j++) {
+                            if ((uint32_t)j == sv) continue;
+                            const uint32_t q = imgs * N + img[j];
+                            h0 += mix64(x0[j] ^ sdP[0][q]);
+                            h1 += mix64(x1[j] ^ sdP[1][q]);
+                        }
+                        if (h1 < m1 || (h1 == m1 && h0 < m0)) { m1 = h1; m0 = h0; }
                     }
-                    if (h1 < b1 || (h1 == b1 && h0 < b0)) { b1 = h1; b0 = h0; }
                 }
-                P.fp[base + l] = make_ulonglong2(b0 | 1ull, b1);
+                sPart[lane] = make_ulonglong2(m0, m1);
+                __syncthreads();
+                const uint32_t lo = b0 + (uint32_t)lane;
+                if ((uint32_t)lane < SB && lo < total) {
+                    ulonglong2 best = sPart[lane * PB];
+                    for (uint32_t k = 1; k < PB; k++) {
+                        const ulonglong2 v = sPart[lane * PB + k];
+                        if (v.y < best.y || (v.y == best.y && v.x < best.x)) best = v;
+                    }
+                    const ulonglong2 f = make_ulonglong2(best.x | 1ull, best.y);
+                    if (MODE == M_FUSED) {
+                        // the seen set is read-only in this launch (commit inserts)
+                        const uint64_t q = pl * (uint64_t)S::MAXS + lo;
+                        P.fp[q] = f;
+                        P.lslot[q] = t_contains(P.T, P.Tmask, f) ? LS_SEEN : LS_ELECT;
+                    } else {
+                        P.fp[((MODE == M_HASH) ? (uint64_t)P.off[pl] : 0ull) + lo] = f;
+                    }
+                }
+                __syncthreads();
             }
         }
-        if (MODE == M_HASH) continue;
+        if (MODE == M_HASH || MODE == M_FUSED) continue;
         // MATERIALIZE / SINGLE: write chosen successors
 #pragma unroll
         for (int r = 0; r <= MR; r++) {
@@ -885,6 +952,177 @@ __global__ __launch_bounds__(64) void k_inv_states(KParams P, uint64_t n, int32_
     for (int b = 0; b < 7; b++) out[i * 7 + b] = inv_eval<N, V>(c, b);
 }
 
+// ---- fused level: election, winner counts, commit --------------------------------------------
+// Thread per sparse successor slot q = pl * MAXS + r (r < cnt[pl]): elect the first slot in TLC
+// order (smallest q) per fingerprint not yet in the seen set.  L slots hold (epoch << 32) | q; a
+// slot of another epoch is empty, so the table is never cleared.  fp was written by the previous
+// launch, so reading another slot's fingerprint needs no fence.
+template <int N, int V, int MR>
+__global__ __launch_bounds__(256) void k_elect(KParams P, uint64_t np) {
+    using S = Spec<N, V, MR>;
+    const uint64_t nq = np * (uint64_t)S::MAXS;
+    const unsigned long long tag = (unsigned long long)P.epoch << 32;
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t pl = q / S::MAXS;
+        const uint32_t r = (uint32_t)(q - pl * S::MAXS);
+        if (r >= P.cnt[pl] || P.lslot[q] != LS_ELECT) continue;
+        const ulonglong2 f = P.fp[q];
+        uint64_t g = l_index(f, P.Lmask);
+        const unsigned long long mine = tag | q;
+        for (;;) {
+            unsigned long long v = __hip_atomic_load(&P.L[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((v >> 32) != P.epoch) {
+                const unsigned long long prev = atomicCAS(&P.L[g], v, mine);
+                if (prev == v) break;
+                v = prev;
+            }
+            if ((v >> 32) == P.epoch) {
+                const ulonglong2 o = P.fp[(uint32_t)v];
+                if (o.x == f.x && o.y == f.y) { atomicMin(&P.L[g], mine); break; }
+            }
+            g = (g + 1) & P.Lmask;
+        }
+        P.lslot[q] = (uint32_t)g;
+    }
+}
+
+// Thread per parent: winners per parent (wcnt) and, per block, the successors generated
+// (gsum[blockIdx.x]; the summary adds the partial sums -- one atomic per wave on a single
+// counter serialises at the memory side and cost more than the whole pass).
+template <int N, int V, int MR>
+__global__ __launch_bounds__(256) void k_wincount(KParams P, uint64_t np) {
+    using S = Spec<N, V, MR>;
+    __shared__ uint32_t wsum[4];
+    if (blockIdx.x == 0 && threadIdx.x == 0) P.wcnt[np] = 0;  // scan input past the last parent
+    uint32_t gen = 0;
+    for (uint64_t pl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; pl < np; pl += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t t = P.cnt[pl];
+        uint32_t w = 0;
+        for (uint32_t r = 0; r < t; r++) {
+            const uint64_t q = pl * (uint64_t)S::MAXS + r;
+            const uint32_t g = P.lslot[q];
+            w += (g < LS_ELECT && (uint32_t)P.L[g] == (uint32_t)q) ? 1u : 0u;
+        }
+        P.wcnt[pl] = w;
+        gen += t;
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) gen += __shfl_down(gen, d, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = gen;
+    __syncthreads();
+    if (threadIdx.x == 0) P.gsum[blockIdx.x] = (unsigned long long)wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// Write the staged successor held by lane t as a record at rec_out (whole wave): core words
+// from lane t's registers, message ids = parent ids (per lane) merged with the added ids.
+template <int N, int V, int MR>
+__device__ __forceinline__ void write_staged(const uint32_t *id, uint32_t nm, const uint32_t *c, const uint4 ax, int t,
+                                             int lane, uint32_t *rec_out) {
+    using S = Spec<N, V, MR>;
+    const uint32_t nadd = rdlane(ax.x, t) >> 16;
+    const uint32_t ay = rdlane(ax.y, t), az = rdlane(ax.z, t);
+    const uint32_t add[4] = {ay & 0xFFFFu, ay >> 16, az & 0xFFFFu, az >> 16};
+    uint32_t v = 0;
+#pragma unroll
+    for (int w = 0; w < S::CW; w++) {
+        const uint32_t x = rdlane(c[w], t);
+        v = (lane == w) ? x : v;
+    }
+    if (lane < S::CW) rec_out[lane] = v;
+    uint16_t *oid = reinterpret_cast<uint16_t *>(rec_out + S::CW);
+#pragma unroll
+    for (int r = 0; r < MR; r++) {
+        const uint32_t k = (uint32_t)(r * 64 + lane);
+        if (k < nm) {
+            uint32_t pos = k;
+#pragma unroll
+            for (int a = 0; a < S::NADD; a++) pos += ((uint32_t)a < nadd && add[a] < id[r]) ? 1u : 0u;
+            oid[pos] = (uint16_t)id[r];
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < S::NADD; a++) {
+        if ((uint32_t)a >= nadd) break;
+        uint32_t less = 0;
+#pragma unroll
+        for (int r = 0; r < MR; r++)
+            less += (uint32_t)__popcll(__ballot((uint32_t)(r * 64 + lane) < nm && id[r] < add[a]));
+#pragma unroll
+        for (int b = 0; b < S::NADD; b++) less += ((uint32_t)b < nadd && add[b] < add[a]) ? 1u : 0u;
+        if (lane == 0) oid[less] = (uint16_t)add[a];
+    }
+}
+
+// One wave per parent with winners: copy each winner (in TLC order) from staging into the next
+// level at next_base + wpos[pl] + i, insert its fingerprint, record its parent pointer and slot
+// key, and check the INVARIANTs (Raft.cfg:33) on it.
+template <int N, int V, int MR>
+__global__ __launch_bounds__(64) void k_commit(KParams P) {
+    using S = Spec<N, V, MR>;
+    using Lo = Layout<N, V>;
+    const int lane = threadIdx.x;
+    const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
+        const uint64_t pl = p - P.p_begin;
+        const uint32_t w0 = P.wpos[pl];
+        if (P.wpos[pl + 1] == w0) continue;
+        const uint32_t *rec = P.front + p * (uint64_t)S::RECW;
+        const uint32_t nm = (rec[Lo::W_MISC] >> 16) & 0xFFu;
+        const uint16_t *rid = reinterpret_cast<const uint16_t *>(rec + S::CW);
+        uint32_t id[MR];
+#pragma unroll
+        for (int r = 0; r < MR; r++) {
+            const uint32_t k = (uint32_t)(r * 64 + lane);
+            id[r] = k < nm ? (uint32_t)rid[k] : 0xFFFFu;
+        }
+        const uint32_t t = P.cnt[pl];
+        uint32_t done = 0;
+        for (uint32_t r0 = 0; r0 < t; r0 += 64) {
+            const uint32_t r = r0 + (uint32_t)lane;
+            const uint64_t q = pl * (uint64_t)S::MAXS + r;
+            bool win = false;
+            if (r < t) {
+                const uint32_t g = P.lslot[q];
+                win = g < LS_ELECT && (uint32_t)P.L[g] == (uint32_t)q;
+            }
+            const uint64_t m = __ballot(win);
+            if (!m) continue;
+            uint32_t c[S::CW];
+            uint4 ax = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+            for (int w = 0; w < S::CW; w++) c[w] = 0u;
+            if (win) {
+                const uint4 *src = P.score + q * (uint64_t)S::CW4;
+#pragma unroll
+                for (int k = 0; k < S::CW4; k++) {
+                    const uint4 x = src[k];
+                    c[4 * k] = x.x; c[4 * k + 1] = x.y; c[4 * k + 2] = x.z; c[4 * k + 3] = x.w;
+                }
+                ax = P.saux[q];
+                const uint32_t key = ax.x & 0xFFFFu;
+                const uint64_t out = P.next_base + w0 + done + (uint32_t)__popcll(m & lt_mask);
+                const uint64_t gid = P.gid_next_base + out;
+                t_insert(P.T, P.Tmask, P.fp[q]);
+                P.par[gid] = P.gid_parent_base + p;
+                P.pslot[gid] = (uint16_t)key;
+                int which = 0;
+                const int iv = check_invs<N, V>(c, P.inv_mask, &which);
+                if (iv != 1) {
+                    const unsigned long long ek = ((((unsigned long long)p << 16) | key) << 8) | (unsigned long long)which;
+                    atomicMin(&P.err[iv == 0 ? ERR_INV : ERR_EVAL], ek);
+                }
+            }
+            uint32_t i = 0;
+            for (uint64_t mm = m; mm; mm &= mm - 1, i++) {
+                const int tt = __ffsll((unsigned long long)mm) - 1;
+                write_staged<N, V, MR>(id, nm, c, ax, tt, lane,
+                                       P.next + (P.next_base + w0 + done + i) * (uint64_t)S::RECW);
+            }
+            done += (uint32_t)__popcll(m);
+        }
+    }
+}
+
 static inline unsigned grid_for(uint64_t n) {
     const uint64_t cap = 256ull * 32ull;  // 32 one-wave blocks per CU on 256 CUs
     return (unsigned)(n < cap ? (n ? n : 1) : cap);
@@ -904,6 +1142,22 @@ struct Launch {
     static void single(const KParams &P, hipStream_t s) {
         hipLaunchKernelGGL((k_expand<N, V, MR, M_SINGLE>), dim3(1), dim3(64), 0, s, P);
     }
+    static void fused(const KParams &P, hipStream_t s) {
+        hipLaunchKernelGGL((k_expand<N, V, MR, M_FUSED>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
+    }
+    static unsigned slot_grid(uint64_t np) {
+        const uint64_t b = (np * (uint64_t)Spec<N, V, MR>::MAXS + 255) / 256, cap = 256ull * 16ull;
+        return (unsigned)(b < cap ? (b ? b : 1) : cap);
+    }
+    static void elect(const KParams &P, uint64_t np, hipStream_t s) {
+        hipLaunchKernelGGL((k_elect<N, V, MR>), dim3(slot_grid(np)), dim3(256), 0, s, P, np);
+    }
+    static void wincount(const KParams &P, uint64_t np, hipStream_t s) {
+        hipLaunchKernelGGL((k_wincount<N, V, MR>), dim3(wincount_blocks(np)), dim3(256), 0, s, P, np);
+    }
+    static void commit(const KParams &P, hipStream_t s) {
+        hipLaunchKernelGGL((k_commit<N, V, MR>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
+    }
     static void fps(const KParams &P, uint64_t n, hipStream_t s) {
         hipLaunchKernelGGL((k_fp_states<N, V, MR>), dim3(grid_for(n)), dim3(64), 0, s, P, n);
     }
@@ -921,6 +1175,10 @@ static void fill(KernelSet *ks) {
     ks->hash = &Launch<N, V, MR>::hash;
     ks->materialize = &Launch<N, V, MR>::mat;
     ks->single = &Launch<N, V, MR>::single;
+    ks->fused = &Launch<N, V, MR>::fused;
+    ks->elect = &Launch<N, V, MR>::elect;
+    ks->wincount = &Launch<N, V, MR>::wincount;
+    ks->commit = &Launch<N, V, MR>::commit;
     ks->fp_states = &Launch<N, V, MR>::fps;
     ks->inv_states = &Launch<N, V, MR>::invs;
 }
@@ -1013,6 +1271,29 @@ __global__ void k_summary(const uint32_t *Gp, const uint32_t *wpos, unsigned lon
     }
 }
 
+// fused level: one copy-back per chunk: successors generated (then zeroed), winners, errors, flags
+__global__ __launch_bounds__(256) void k_summary_fused(const unsigned long long *gsum, unsigned nb,
+                                                       const uint32_t *wtotal, unsigned long long *err,
+                                                       uint32_t *flags, unsigned long long *out) {
+    __shared__ unsigned long long part[4];
+    unsigned long long g = 0;
+    for (unsigned i = threadIdx.x; i < nb; i += 256) g += gsum[i];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) g += __shfl_down(g, d, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = g;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        out[0] = part[0] + part[1] + part[2] + part[3];
+        out[1] = *wtotal;
+        for (int i = 0; i < ERR_NSLOTS; i++) {
+            out[2 + i] = err[i];
+            err[i] = ~0ull;
+        }
+        out[2 + ERR_NSLOTS] = flags[0];
+        flags[0] = 0;
+    }
+}
+
 // One-workgroup exclusive scan for small chunks (n <= 64K): out[i] = sum in[0..i), out[n] = total.
 // WIN = true computes the winner flags inline (flag_j = L[lslot[j]] == j, k_winflag) and
 // also stores them, replacing the flag kernel + a two-kernel library scan.
@@ -1092,6 +1373,10 @@ void launch_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned lon
                     unsigned long long *out, hipStream_t s) {
     hipLaunchKernelGGL(k_summary, dim3(1), dim3(64), 0, s, Gp, wpos, const_cast<unsigned long long *>(err),
                        const_cast<uint32_t *>(flags), out);
+}
+void launch_summary_fused(const unsigned long long *gsum, unsigned nblocks, const uint32_t *wtotal,
+                          unsigned long long *err, uint32_t *flags, unsigned long long *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_summary_fused, dim3(1), dim3(256), 0, s, gsum, nblocks, wtotal, err, flags, out);
 }
 void launch_scan_small(const uint32_t *in, uint64_t n, uint32_t *out, hipStream_t s) {
     hipLaunchKernelGGL((k_scan_small<false>), dim3(1), dim3(1024), 0, s, in, (const uint32_t *)nullptr, n,
