@@ -81,6 +81,8 @@ typedef struct rmc_config {
     int32_t virtual_shards;    /* > 1: run that many fingerprint-owner shards in this process on one device
                                   (the multi-GPU partition/exchange logic with device copies for transport) */
     uint32_t timing_phases;    /* bit i: HIP-event time phase i into rmc_level_stats.kernel_ms (0 = all) */
+    uint32_t device_levels;    /* single GPU: BFS levels enqueued per host round trip by rmc_run /
+                                  rmc_run_levels (0 = auto, 1 = the host drives every level) */
 } rmc_config;
 
 /* Statistics of one BFS level (what TLC's progress line reports). */
@@ -133,6 +135,18 @@ int rmc_init(void *ctx, rmc_level_stats *st);
  * seen-set insertion with TLC -workers 1 first-discovery order, INVARIANT check
  * on new states (Raft.cfg:33).  Returns RMC_OK, RMC_DONE or an error status. */
 int rmc_step(void *ctx, rmc_level_stats *st);
+
+/* As many BFS levels as one host round trip covers: on a single GPU up to
+ * cfg.device_levels levels enqueued back to back, each level's kernels taking its
+ * size from the previous level's commit on the device (stopping early at the end,
+ * an error, or a level that needs larger buffers); otherwise one rmc_step.
+ * Per-level statistics go to levels[0..*n); cap >= 1.  Same return as rmc_step for
+ * the last level reported. */
+int rmc_steps(void *ctx, rmc_level_stats *levels, uint32_t cap, uint32_t *n);
+
+/* Phase timing from now on: 0 = off (no HIP events between kernels), 0xFFFFFFFF = every
+ * phase, otherwise a mask as cfg.timing_phases. */
+int rmc_set_timing(void *ctx, uint32_t phases);
 
 /* Forget every explored state (seen set, levels, trace) but keep the device
  * buffers, so the next rmc_init starts a fresh run (TLC: a new invocation). */

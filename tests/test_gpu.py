@@ -141,6 +141,43 @@ def test_results_independent_of_chunking_and_seen_growth():
         mc.close()
 
 
+@pytest.mark.parametrize("device_levels", [1, 2, 3])
+@pytest.mark.parametrize("name", sorted(LEVELS))
+def test_device_level_loop_matches_golden(name, device_levels):
+    """Host-driven levels (1) and device-driven batches of 2 / 3 levels (odd and even
+    frontier-buffer swaps, a batch boundary every few levels) give TLC's results."""
+    g = LEVELS[name]
+    mc, res = run_cfg(g, device_levels=device_levels)
+    check_levels(g, res)
+    if name in TRACES:
+        tr = mc.trace()
+        assert [st for _, st in tr] == [e["state"] for e in TRACES[name]["steps"]]
+    mc.close()
+
+
+def test_steps_api_batches_levels():
+    """rmc_steps hands back several levels per host round trip on one GPU, and the
+    per-level statistics equal the host-driven ones."""
+    g = LEVELS["n3_v1_e2_r3"]
+    mk = lambda **kw: raftmc.ModelChecker(raftmc.ModelConfig(n_servers=3, n_vals=1, max_election=2, max_restart=3,
+                                                             **kw))
+    a, b = mk(), mk(device_levels=1)
+    a.init(); b.init()
+    la, calls = [], 0
+    while True:
+        got = a.steps()
+        calls += 1
+        la += got
+        if got[-1].status != "ok":
+            break
+    lb = [b.step() for _ in range(len(la))]
+    assert calls < len(la)
+    assert [(x.level, x.expanded, x.generated, x.new_states, x.queue) for x in la] == \
+           [(x.level, x.expanded, x.generated, x.new_states, x.queue) for x in lb]
+    assert a.result().distinct == g["distinct"]
+    a.close(); b.close()
+
+
 def test_seeded_trace_independent_of_chunking():
     g = LEVELS["seeded_n3_v1_e2_r3"]
     mc, res = run_cfg(g, chunk_successors=6000, seen_log2=10)

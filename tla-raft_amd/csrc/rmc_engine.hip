@@ -132,7 +132,6 @@ uint64_t next_pow2(uint64_t x) {
     return p;
 }
 
-constexpr uint64_t SMALL_SCAN = 1u << 12;  // one-workgroup scans below this size (one CU: tiny chunks only)
 
 enum Phase { PH_COUNT = 0, PH_HASH = 1, PH_DEDUP = 2, PH_MAT = 3, PH_XCHG = 4, PH_OTHER = 5 };
 
@@ -167,8 +166,10 @@ struct Shard {
     uint32_t epoch = 0;
     // fused single-shard level: sparse successor staging (slot q = chunk parent * maxsucc + rank)
     uint4 *score = nullptr, *saux = nullptr;
-    uint32_t *wcnt = nullptr;
-    unsigned long long *gsum = nullptr;
+    uint32_t *wcnt = nullptr, *bw = nullptr, *bg = nullptr, *boff = nullptr, *tickets = nullptr;
+    // device-driven level loop: control block, per-level records, and their pinned host copies
+    LevelCtl *ctl = nullptr, *hctl = nullptr, *hsnap = nullptr;
+    LevelRec *lrec = nullptr, *hlrec = nullptr;
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
     // exchange buffers (W > 1)
@@ -214,6 +215,8 @@ struct rmc_ctx {
     uint64_t chunk_parents = 0, Gcap = 0, Lcap_max = 0;
 
     std::vector<hipEvent_t> evpool;
+    std::vector<hipEvent_t> gev;  // device-loop group snapshots
+    bool timing_on = true;        // rmc_set_timing
     struct EvRec { int ph; int a, b; };
     std::vector<EvRec> evrecs;
     int evused = 0;
@@ -258,6 +261,16 @@ struct rmc_ctx {
         P.par = s.par;
         P.pslot = s.pslot;
         return P;
+    }
+
+    // fused single-shard level: the chunk buffers every kernel of the level shares
+    KParams chunk_params(const Shard &s, const uint32_t *front, uint32_t *next) const {
+        KParams Q = base(s);
+        Q.front = front; Q.next = next;
+        Q.cnt = s.cnt; Q.fp = s.fp; Q.wpos = s.wpos; Q.wcnt = s.wcnt;
+        Q.bw = s.bw; Q.bg = s.bg; Q.boff = s.boff; Q.tickets = s.tickets; Q.sum = s.sum;
+        Q.score = s.score; Q.saux = s.saux; Q.lslot = s.lslot; Q.L = s.L;
+        return Q;
     }
 
     // ---- packing (unpacked int32 interchange <-> record) ------------------------------
@@ -476,6 +489,7 @@ struct rmc_ctx {
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 31)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^31");
         chunk_parents = Gcap / ks.maxsucc;
+        if (W == 1) chunk_parents = std::min<uint64_t>(chunk_parents, (uint64_t)WTILE * 1024);  // winner-count tiles
         Lcap_max = next_pow2(2 * Gcap);
 
         sh.resize(virt ? W : 1);
@@ -510,7 +524,16 @@ struct rmc_ctx {
             s.score = dmalloc<uint4>(Gcap * (uint64_t)(ks.CW / 4));
             s.saux = dmalloc<uint4>(Gcap);
             s.wcnt = dmalloc<uint32_t>(chunk_parents + 1);
-            s.gsum = dmalloc<unsigned long long>(WC_BLOCKS);
+            s.bw = dmalloc<uint32_t>(1024);
+            s.bg = dmalloc<uint32_t>(1024);
+            s.boff = dmalloc<uint32_t>(1024);
+            s.tickets = dmalloc<uint32_t>(4);
+            HIPCHK(hipMemsetAsync(s.tickets, 0, 16, stream));
+            s.ctl = dmalloc<LevelCtl>(1);
+            s.lrec = dmalloc<LevelRec>(LREC_CAP);
+            HIPCHK(hipHostMalloc((void **)&s.hctl, sizeof(LevelCtl), hipHostMallocDefault));
+            HIPCHK(hipHostMalloc((void **)&s.hsnap, 3 * sizeof(LevelCtl), hipHostMallocDefault));
+            HIPCHK(hipHostMalloc((void **)&s.hlrec, sizeof(LevelRec) * LREC_CAP, hipHostMallocDefault));
         }
         size_t t1 = 0, t2 = 0;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, s.cnt, s.off, (int)Gcap + 1, stream));
@@ -554,9 +577,13 @@ struct rmc_ctx {
         dfree(s.okey2); dfree(s.iota); dfree(s.perm); dfree(s.sflag); dfree(s.spos); dfree(s.sfp); dfree(s.ocnt);
         dfree(s.rfp); dfree(s.rlslot); dfree(s.rflag); dfree(s.rpos); dfree(s.rcount); dfree(s.sx); dfree(s.rx);
         dfree(s.pick_idx); dfree(s.err); dfree(s.sum); dfree(s.flags);
-        dfree(s.score); dfree(s.saux); dfree(s.wcnt); dfree(s.gsum);
+        dfree(s.score); dfree(s.saux); dfree(s.wcnt); dfree(s.bw); dfree(s.bg); dfree(s.boff); dfree(s.tickets);
+        dfree(s.ctl); dfree(s.lrec);
         if (s.hsum) (void)hipHostFree(s.hsum);
-        s.hsum = nullptr;
+        if (s.hctl) (void)hipHostFree(s.hctl);
+        if (s.hsnap) (void)hipHostFree(s.hsnap);
+        if (s.hlrec) (void)hipHostFree(s.hlrec);
+        s.hsum = nullptr; s.hctl = nullptr; s.hsnap = nullptr; s.hlrec = nullptr;
     }
 
     void release() {
@@ -569,6 +596,8 @@ struct rmc_ctx {
         h_red = nullptr;
         for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
         evpool.clear();
+        for (hipEvent_t e : gev) (void)hipEventDestroy(e);
+        gev.clear();
 #ifdef RMC_WITH_RCCL
         if (comm) (void)ncclCommDestroy(comm);
         comm = nullptr;
@@ -650,7 +679,7 @@ struct rmc_ctx {
     }
     template <class F>
     void timed(int ph, F &&f) {
-        if (cfg.timing_phases && !(cfg.timing_phases & (1u << ph))) { f(); return; }
+        if (!timing_on || (cfg.timing_phases && !(cfg.timing_phases & (1u << ph)))) { f(); return; }
         const int a = ev();
         HIPCHK(hipEventRecord(evpool[a], stream));
         f();
@@ -894,11 +923,10 @@ struct rmc_ctx {
             const uint64_t Lcap = std::min(next_pow2(2 * Gub), Lcap_max);
             ++s.epoch;
             auto params = [&] {
-                KParams Q = base(s);
-                Q.front = s.cur; Q.p_begin = p0; Q.p_end = p1; Q.cnt = s.cnt; Q.fp = s.fp;
-                Q.wpos = s.wpos; Q.wcnt = s.wcnt; Q.gsum = s.gsum; Q.next = s.nxt; Q.next_base = nxt_n;
+                KParams Q = chunk_params(s, s.cur, s.nxt);
+                Q.p_begin = p0; Q.p_end = p1; Q.next_base = nxt_n;
                 Q.gid_next_base = gid_nxt; Q.gid_parent_base = gid_cur;
-                Q.score = s.score; Q.saux = s.saux; Q.lslot = s.lslot; Q.L = s.L; Q.Lmask = Lcap - 1;
+                Q.Lmask = Lcap - 1;
                 Q.epoch = s.epoch;
                 return Q;
             };
@@ -907,20 +935,15 @@ struct rmc_ctx {
             timed(PH_DEDUP, [&] {
                 ks.elect(params(), np_, stream);
                 ks.wincount(params(), np_, stream);
-                if (np_ <= SMALL_SCAN)
-                    launch_scan_small(s.wcnt, np_, s.wpos, stream);
-                else
-                    HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.wcnt, s.wpos, (int)np_ + 1, stream));
             });
             if (!small) {
-                const uint64_t Wub = d2h(s.wpos + np_);
+                const uint64_t Wub = d2h(s.sum + 1);
                 collect_times(st);
                 grow_records(s.nxt, s.nxt_cap, nxt_n, nxt_n + Wub, RECW);
                 grow_trace(s, gid_nxt + nxt_n + Wub);
                 grow_seen(s, s.T_count + Wub);
             }
-            timed(PH_MAT, [&] { ks.commit(params(), stream); });
-            launch_summary_fused(s.gsum, wincount_blocks(np_), s.wpos + np_, s.err, s.flags, s.sum, stream);
+            timed(PH_MAT, [&] { ks.commit(params(), stream); });  // + chunk summary
             HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
             HIPCHK(hipGetLastError());
@@ -963,6 +986,163 @@ struct rmc_ctx {
         return st->status;
     }
 
+    // ---- device-driven levels (single GPU) ---------------------------------------------
+    // Up to `maxl` levels are enqueued with no host round trip: each level's commit writes the
+    // next level's parent count, id bases, epoch and table size into the control block that the
+    // following kernels read, and stops the loop on an empty level, an error, or a level whose
+    // successor bound might not fit the buffers (the host then grows them and carries on).
+    int batch_levels() const { return cfg.device_levels ? (int)cfg.device_levels : LREC_CAP; }
+    uint64_t dev_parents() const { return std::min<uint64_t>(chunk_parents, 1ull << 15); }
+    bool batch_ok() const {
+        return W == 1 && inited && !finished && cfg.device_levels != 1 && sh[0].cur_n > 0 &&
+               sh[0].cur_n <= dev_parents();
+    }
+
+    // Returns the number of level stats written to out[0..maxl] (the error level included).
+    int step_batch(rmc_level_stats *out, int maxl) {
+        auto t0 = std::chrono::steady_clock::now();
+        Shard &s = sh[0];
+        const uint64_t DP = dev_parents(), MS = (uint64_t)ks.maxsucc;
+        const int K = std::max(1, std::min(maxl, LREC_CAP));
+        // capacities with headroom for several levels; the first level always fits
+        const uint64_t target = std::min(std::max<uint64_t>(s.cur_n * MS * 32, 1ull << 16), DP * MS);
+        grow_records(s.cur, s.cur_cap, s.cur_n, target, RECW);
+        grow_records(s.nxt, s.nxt_cap, 0, target, RECW);
+        const int L0 = (int)s.level_start.size();
+        const uint64_t gid0 = s.level_start[L0 - 1];
+        grow_trace(s, gid0 + s.cur_n + 4 * target);
+        grow_seen(s, s.T_count + 2 * target);
+        LevelCtl &h = *s.hctl;
+        std::memset(&h, 0, sizeof h);
+        h.cur_n = s.cur_n;
+        h.gid_cur = gid0;
+        h.T_count = s.T_count;
+        h.Lmask = std::min(next_pow2(2 * s.cur_n * MS), Lcap_max) - 1;
+        h.nxt_cap = std::min(s.cur_cap, s.nxt_cap);
+        h.trace_cap = s.trace_cap;
+        h.T_cap = s.T_cap;
+        h.chunk_parents = DP;
+        h.Lcap_max = Lcap_max;
+        h.level = (uint32_t)L0;
+        h.epoch = ++s.epoch;
+        h.stop = CTL_RUN;
+        h.batch = (uint32_t)K;
+        HIPCHK(hipMemcpyAsync(s.ctl, &h, sizeof h, hipMemcpyHostToDevice, stream));
+        uint32_t *bufs[2] = {s.cur, s.nxt};
+        std::vector<size_t> mark(K);
+        // Levels go in groups; after each group a snapshot of the control block is copied back
+        // with an event.  Group g + 2 is enqueued only once group g's snapshot says the loop is
+        // still running, so the device always has a group queued and at most two groups of
+        // no-op launches follow the last level.
+        const int GL = 4, ngroups = (K + GL - 1) / GL;
+        while ((int)gev.size() < 3) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            gev.push_back(e);
+        }
+        auto enqueue_group = [&](int g) {
+            for (int i = g * GL; i < std::min(K, (g + 1) * GL); i++) {
+                mark[i] = evrecs.size();
+                KParams Q = chunk_params(s, bufs[i & 1], bufs[(i + 1) & 1]);
+                Q.ctl = s.ctl;
+                Q.lrec = s.lrec;
+                Q.p_begin = 0;
+                Q.p_end = DP;  // grids are sized on the bound; the kernels read the level from ctl
+                timed(PH_HASH, [&] { ks.fused(Q, stream); });
+                timed(PH_DEDUP, [&] {
+                    ks.elect(Q, DP, stream);
+                    ks.wincount(Q, DP, stream);
+                });
+                timed(PH_MAT, [&] { ks.commit(Q, stream); });
+            }
+            HIPCHK(hipMemcpyAsync(&s.hsnap[g % 3], s.ctl, sizeof(LevelCtl), hipMemcpyDeviceToHost, stream));
+            HIPCHK(hipEventRecord(gev[g % 3], stream));
+        };
+        int enq = 0;
+        for (; enq < std::min(2, ngroups); enq++) enqueue_group(enq);
+        for (; enq < ngroups; enq++) {
+            HIPCHK(hipEventSynchronize(gev[(enq - 2) % 3]));
+            if (s.hsnap[(enq - 2) % 3].stop != CTL_RUN) break;
+            enqueue_group(enq);
+        }
+        for (int i = enq * GL; i < K; i++) mark[i] = evrecs.size();
+        HIPCHK(hipMemcpyAsync(s.hctl, s.ctl, sizeof(LevelCtl), hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        HIPCHK(hipGetLastError());
+        const LevelCtl c = *s.hctl;
+        const int D = (int)c.done_levels;
+        if (D > 0 && D <= K) {
+            HIPCHK(hipMemcpyAsync(s.hlrec, s.lrec, sizeof(LevelRec) * D, hipMemcpyDeviceToHost, stream));
+            HIPCHK(hipStreamSynchronize(stream));
+        }
+        if (D > K || c.stop == CTL_RUN) throw Fail(RMC_E_STATE, "device level loop did not stop");
+        const int nst = D + (c.stop == CTL_ERROR ? 1 : 0);
+        for (int i = 0; i < nst; i++) std::memset(&out[i], 0, sizeof out[i]);
+        // phase times of the levels that ran (later levels' kernels returned at once)
+        for (size_t j = 0; j < evrecs.size(); j++) {
+            const int lv = (int)(std::upper_bound(mark.begin(), mark.end(), j) - mark.begin()) - 1;
+            if (lv < 0 || lv >= nst) continue;
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, evpool[evrecs[j].a], evpool[evrecs[j].b]));
+            out[lv].kernel_ms[evrecs[j].ph] += ms;
+            out[lv].kernel_launches[evrecs[j].ph] += 1;
+        }
+        evrecs.clear();
+        evused = 0;
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        for (int i = 0; i < D; i++) {
+            const LevelRec &r = s.hlrec[i];
+            rmc_level_stats *st = &out[i];
+            const int L = L0 + i;
+            const uint64_t gid_nxt = s.level_start[L - 1] + r.expanded;
+            total_generated += r.generated;
+            total_distinct += r.new_states;
+            s.T_count += r.new_states;
+            if (r.new_states) {
+                s.level_start.push_back(gid_nxt);
+                depth = L + 1;
+            } else {
+                finished = true;
+                status = RMC_DONE;
+                queue_at_end = 0;
+            }
+            st->level = L;
+            st->expanded = r.expanded;
+            st->generated = r.generated;
+            st->new_states = r.new_states;
+            st->total_generated = total_generated;
+            st->total_distinct = total_distinct;
+            st->queue = r.new_states;
+            st->status = finished ? RMC_DONE : RMC_OK;
+            st->seconds = el / nst;
+        }
+        if (D & 1) {
+            std::swap(s.cur, s.nxt);
+            std::swap(s.cur_cap, s.nxt_cap);
+        }
+        s.cur_n = c.cur_n;
+        s.epoch = c.epoch;
+        if (s.T_count != c.T_count) throw Fail(RMC_E_STATE, "device level loop: seen-set count mismatch");
+        seconds += el;
+        if (c.stop == CTL_ERROR) {
+            // the level the loop stopped in is intact: report its error as the host path does
+            rmc_level_stats *st = &out[D];
+            st->seconds = el / nst;
+            if (s.hsum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
+            const int L = (int)s.level_start.size();
+            st->level = L;
+            st->expanded = s.cur_n;
+            const uint64_t gid_cur = s.level_start[L - 1];
+            s.T_count += s.hsum[1];
+            unsigned long long best;
+            const int kind = first_error(s.hsum + 2, &best);
+            if (kind < 0) throw Fail(RMC_E_STATE, "device level loop stopped without an error");
+            stop_on_error(kind, best, 0, 0, gid_cur, gid_cur + s.cur_n, 0, st);
+        }
+        return nst;
+    }
+
     // TLC's counters at the moment the first error (in -workers 1 order) is reported.
     void stop_on_error(int kind, unsigned long long ek, uint64_t p0, uint64_t nxt_before, uint64_t gid_cur,
                        uint64_t gid_nxt, uint64_t gen_before_chunk, rmc_level_stats *st) {
@@ -978,7 +1158,7 @@ struct rmc_ctx {
             HIPCHK(hipMemcpy(cn.data(), s.cnt, pl * 4, hipMemcpyDeviceToHost));
             for (uint32_t x : cn) off_p += x;
         }
-        const uint64_t wbase = d2h(s.wpos + pl);
+        const uint64_t wbase = (uint64_t)d2h(s.boff + pl / WTILE) + d2h(s.wpos + pl);
         // winners among p's first `upto` successor slots (election table of this chunk)
         auto winners_in = [&](uint32_t upto) -> uint64_t {
             if (!upto) return 0;
@@ -1425,11 +1605,42 @@ int rmc_run(void *ctx, rmc_result *res) {
     rmc_ctx *c = (rmc_ctx *)ctx;
     return guarded(c, [&] {
         if (!c->inited) c->init(nullptr);
-        int rc = RMC_OK;
-        while (!c->finished) rc = c->step(nullptr);
-        (void)rc;
+        std::vector<rmc_level_stats> tmp(LREC_CAP + 1);
+        while (!c->finished) {
+            if (c->batch_ok())
+                c->step_batch(tmp.data(), c->batch_levels());
+            else
+                c->step(nullptr);
+        }
         if (res) c->result(res);
         return c->status;
+    });
+}
+
+int rmc_steps(void *ctx, rmc_level_stats *levels, uint32_t cap, uint32_t *n) {
+    rmc_ctx *c = (rmc_ctx *)ctx;
+    if (!levels || !cap || !n) return RMC_E_ARG;
+    *n = 0;
+    return guarded(c, [&] {
+        if (!c->inited) throw Fail(RMC_E_STATE, "rmc_steps before rmc_init");
+        if (c->finished) return c->status == RMC_OK ? RMC_DONE : c->status;
+        if (c->batch_ok() && cap > 1) {
+            const int k = c->step_batch(levels, std::min<int>(c->batch_levels(), (int)cap - 1));
+            *n = (uint32_t)k;
+            return levels[k - 1].status;
+        }
+        const int rc = c->step(levels);
+        *n = 1;
+        return rc;
+    });
+}
+
+int rmc_set_timing(void *ctx, uint32_t phases) {
+    rmc_ctx *c = (rmc_ctx *)ctx;
+    return guarded(c, [&] {
+        c->timing_on = phases != 0;
+        if (phases != 0) c->cfg.timing_phases = phases == 0xFFFFFFFFu ? 0u : phases;
+        return RMC_OK;
     });
 }
 
@@ -1450,9 +1661,16 @@ int rmc_run_levels(void *ctx, rmc_level_stats *levels, uint32_t cap, uint32_t *n
             c->init(n < cap && levels ? &levels[n] : &tmp);
             n++;
         }
+        std::vector<rmc_level_stats> bt(LREC_CAP + 1);
         while (!c->finished) {
-            c->step(n < cap && levels ? &levels[n] : &tmp);
-            n++;
+            if (c->batch_ok()) {
+                const int k = c->step_batch(bt.data(), c->batch_levels());
+                for (int i = 0; i < k; i++, n++)
+                    if (n < cap && levels) levels[n] = bt[i];
+            } else {
+                c->step(n < cap && levels ? &levels[n] : &tmp);
+                n++;
+            }
         }
         if (n_levels) *n_levels = n < cap ? n : cap;
         if (res) c->result(res);

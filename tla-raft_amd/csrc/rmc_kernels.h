@@ -19,6 +19,32 @@ struct Tables {
 
 enum ErrSlot { ERR_ASSERT = 0, ERR_DEADLOCK = 1, ERR_INV = 2, ERR_EVAL = 3, ERR_NSLOTS = 4 };
 
+// Device-driven level loop (single GPU): the host enqueues several BFS levels without
+// reading anything back.  Each level's kernels take their parent count, id bases,
+// election epoch and table size from this block, which the previous level's commit
+// wrote; once `stop` is set every later kernel returns at once.
+enum CtlStop : uint32_t { CTL_RUN = 0, CTL_DONE = 1, CTL_ERROR = 2, CTL_HOST = 3 };
+struct LevelCtl {
+    unsigned long long cur_n;    // parents of the level being expanded
+    unsigned long long gid_cur;  // global id of its first state
+    unsigned long long T_count;  // fingerprints in the seen set
+    unsigned long long Lmask;    // election table mask for this level
+    // capacities (host-written before the batch)
+    unsigned long long nxt_cap, trace_cap, T_cap, chunk_parents, Lcap_max;
+    uint32_t level;              // level being expanded (1 = Init's level)
+    uint32_t epoch;              // election table epoch of this level
+    uint32_t stop;               // CtlStop: RUN, DONE (empty level), ERROR, HOST (next level needs the host)
+    uint32_t done_levels;        // levels committed in this batch (index into LevelRec)
+    uint32_t batch;              // levels the host enqueued: the loop hands back after that many
+    uint32_t pad_;
+};
+struct LevelRec { unsigned long long expanded, generated, new_states; };
+constexpr int LREC_CAP = 1024;   // levels per batch at most
+constexpr uint32_t WTILE = 1024; // parents per tile of the winner-count scan (1024 tiles at most)
+
+// In device-loop mode the host sizes every grid on a bound of the level's parents (p_end -
+// p_begin of the KParams it passes); the kernels read the real range from the LevelCtl.
+
 // Kernel parameters (passed by value).
 struct KParams {
     Dims d;
@@ -34,7 +60,7 @@ struct KParams {
     // per successor (chunk-local index j)
     ulonglong2 *fp;
     const uint32_t *wflag;     // 1 = winner (new, first in TLC order)
-    const uint32_t *wpos;      // exclusive scan of wflag
+    uint32_t *wpos;            // exclusive scan of wflag (fused level: of wcnt inside a tile)
     // seen set (open addressing, 16-B slots, lo word |= 1, 0 = empty)
     ulonglong2 *T;
     uint64_t Tmask;
@@ -54,15 +80,20 @@ struct KParams {
     // -> scan -> commit.  Successor slot q = (p - p_begin) * maxsucc + rank is sparse and
     // increases in TLC order; it indexes fp, lslot, score (core words, CW/4 uint4 each) and
     // saux {key | nadd << 16, add0 | add1 << 16, add2 | add3 << 16, 0}.  wpos is then the
-    // exclusive scan of wcnt (winners per parent).
+    // exclusive scan of wcnt (winners per parent) inside each WTILE-parent tile, and a
+    // parent's first winner lands at boff[tile] + wpos.
     uint4 *score;
     uint4 *saux;
     uint32_t *lslot;           // LS_SEEN, LS_ELECT, or the election slot in L
     unsigned long long *L;     // chunk election table, (epoch << 32) | q
     uint64_t Lmask;
     uint32_t epoch;
-    uint32_t *wcnt;            // winners per parent (chunk-local), [np] = 0
-    unsigned long long *gsum;  // successors generated in the chunk
+    uint32_t *wcnt;            // winners per parent (chunk-local)
+    uint32_t *bw, *bg, *boff;  // per tile: winners, successors generated, first winner's offset
+    uint32_t *tickets;         // [0] winner-count pass: last-block counter (0 between launches)
+    unsigned long long *sum;   // chunk summary {generated, winners, error keys[ERR_NSLOTS], flags}
+    LevelCtl *ctl;             // device-driven level loop (nullptr: the host drives the chunk)
+    LevelRec *lrec;            // statistics of each level the device loop commits
     // single-state hook outputs
     uint32_t *out_keys;
     uint32_t *out_count;
@@ -76,8 +107,9 @@ struct KernelSet {
     void (*single)(const KParams &, hipStream_t);           // all successors of front[0] -> next, fp, out_keys
     void (*fused)(const KParams &, hipStream_t);            // expand + hash + probe + staging (one pass)
     void (*elect)(const KParams &, uint64_t np, hipStream_t);     // first-in-TLC-order election per fingerprint
-    void (*wincount)(const KParams &, uint64_t np, hipStream_t);  // winners per parent, successors generated
-    void (*commit)(const KParams &, hipStream_t);           // winners -> next level, seen set, trace, invariants
+    void (*wincount)(const KParams &, uint64_t np, hipStream_t);  // winners per parent + their scan, successors generated
+    void (*commit)(const KParams &, hipStream_t);           // winners -> next level, seen set, trace, invariants;
+                                                            // chunk summary (and the device loop's next level)
     void (*fp_states)(const KParams &, uint64_t n, hipStream_t);  // fp of front[0..n) -> fp
     void (*inv_states)(const KParams &, uint64_t n, int32_t *out, hipStream_t); // per state: 1/0/-1 for inv_mask bits
 };
@@ -92,16 +124,7 @@ void launch_winflag(const uint32_t *lslot, const unsigned long long *L, const ui
                     uint32_t *wflag, hipStream_t s);
 void launch_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned long long *err, const uint32_t *flags,
                     unsigned long long *out, hipStream_t s);
-// fused level: summary = {successors generated (sum of the wincount blocks' partial sums),
-// winners (wpos[np]), error keys (then reset), flags (then reset)}
-void launch_summary_fused(const unsigned long long *gsum, unsigned nblocks, const uint32_t *wtotal,
-                          unsigned long long *err, uint32_t *flags, unsigned long long *out, hipStream_t s);
 constexpr uint32_t LS_SEEN = 0xFFFFFFFFu, LS_ELECT = 0xFFFFFFFEu;
-constexpr unsigned WC_BLOCKS = 1024;  // max blocks of the wincount pass (= partial sums in gsum)
-inline unsigned wincount_blocks(uint64_t np) {
-    const uint64_t b = (np + 255) / 256;
-    return (unsigned)(b < WC_BLOCKS ? (b ? b : 1) : WC_BLOCKS);
-}
 void launch_scan_small(const uint32_t *in, uint64_t n, uint32_t *out, hipStream_t s);
 void launch_winscan_small(const uint32_t *lslot, const unsigned long long *L, const uint32_t *Gp, uint64_t Gub,
                           uint32_t *wflag, uint32_t *wpos, hipStream_t s);

@@ -40,6 +40,47 @@ __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// ---- device-driven level loop -------------------------------------------------------------
+// With P.ctl set, a level's kernels take the parent range, id bases, election epoch and
+// table size from the control block the previous level's commit wrote (a kernel boundary
+// makes it visible); once the loop has stopped every block returns at once.
+__device__ __forceinline__ bool level_args(KParams &P) {
+    if (!P.ctl) return true;
+    const LevelCtl *c = P.ctl;
+    if (c->stop != CTL_RUN) return false;
+    P.p_begin = 0;
+    P.p_end = c->cur_n;
+    P.gid_parent_base = c->gid_cur;
+    P.gid_next_base = c->gid_cur + c->cur_n;
+    P.next_base = 0;
+    P.epoch = c->epoch;
+    P.Lmask = c->Lmask;
+    return true;
+}
+
+// True in the last block of the launch to get here (MI355X guide, counter hand-off): every
+// wave drains its stores, lane 0 releases at agent scope before taking a ticket; the last
+// arriver acquires before reading what the other blocks wrote and re-arms the counter.
+// Every block of the launch must call it.
+__device__ __forceinline__ bool last_block(uint32_t *ticket, uint32_t *flag_lds) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = t == gridDim.x - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *flag_lds = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return *flag_lds != 0;
+}
+
 template <int N, int V, int MR>
 struct Spec {
     using L = Layout<N, V>;
@@ -655,6 +696,7 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
     __shared__ uint8_t pimg[NPM * N];                   // permutation images
     __shared__ uint64_t sU[MAXS], sX[2][MAXS * N];      // compacted successor rows
     __shared__ uint32_t sS[MAXS];
+    if (MODE == M_FUSED && !level_args(P)) return;
     const int lane = threadIdx.x;
     if (SUMS) {
         for (int i = lane; i < P.t.np * N; i += 64) pimg[i] = P.t.perms[(i / N) * MAXN + (i % N)];
@@ -958,8 +1000,10 @@ __global__ __launch_bounds__(64) void k_inv_states(KParams P, uint64_t n, int32_
 // slot of another epoch is empty, so the table is never cleared.  fp was written by the previous
 // launch, so reading another slot's fingerprint needs no fence.
 template <int N, int V, int MR>
-__global__ __launch_bounds__(256) void k_elect(KParams P, uint64_t np) {
+__global__ __launch_bounds__(256) void k_elect(KParams P) {
     using S = Spec<N, V, MR>;
+    if (!level_args(P)) return;
+    const uint64_t np = P.p_end - P.p_begin;
     const uint64_t nq = np * (uint64_t)S::MAXS;
     const unsigned long long tag = (unsigned long long)P.epoch << 32;
     for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (uint64_t)gridDim.x * blockDim.x) {
@@ -986,31 +1030,129 @@ __global__ __launch_bounds__(256) void k_elect(KParams P, uint64_t np) {
     }
 }
 
-// Thread per parent: winners per parent (wcnt) and, per block, the successors generated
-// (gsum[blockIdx.x]; the summary adds the partial sums -- one atomic per wave on a single
-// counter serialises at the memory side and cost more than the whole pass).
-template <int N, int V, int MR>
-__global__ __launch_bounds__(256) void k_wincount(KParams P, uint64_t np) {
-    using S = Spec<N, V, MR>;
-    __shared__ uint32_t wsum[4];
-    if (blockIdx.x == 0 && threadIdx.x == 0) P.wcnt[np] = 0;  // scan input past the last parent
-    uint32_t gen = 0;
-    for (uint64_t pl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; pl < np; pl += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t t = P.cnt[pl];
-        uint32_t w = 0;
-        for (uint32_t r = 0; r < t; r++) {
-            const uint64_t q = pl * (uint64_t)S::MAXS + r;
-            const uint32_t g = P.lslot[q];
-            w += (g < LS_ELECT && (uint32_t)P.L[g] == (uint32_t)q) ? 1u : 0u;
-        }
-        P.wcnt[pl] = w;
-        gen += t;
-    }
+// Exclusive scan of one value per thread over a 1024-thread block (16 waves); *total gets the
+// block's sum.  ws holds 16 words of LDS.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *ws, uint32_t *total) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint32_t x = v;
 #pragma unroll
-    for (int d = 32; d > 0; d >>= 1) gen += __shfl_down(gen, d, 64);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = gen;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) P.gsum[blockIdx.x] = (unsigned long long)wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (lane == 63) ws[wv] = x;
+    __syncthreads();
+    uint32_t base = 0, all = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++) {
+        const uint32_t w = ws[k];
+        base += k < wv ? w : 0u;
+        all += w;
+    }
+    *total = all;
+    return base + x - v;
+}
+
+// One 1024-thread block per WTILE-parent tile, thread per parent: winners per parent (wcnt),
+// their exclusive scan inside the tile (wpos), and per tile the winners (bw) and successors
+// generated (bg).  The last block to finish scans the tile totals into boff and writes
+// {generated, winners} to sum[0..1] -- the only values the host needs before commit.
+template <int N, int V, int MR>
+__global__ __launch_bounds__(1024) void k_wincount(KParams P) {
+    using S = Spec<N, V, MR>;
+    __shared__ uint32_t ws[16];
+    __shared__ uint32_t flag;
+    if (!level_args(P)) return;
+    const uint64_t np = P.p_end - P.p_begin;
+    const uint32_t ntiles = (uint32_t)((np + WTILE - 1) / WTILE);
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t pl = (uint64_t)tile * WTILE + threadIdx.x;
+        uint32_t w = 0, t = 0;
+        if (pl < np) {
+            t = P.cnt[pl];
+            // 8 slots at a time: their slot loads, then their election-word loads, go out
+            // together instead of as a chain of 2t dependent round trips
+            for (uint32_t r0 = 0; r0 < t; r0 += 8) {
+                uint32_t g[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t r = r0 + (uint32_t)k;
+                    g[k] = r < t ? P.lslot[pl * (uint64_t)S::MAXS + r] : LS_SEEN;
+                }
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t q = (uint32_t)(pl * (uint64_t)S::MAXS + r0 + (uint32_t)k);
+                    w += (g[k] < LS_ELECT && (uint32_t)P.L[g[k]] == q) ? 1u : 0u;
+                }
+            }
+        }
+        uint32_t wt, gt;
+        const uint32_t x = block_excl_scan(w, ws, &wt);
+        (void)block_excl_scan(t, ws, &gt);
+        if (pl < np) {
+            P.wcnt[pl] = w;
+            P.wpos[pl] = x;
+        }
+        if (threadIdx.x == 0) {
+            P.bw[tile] = wt;
+            P.bg[tile] = gt;
+        }
+    }
+    if (!last_block(&P.tickets[0], &flag)) return;
+    // tile offsets (ntiles <= 1024 = blockDim.x) and the chunk totals
+    uint32_t wsum = 0, gsum = 0, wtot, gtot;
+    const uint32_t i = threadIdx.x;
+    if (i < ntiles) { wsum = P.bw[i]; gsum = P.bg[i]; }
+    const uint32_t o = block_excl_scan(wsum, ws, &wtot);
+    (void)block_excl_scan(gsum, ws, &gtot);
+    if (i < ntiles) P.boff[i] = o;
+    if (i == 0) {
+        P.sum[0] = gtot;
+        P.sum[1] = wtot;
+    }
+}
+
+// Chunk summary, after the commit pass: {generated, winners} (from the winner
+// count pass), the error keys and flags (then re-armed).  In device-loop mode it also
+// records the level and advances the control block to the next one -- or stops the loop.
+template <int MAXS>
+__device__ void finish_level(const KParams &P) {
+    unsigned long long *sm = P.sum;
+    const unsigned long long G = sm[0], Wn = sm[1];
+    bool bad = false;
+    for (int k = 0; k < ERR_NSLOTS; k++) {
+        const unsigned long long e = __hip_atomic_exchange(&P.err[k], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sm[2 + k] = e;
+        bad |= e != ~0ull;
+    }
+    const uint32_t fl = __hip_atomic_exchange(&P.flags[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm[2 + ERR_NSLOTS] = fl;
+    bad |= fl != 0;
+    LevelCtl *c = P.ctl;
+    if (!c) return;
+    if (bad) { c->stop = CTL_ERROR; return; }  // the host reports the error from this level's buffers
+    if (c->done_levels < (uint32_t)LREC_CAP) {
+        LevelRec &r = P.lrec[c->done_levels];
+        r.expanded = c->cur_n;
+        r.generated = G;
+        r.new_states = Wn;
+    }
+    c->done_levels++;
+    c->gid_cur += c->cur_n;
+    c->cur_n = Wn;
+    c->T_count += Wn;
+    c->level++;
+    c->epoch++;
+    const unsigned long long Gub = Wn * (unsigned long long)MAXS;
+    unsigned long long lc = 1;
+    while (lc < 2 * Gub) lc <<= 1;
+    c->Lmask = (lc < c->Lcap_max ? lc : c->Lcap_max) - 1;
+    if (Wn == 0)
+        c->stop = CTL_DONE;
+    else if (c->done_levels >= c->batch || c->done_levels >= (uint32_t)LREC_CAP || Wn > c->chunk_parents ||
+             Gub > c->nxt_cap || c->gid_cur + Wn + Gub > c->trace_cap || 2 * (c->T_count + Gub) > c->T_cap)
+        c->stop = CTL_HOST;  // the next level is not known to fit the buffers: the host grows them
 }
 
 // Write the staged successor held by lane t as a record at rec_out (whole wave): core words
@@ -1060,12 +1202,13 @@ template <int N, int V, int MR>
 __global__ __launch_bounds__(64) void k_commit(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
+    if (!level_args(P)) return;
     const int lane = threadIdx.x;
     const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
     for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
         const uint64_t pl = p - P.p_begin;
-        const uint32_t w0 = P.wpos[pl];
-        if (P.wpos[pl + 1] == w0) continue;
+        if (!P.wcnt[pl]) continue;
+        const uint32_t w0 = P.boff[pl / WTILE] + P.wpos[pl];
         const uint32_t *rec = P.front + p * (uint64_t)S::RECW;
         const uint32_t nm = (rec[Lo::W_MISC] >> 16) & 0xFFu;
         const uint16_t *rid = reinterpret_cast<const uint16_t *>(rec + S::CW);
@@ -1123,6 +1266,15 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
     }
 }
 
+// The chunk summary / device-loop step as its own one-lane launch: a last-block hand-off in the
+// commit pass would put every one of its (up to 8192) blocks through one arrival counter.
+template <int N, int V, int MR>
+__global__ __launch_bounds__(64) void k_finish(KParams P) {
+    if (threadIdx.x != 0) return;
+    if (P.ctl && P.ctl->stop != CTL_RUN) return;
+    finish_level<Spec<N, V, MR>::MAXS>(P);
+}
+
 static inline unsigned grid_for(uint64_t n) {
     const uint64_t cap = 256ull * 32ull;  // 32 one-wave blocks per CU on 256 CUs
     return (unsigned)(n < cap ? (n ? n : 1) : cap);
@@ -1150,13 +1302,15 @@ struct Launch {
         return (unsigned)(b < cap ? (b ? b : 1) : cap);
     }
     static void elect(const KParams &P, uint64_t np, hipStream_t s) {
-        hipLaunchKernelGGL((k_elect<N, V, MR>), dim3(slot_grid(np)), dim3(256), 0, s, P, np);
+        hipLaunchKernelGGL((k_elect<N, V, MR>), dim3(slot_grid(np)), dim3(256), 0, s, P);
     }
     static void wincount(const KParams &P, uint64_t np, hipStream_t s) {
-        hipLaunchKernelGGL((k_wincount<N, V, MR>), dim3(wincount_blocks(np)), dim3(256), 0, s, P, np);
+        const uint64_t tiles = (np + WTILE - 1) / WTILE;
+        hipLaunchKernelGGL((k_wincount<N, V, MR>), dim3(tiles ? (unsigned)tiles : 1u), dim3(1024), 0, s, P);
     }
     static void commit(const KParams &P, hipStream_t s) {
         hipLaunchKernelGGL((k_commit<N, V, MR>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
+        hipLaunchKernelGGL((k_finish<N, V, MR>), dim3(1), dim3(64), 0, s, P);
     }
     static void fps(const KParams &P, uint64_t n, hipStream_t s) {
         hipLaunchKernelGGL((k_fp_states<N, V, MR>), dim3(grid_for(n)), dim3(64), 0, s, P, n);
@@ -1271,29 +1425,6 @@ __global__ void k_summary(const uint32_t *Gp, const uint32_t *wpos, unsigned lon
     }
 }
 
-// fused level: one copy-back per chunk: successors generated (then zeroed), winners, errors, flags
-__global__ __launch_bounds__(256) void k_summary_fused(const unsigned long long *gsum, unsigned nb,
-                                                       const uint32_t *wtotal, unsigned long long *err,
-                                                       uint32_t *flags, unsigned long long *out) {
-    __shared__ unsigned long long part[4];
-    unsigned long long g = 0;
-    for (unsigned i = threadIdx.x; i < nb; i += 256) g += gsum[i];
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) g += __shfl_down(g, d, 64);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = g;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        out[0] = part[0] + part[1] + part[2] + part[3];
-        out[1] = *wtotal;
-        for (int i = 0; i < ERR_NSLOTS; i++) {
-            out[2 + i] = err[i];
-            err[i] = ~0ull;
-        }
-        out[2 + ERR_NSLOTS] = flags[0];
-        flags[0] = 0;
-    }
-}
-
 // One-workgroup exclusive scan for small chunks (n <= 64K): out[i] = sum in[0..i), out[n] = total.
 // WIN = true computes the winner flags inline (flag_j = L[lslot[j]] == j, k_winflag) and
 // also stores them, replacing the flag kernel + a two-kernel library scan.
@@ -1373,10 +1504,6 @@ void launch_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned lon
                     unsigned long long *out, hipStream_t s) {
     hipLaunchKernelGGL(k_summary, dim3(1), dim3(64), 0, s, Gp, wpos, const_cast<unsigned long long *>(err),
                        const_cast<uint32_t *>(flags), out);
-}
-void launch_summary_fused(const unsigned long long *gsum, unsigned nblocks, const uint32_t *wtotal,
-                          unsigned long long *err, uint32_t *flags, unsigned long long *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_summary_fused, dim3(1), dim3(256), 0, s, gsum, nblocks, wtotal, err, flags, out);
 }
 void launch_scan_small(const uint32_t *in, uint64_t n, uint32_t *out, hipStream_t s) {
     hipLaunchKernelGGL((k_scan_small<false>), dim3(1), dim3(1024), 0, s, in, (const uint32_t *)nullptr, n,

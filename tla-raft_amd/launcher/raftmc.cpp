@@ -255,16 +255,21 @@ int main(int argc, char **argv) {
     if (rc < 0) { std::printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 75; }
     std::printf("Finished computing initial states: 1 distinct state generated at %s.\n", now_str().c_str());
     double gpu_seconds = 0;
+    std::vector<rmc_level_stats> lv(65);
     while (rc == RMC_OK) {
-        rc = rmc_step(ctx, &st);
+        uint32_t nl = 0;
+        rc = rmc_steps(ctx, lv.data(), (uint32_t)lv.size(), &nl);
         if (rc < 0) break;
-        gpu_seconds += st.seconds;
         const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        std::printf("Progress(%d) at %s: %llu states generated (%.0f s/min), %llu distinct states found (%.0f ds/min), "
-                    "%llu states left on queue.\n",
-                    st.level + 1, now_str().c_str(), (unsigned long long)st.total_generated,
-                    st.total_generated / el * 60.0, (unsigned long long)st.total_distinct,
-                    st.total_distinct / el * 60.0, (unsigned long long)st.queue);
+        for (uint32_t i = 0; i < nl; i++) {
+            const rmc_level_stats &q = lv[i];
+            gpu_seconds += q.seconds;
+            std::printf("Progress(%d) at %s: %llu states generated (%.0f s/min), %llu distinct states found (%.0f ds/min), "
+                        "%llu states left on queue.\n",
+                        q.level + 1, now_str().c_str(), (unsigned long long)q.total_generated,
+                        q.total_generated / el * 60.0, (unsigned long long)q.total_distinct,
+                        q.total_distinct / el * 60.0, (unsigned long long)q.queue);
+        }
         std::fflush(stdout);
     }
     if (rc < 0) {

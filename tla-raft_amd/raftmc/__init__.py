@@ -47,6 +47,7 @@ class _Config(ctypes.Structure):
         ("seen_log2", ctypes.c_int32), ("no_symmetry", ctypes.c_int32), ("chunk_successors", ctypes.c_uint64),
         ("rank", ctypes.c_int32), ("world_size", ctypes.c_int32), ("comm_unique_id", ctypes.c_void_p),
         ("virtual_shards", ctypes.c_int32), ("timing_phases", ctypes.c_uint32),
+        ("device_levels", ctypes.c_uint32),
     ]
 
 
@@ -85,6 +86,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.rmc_create.argtypes = [P(_Config), P(vp)]
     lib.rmc_init.argtypes = [vp, P(_LevelStats)]
     lib.rmc_step.argtypes = [vp, P(_LevelStats)]
+    lib.rmc_steps.argtypes = [vp, P(_LevelStats), u32, P(u32)]
+    lib.rmc_set_timing.argtypes = [vp, u32]
     lib.rmc_run.argtypes = [vp, P(_Result)]
     lib.rmc_reset.argtypes = [vp]
     lib.rmc_run_levels.argtypes = [vp, P(_LevelStats), u32, P(u32), P(_Result)]
@@ -124,6 +127,7 @@ class ModelConfig:
     world_size: int = 1              # multi-GPU: ranks (one process per GPU)
     comm_unique_id: Optional[bytes] = None  # 128 bytes from comm_unique_id() on rank 0
     timing_phases: int = 0           # bit i: time phase i with HIP events (0 = all phases)
+    device_levels: int = 0           # levels per host round trip in run() (0 = auto, 1 = host-driven)
 
     def to_c(self) -> _Config:
         c = _Config()
@@ -143,6 +147,7 @@ class ModelConfig:
         c.rank, c.world_size = self.rank, self.world_size
         c.virtual_shards = self.virtual_shards
         c.timing_phases = self.timing_phases
+        c.device_levels = self.device_levels
         if self.comm_unique_id is not None:
             self._idbuf = ctypes.create_string_buffer(bytes(self.comm_unique_id), 128)
             c.comm_unique_id = ctypes.cast(self._idbuf, ctypes.c_void_p)
@@ -347,6 +352,19 @@ class ModelChecker:
         ls = self._stats(st)
         self.levels.append(ls)
         return ls
+
+    def set_timing(self, phases: int) -> None:
+        """HIP-event phase timing from now on: 0 = off, 0xFFFFFFFF = all phases, else a phase mask."""
+        self._check(self.lib.rmc_set_timing(self.h, phases))
+
+    def steps(self, cap: int = 65) -> List[LevelStats]:
+        """The levels one host round trip covers (rmc_steps): a device-driven batch on one GPU."""
+        buf = (_LevelStats * cap)()
+        n = ctypes.c_uint32()
+        self._check(self.lib.rmc_steps(self.h, buf, cap, ctypes.byref(n)))
+        out = [self._stats(buf[i]) for i in range(n.value)]
+        self.levels.extend(out)
+        return out
 
     def run(self) -> Result:
         """Exhaust the state space (or stop at the first error) inside the library."""
