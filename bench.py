@@ -90,6 +90,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe-peak", action="store_true")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -182,7 +183,7 @@ def main():
     per_launch_ms = phase_ms[dom] / max(1, launches[dom])
     bytes_total = alg_bytes(PHASES[dom], Fs, Gs, Ns, S, CWB)
     achieved = bytes_total / max(1, launches[dom]) / (per_launch_ms / 1e3) / 1e9 if per_launch_ms > 0 else 0.0
-    traffic, pmc_src = pmc_traffic(mc, PHASES[dom], args.workload)
+    traffic, pmc_src = pmc_traffic(mc, PHASES[dom], args.workload, res.depth)
     roof = {"bound": "hbm", "kernel": PHASES[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_source": pmc_src,
@@ -191,6 +192,20 @@ def main():
             "timed_steps": len(range(0, args.steps, TIMING_EVERY)),
             "phase_ms_per_step": {PHASES[i]: round(phase_ms[i] / len(range(0, args.steps, TIMING_EVERY)), 4)
                                   for i in range(4)}}
+    # seen-set probe throughput of the run (one probe per generated successor in the expansion
+    # pass, one insert per new state in commit) against the random-probe peak of the same slot
+    # layout measured on this GPU: a table the size of the run's (2^22 slots, L2/MALL-resident)
+    # and one far beyond the caches (2^28 slots = 4 GiB, HBM-resident)
+    probes = (res.generated + res.distinct) * args.steps * (world if parallelism.startswith("replicas") else 1)
+    seen = {"probes_per_step": res.generated + res.distinct,
+            "achieved_probes_per_s": round(probes / elapsed, 1)}
+    if rank == 0 and not args.no_probe_peak:
+        pk_small = raftmc.probe_peak(local, 22, 1 << 26)
+        pk_hbm = raftmc.probe_peak(local, 28, 1 << 28)
+        seen.update({"peak_probes_per_s_2^22_slots": round(pk_small, 1),
+                     "peak_probes_per_s_2^28_slots": round(pk_hbm, 1),
+                     "frac_of_hbm_probe_peak": round(probes / elapsed / pk_hbm, 5),
+                     "slot_bytes": 16})
     line = {
         "metric": "distinct states/sec (whole node) + wall-time to exhaust",
         "value": round(value, 1),
@@ -208,6 +223,7 @@ def main():
                    "depth": res.depth, "verdict": "Inv holds" if res.status == "done" else res.status,
                    "parallelism": parallelism},
         "roofline": roof,
+        "seen_set": seen,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(w)
@@ -222,7 +238,10 @@ KERNEL_NAME = {"expand_hash": "void rmc::k_expand<{n}, {V}, {mr}, 4>(rmc::KParam
                "materialize": "void rmc::k_commit<{n}, {V}, {mr}>(rmc::KParams)"}
 
 
-def pmc_traffic(mc, phase, workload):
+PMC_RUNS = 6  # tools/pmc.sh: bench.py --steps 5 --warmup 1 per counter pass
+
+
+def pmc_traffic(mc, phase, workload, depth):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
     (tools/pmc.sh + tools/pmc_summary.py, FETCH_SIZE x2 correction per MI355X_MICROARCH.md)."""
     import glob
@@ -236,7 +255,11 @@ def pmc_traffic(mc, phase, workload):
     e = d.get(name)
     if not e or "hbm_bytes_per_dispatch" not in e:
         return None, None
-    return round(e["hbm_bytes_per_dispatch"]), os.path.relpath(files[-1], ROOT)
+    # the device-driven level loop enqueues a few levels past the last one, whose launches
+    # return at once: spread the pass's bytes over the launches that expanded a level
+    real = PMC_RUNS * depth
+    per = e["hbm_bytes_per_dispatch"] * e["dispatches"] / real if e["dispatches"] >= real else e["hbm_bytes_per_dispatch"]
+    return round(per), os.path.relpath(files[-1], ROOT)
 
 
 def record_bytes(mc):

@@ -167,6 +167,11 @@ int rmc_trace_len(void *ctx, uint32_t *len);
 int rmc_trace_state(void *ctx, uint32_t i, int32_t *unpacked, size_t cap_ints,
                     int32_t *action, int32_t *server, int32_t *witness);
 
+/* Measurement support (bench.py): the random-probe peak of the seen-set layout -- `probes`
+ * one-slot reads of 16-B slots at uniformly random indices of a 2^table_log2-slot table,
+ * best of 3 timed launches; no model-checking state is touched. */
+int rmc_probe_peak(int device, uint32_t table_log2, uint64_t probes, double *probes_per_s, double *seconds);
+
 const char *rmc_last_error(void *ctx);
 void rmc_destroy(void *ctx);
 

@@ -88,6 +88,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.rmc_step.argtypes = [vp, P(_LevelStats)]
     lib.rmc_steps.argtypes = [vp, P(_LevelStats), u32, P(u32)]
     lib.rmc_set_timing.argtypes = [vp, u32]
+    lib.rmc_probe_peak.argtypes = [i32, u32, u64, P(ctypes.c_double), P(ctypes.c_double)]
     lib.rmc_run.argtypes = [vp, P(_Result)]
     lib.rmc_reset.argtypes = [vp]
     lib.rmc_run_levels.argtypes = [vp, P(_LevelStats), u32, P(u32), P(_Result)]
@@ -152,6 +153,16 @@ class ModelConfig:
             self._idbuf = ctypes.create_string_buffer(bytes(self.comm_unique_id), 128)
             c.comm_unique_id = ctypes.cast(self._idbuf, ctypes.c_void_p)
         return c
+
+
+def probe_peak(device: int = -1, table_log2: int = 28, probes: int = 1 << 28) -> float:
+    """Random one-slot probes/s of a seen-set-shaped table (16-B slots) on the GPU."""
+    lib = load_library()
+    r, t = ctypes.c_double(), ctypes.c_double()
+    rc = lib.rmc_probe_peak(device, table_log2, probes, ctypes.byref(r), ctypes.byref(t))
+    if rc != RMC_OK:
+        raise RmcError(f"rmc_probe_peak failed: {ERRORS.get(rc, rc)}")
+    return r.value
 
 
 def parse_config(cfg_text: str, tla_text: Optional[str] = None) -> ModelConfig:
