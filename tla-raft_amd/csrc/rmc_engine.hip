@@ -163,10 +163,12 @@ struct Shard {
     uint32_t *cnt = nullptr, *off = nullptr, *lslot = nullptr, *wflag = nullptr, *wpos = nullptr;
     ulonglong2 *fp = nullptr;
     unsigned long long *L = nullptr;
+    ulonglong2 *LXY = nullptr;  // fused path: fingerprint of each election slot (tagged)
     uint32_t epoch = 0;
+    uint32_t lxy_epoch0 = 0;    // epoch of the last LXY clear (16-bit tags repeat after 65535 epochs)
     // fused single-shard level: sparse successor staging (slot q = chunk parent * maxsucc + rank)
     uint4 *score = nullptr, *saux = nullptr;
-    uint32_t *wcnt = nullptr, *bw = nullptr, *bg = nullptr, *boff = nullptr, *tickets = nullptr;
+    uint32_t *wcnt = nullptr, *wacc = nullptr, *bw = nullptr, *bg = nullptr, *boff = nullptr, *tickets = nullptr;
     // device-driven level loop: control block, per-level records, and their pinned host copies
     LevelCtl *ctl = nullptr, *hctl = nullptr, *hsnap = nullptr;
     LevelRec *lrec = nullptr, *hlrec = nullptr;
@@ -267,9 +269,9 @@ struct rmc_ctx {
     KParams chunk_params(const Shard &s, const uint32_t *front, uint32_t *next) const {
         KParams Q = base(s);
         Q.front = front; Q.next = next;
-        Q.cnt = s.cnt; Q.fp = s.fp; Q.wpos = s.wpos; Q.wcnt = s.wcnt;
+        Q.cnt = s.cnt; Q.fp = s.fp; Q.wpos = s.wpos; Q.wcnt = s.wcnt; Q.wacc = s.wacc;
         Q.bw = s.bw; Q.bg = s.bg; Q.boff = s.boff; Q.tickets = s.tickets; Q.sum = s.sum;
-        Q.score = s.score; Q.saux = s.saux; Q.lslot = s.lslot; Q.L = s.L;
+        Q.score = s.score; Q.saux = s.saux; Q.lslot = s.lslot; Q.L = s.L; Q.LXY = s.LXY;
         return Q;
     }
 
@@ -519,11 +521,16 @@ struct rmc_ctx {
         HIPCHK(hipMemsetAsync(s.cnt, 0, (chunk_parents + 1) * 4, stream));
         HIPCHK(hipMemsetAsync(s.wflag, 0, (Gcap + 1) * 4, stream));
         s.L = dmalloc<unsigned long long>(Lcap_max);
-        HIPCHK(hipMemsetAsync(s.L, 0, Lcap_max * 8, stream));
+        // fused path: an all-ones election word is older than every epoch's (elect_key)
+        HIPCHK(hipMemsetAsync(s.L, W == 1 ? 0xFF : 0, Lcap_max * 8, stream));
         if (W == 1) {
+            s.LXY = dmalloc<ulonglong2>(Lcap_max);
+            HIPCHK(hipMemsetAsync(s.LXY, 0, Lcap_max * 16, stream));
             s.score = dmalloc<uint4>(Gcap * (uint64_t)(ks.CW / 4));
             s.saux = dmalloc<uint4>(Gcap);
             s.wcnt = dmalloc<uint32_t>(chunk_parents + 1);
+            s.wacc = dmalloc<uint32_t>(chunk_parents + 1);
+            HIPCHK(hipMemsetAsync(s.wacc, 0, (chunk_parents + 1) * 4, stream));
             s.bw = dmalloc<uint32_t>(1024);
             s.bg = dmalloc<uint32_t>(1024);
             s.boff = dmalloc<uint32_t>(1024);
@@ -573,11 +580,11 @@ struct rmc_ctx {
 
     void free_shard(Shard &s) {
         dfree(s.cur); dfree(s.nxt); dfree(s.T); dfree(s.par); dfree(s.pslot); dfree(s.cnt); dfree(s.off);
-        dfree(s.lslot); dfree(s.wflag); dfree(s.wpos); dfree(s.fp); dfree(s.L); dfree(s.tmp); dfree(s.okey);
+        dfree(s.lslot); dfree(s.wflag); dfree(s.wpos); dfree(s.fp); dfree(s.L); dfree(s.LXY); dfree(s.tmp); dfree(s.okey);
         dfree(s.okey2); dfree(s.iota); dfree(s.perm); dfree(s.sflag); dfree(s.spos); dfree(s.sfp); dfree(s.ocnt);
         dfree(s.rfp); dfree(s.rlslot); dfree(s.rflag); dfree(s.rpos); dfree(s.rcount); dfree(s.sx); dfree(s.rx);
         dfree(s.pick_idx); dfree(s.err); dfree(s.sum); dfree(s.flags);
-        dfree(s.score); dfree(s.saux); dfree(s.wcnt); dfree(s.bw); dfree(s.bg); dfree(s.boff); dfree(s.tickets);
+        dfree(s.score); dfree(s.saux); dfree(s.wcnt); dfree(s.wacc); dfree(s.bw); dfree(s.bg); dfree(s.boff); dfree(s.tickets);
         dfree(s.ctl); dfree(s.lrec);
         if (s.hsum) (void)hipHostFree(s.hsum);
         if (s.hctl) (void)hipHostFree(s.hctl);
@@ -900,6 +907,14 @@ struct rmc_ctx {
         return kind;
     }
 
+    // The fused path's election slots carry 16-bit epoch tags (elect_tag): before the next
+    // `ahead` epochs could reuse a tag still in LXY, clear it (all tags are nonzero).
+    void renew_election_tags(Shard &s, uint32_t ahead) {
+        if (!s.LXY || s.epoch + ahead - s.lxy_epoch0 < 0xFFFFu) return;
+        HIPCHK(hipMemsetAsync(s.LXY, 0, Lcap_max * 16, stream));
+        s.lxy_epoch0 = s.epoch;
+    }
+
     int step_single(rmc_level_stats *st) {
         auto t0 = std::chrono::steady_clock::now();
         Shard &s = sh[0];
@@ -921,6 +936,7 @@ struct rmc_ctx {
                 grow_seen(s, s.T_count + Gub);
             }
             const uint64_t Lcap = std::min(next_pow2(2 * Gub), Lcap_max);
+            renew_election_tags(s, 1);
             ++s.epoch;
             auto params = [&] {
                 KParams Q = chunk_params(s, s.cur, s.nxt);
@@ -932,10 +948,7 @@ struct rmc_ctx {
             };
             // expand + fingerprint + seen-set probe + staging, one evaluation per parent
             timed(PH_HASH, [&] { ks.fused(params(), stream); });
-            timed(PH_DEDUP, [&] {
-                ks.elect(params(), np_, stream);
-                ks.wincount(params(), np_, stream);
-            });
+            timed(PH_DEDUP, [&] { ks.wincount(params(), np_, stream); });
             if (!small) {
                 const uint64_t Wub = d2h(s.sum + 1);
                 collect_times(st);
@@ -1024,6 +1037,7 @@ struct rmc_ctx {
         h.chunk_parents = DP;
         h.Lcap_max = Lcap_max;
         h.level = (uint32_t)L0;
+        renew_election_tags(s, K + 1);
         h.epoch = ++s.epoch;
         h.stop = CTL_RUN;
         h.batch = (uint32_t)K;
@@ -1049,10 +1063,7 @@ struct rmc_ctx {
                 Q.p_begin = 0;
                 Q.p_end = DP;  // grids are sized on the bound; the kernels read the level from ctl
                 timed(PH_HASH, [&] { ks.fused(Q, stream); });
-                timed(PH_DEDUP, [&] {
-                    ks.elect(Q, DP, stream);
-                    ks.wincount(Q, DP, stream);
-                });
+                timed(PH_DEDUP, [&] { ks.wincount(Q, DP, stream); });
                 timed(PH_MAT, [&] { ks.commit(Q, stream); });
             }
             HIPCHK(hipMemcpyAsync(&s.hsnap[g % 3], s.ctl, sizeof(LevelCtl), hipMemcpyDeviceToHost, stream));

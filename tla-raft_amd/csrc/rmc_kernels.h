@@ -76,7 +76,7 @@ struct KParams {
     uint32_t *flags;           // [0] msg-cap overflow, [1] violated invariant bit, [2] eval-error invariant bit
     // sharded mode: winners go to owner-grouped exchange records (RECW + 4 words each)
     uint32_t *xrec;
-    // fused single-shard level: expand (+hash, +seen-set probe, +staging) -> elect -> wincount
+    // fused single-shard level: expand (+hash, +seen-set probe, +election, +staging) -> wincount
     // -> scan -> commit.  Successor slot q = (p - p_begin) * maxsucc + rank is sparse and
     // increases in TLC order; it indexes fp, lslot, score (core words, CW/4 uint4 each) and
     // saux {key | nadd << 16, add0 | add1 << 16, add2 | add3 << 16, 0}.  wpos is then the
@@ -85,10 +85,14 @@ struct KParams {
     uint4 *score;
     uint4 *saux;
     uint32_t *lslot;           // LS_SEEN, LS_ELECT, or the election slot in L
-    unsigned long long *L;     // chunk election table, (epoch << 32) | q
+    unsigned long long *L;     // chunk election table: sharded path (epoch << 32) | q; fused path
+                               // the election word ((0xFFFFFFFF - epoch) << 32) | q (elect_key)
+    ulonglong2 *LXY;           // fused path: the fingerprint each election slot holds, both words
+                               // tagged with the chunk's 16-bit tag (elect_tag) in their low bits
     uint64_t Lmask;
     uint32_t epoch;
     uint32_t *wcnt;            // winners per parent (chunk-local)
+    uint32_t *wacc;            // winners per parent as the election counts them (0 between chunks)
     uint32_t *bw, *bg, *boff;  // per tile: winners, successors generated, first winner's offset
     uint32_t *tickets;         // [0] winner-count pass: last-block counter (0 between launches)
     unsigned long long *sum;   // chunk summary {generated, winners, error keys[ERR_NSLOTS], flags}
@@ -105,8 +109,7 @@ struct KernelSet {
     void (*hash)(const KParams &, hipStream_t);
     void (*materialize)(const KParams &, hipStream_t);
     void (*single)(const KParams &, hipStream_t);           // all successors of front[0] -> next, fp, out_keys
-    void (*fused)(const KParams &, hipStream_t);            // expand + hash + probe + staging (one pass)
-    void (*elect)(const KParams &, uint64_t np, hipStream_t);     // first-in-TLC-order election per fingerprint
+    void (*fused)(const KParams &, hipStream_t);            // expand + hash + probe + election + staging
     void (*wincount)(const KParams &, uint64_t np, hipStream_t);  // winners per parent + their scan, successors generated
     void (*commit)(const KParams &, hipStream_t);           // winners -> next level, seen set, trace, invariants;
                                                             // chunk summary (and the device loop's next level)

@@ -671,6 +671,58 @@ __device__ __forceinline__ uint64_t l_index(const ulonglong2 f, uint64_t mask) {
     return (f.x ^ (f.x >> 31) ^ (f.y >> 7)) & mask;
 }
 
+// ---- in-launch election (fused single-GPU level) -------------------------------------------
+// The first successor in TLC order (smallest slot q) per new fingerprint wins.  Election slot g
+// holds the fingerprint in LXY[g] -- both words carry the chunk's 16-bit tag in their low bits,
+// so slots of earlier chunks read as free and the table is never cleared (the host clears it
+// once every 65535 epochs) -- and the election word L[g] = elect_key(epoch, smallest q).  The
+// word of a newer epoch is smaller than any older one (and than the all-ones initial value), so
+// every candidate just takes the minimum.  All accesses are agent-scope atomics on the slot's
+// own words: a claimer CASes x then stores y; a candidate that finds x equal but y not yet
+// tagged retries the same slot on its next iteration (never spinning in place, so a claimer
+// in the same wave always gets to its store).
+__device__ __forceinline__ uint32_t elect_tag(uint32_t epoch) { return epoch % 0xFFFFu + 1u; }
+__device__ __forceinline__ unsigned long long elect_key(uint32_t epoch, uint64_t q) {
+    return ((unsigned long long)(0xFFFFFFFFu - epoch) << 32) | (unsigned long long)(uint32_t)q;
+}
+
+// The candidate that becomes a slot's minimum adds one to its parent's winner count (wacc) and
+// takes one off the parent of the candidate it displaced (the old minimum the atomic returns), so
+// once the launch is done wacc holds winners per parent.
+template <int MAXS>
+__device__ __forceinline__ uint32_t elect_slot(ulonglong2 *LXY, unsigned long long *L, uint32_t *wacc, uint64_t mask,
+                                               uint32_t epoch, const ulonglong2 f, uint64_t q) {
+    const unsigned long long tag = elect_tag(epoch);
+    const unsigned long long xk = (f.x & ~0xFFFFull) | tag, yk = (f.y & ~0xFFFFull) | tag;
+    uint64_t g = l_index(f, mask);
+    for (;;) {
+        unsigned long long *px = &LXY[g].x, *py = &LXY[g].y;
+        unsigned long long v = __hip_atomic_load(px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v & 0xFFFFull) != tag) {
+            const unsigned long long prev = atomicCAS(px, v, xk);
+            if (prev == v) {
+                __hip_atomic_store(py, yk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            v = prev;
+            if ((v & 0xFFFFull) != tag) continue;
+        }
+        if (v == xk) {
+            const unsigned long long y = __hip_atomic_load(py, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((y & 0xFFFFull) != tag) continue;  // the claimer's y is not visible yet: this slot again
+            if (y == yk) break;
+        }
+        g = (g + 1) & mask;
+    }
+    const unsigned long long mine = elect_key(epoch, q);
+    const unsigned long long old = atomicMin(&L[g], mine);
+    if (old > mine) {
+        atomicAdd(&wacc[q / MAXS], 1u);
+        if ((old >> 32) == (mine >> 32)) atomicSub(&wacc[(uint32_t)old / MAXS], 1u);
+    }
+    return (uint32_t)g;
+}
+
 __device__ __forceinline__ void t_insert(ulonglong2 *T, uint64_t mask, ulonglong2 f) {
     uint64_t h = t_index(f, mask);
     for (;;) {
@@ -889,7 +941,8 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
                         // the seen set is read-only in this launch (commit inserts)
                         const uint64_t q = pl * (uint64_t)S::MAXS + lo;
                         P.fp[q] = f;
-                        P.lslot[q] = t_contains(P.T, P.Tmask, f) ? LS_SEEN : LS_ELECT;
+                        P.lslot[q] = t_contains(P.T, P.Tmask, f) ? LS_SEEN
+                                                                 : elect_slot<S::MAXS>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q);
                     } else {
                         P.fp[((MODE == M_HASH) ? (uint64_t)P.off[pl] : 0ull) + lo] = f;
                     }
@@ -994,42 +1047,7 @@ __global__ __launch_bounds__(64) void k_inv_states(KParams P, uint64_t n, int32_
     for (int b = 0; b < 7; b++) out[i * 7 + b] = inv_eval<N, V>(c, b);
 }
 
-// ---- fused level: election, winner counts, commit --------------------------------------------
-// Thread per sparse successor slot q = pl * MAXS + r (r < cnt[pl]): elect the first slot in TLC
-// order (smallest q) per fingerprint not yet in the seen set.  L slots hold (epoch << 32) | q; a
-// slot of another epoch is empty, so the table is never cleared.  fp was written by the previous
-// launch, so reading another slot's fingerprint needs no fence.
-template <int N, int V, int MR>
-__global__ __launch_bounds__(256) void k_elect(KParams P) {
-    using S = Spec<N, V, MR>;
-    if (!level_args(P)) return;
-    const uint64_t np = P.p_end - P.p_begin;
-    const uint64_t nq = np * (uint64_t)S::MAXS;
-    const unsigned long long tag = (unsigned long long)P.epoch << 32;
-    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t pl = q / S::MAXS;
-        const uint32_t r = (uint32_t)(q - pl * S::MAXS);
-        if (r >= P.cnt[pl] || P.lslot[q] != LS_ELECT) continue;
-        const ulonglong2 f = P.fp[q];
-        uint64_t g = l_index(f, P.Lmask);
-        const unsigned long long mine = tag | q;
-        for (;;) {
-            unsigned long long v = __hip_atomic_load(&P.L[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((v >> 32) != P.epoch) {
-                const unsigned long long prev = atomicCAS(&P.L[g], v, mine);
-                if (prev == v) break;
-                v = prev;
-            }
-            if ((v >> 32) == P.epoch) {
-                const ulonglong2 o = P.fp[(uint32_t)v];
-                if (o.x == f.x && o.y == f.y) { atomicMin(&P.L[g], mine); break; }
-            }
-            g = (g + 1) & P.Lmask;
-        }
-        P.lslot[q] = (uint32_t)g;
-    }
-}
-
+// ---- fused level: winner counts, commit --------------------------------------------------------
 // Exclusive scan of one value per thread over a 1024-thread block (16 waves); *total gets the
 // block's sum.  ws holds 16 words of LDS.
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *ws, uint32_t *total) {
@@ -1054,13 +1072,12 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *ws, ui
     return base + x - v;
 }
 
-// One 1024-thread block per WTILE-parent tile, thread per parent: winners per parent (wcnt),
-// their exclusive scan inside the tile (wpos), and per tile the winners (bw) and successors
-// generated (bg).  The last block to finish scans the tile totals into boff and writes
+// One 1024-thread block per WTILE-parent tile, thread per parent: winners per parent (wcnt, as the
+// election counted them in wacc), their exclusive scan inside the tile (wpos), and per tile the
+// winners (bw) and successors generated (bg).  The last block to finish scans the tile totals into boff and writes
 // {generated, winners} to sum[0..1] -- the only values the host needs before commit.
 template <int N, int V, int MR>
 __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
-    using S = Spec<N, V, MR>;
     __shared__ uint32_t ws[16];
     __shared__ uint32_t flag;
     if (!level_args(P)) return;
@@ -1070,22 +1087,11 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
         const uint64_t pl = (uint64_t)tile * WTILE + threadIdx.x;
         uint32_t w = 0, t = 0;
         if (pl < np) {
+            // winners per parent were counted by the election itself; the accumulator is
+            // re-armed for the next chunk here
             t = P.cnt[pl];
-            // 8 slots at a time: their slot loads, then their election-word loads, go out
-            // together instead of as a chain of 2t dependent round trips
-            for (uint32_t r0 = 0; r0 < t; r0 += 8) {
-                uint32_t g[8];
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint32_t r = r0 + (uint32_t)k;
-                    g[k] = r < t ? P.lslot[pl * (uint64_t)S::MAXS + r] : LS_SEEN;
-                }
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint32_t q = (uint32_t)(pl * (uint64_t)S::MAXS + r0 + (uint32_t)k);
-                    w += (g[k] < LS_ELECT && (uint32_t)P.L[g[k]] == q) ? 1u : 0u;
-                }
-            }
+            w = P.wacc[pl];
+            P.wacc[pl] = 0u;
         }
         uint32_t wt, gt;
         const uint32_t x = block_excl_scan(w, ws, &wt);
@@ -1297,13 +1303,6 @@ struct Launch {
     static void fused(const KParams &P, hipStream_t s) {
         hipLaunchKernelGGL((k_expand<N, V, MR, M_FUSED>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
     }
-    static unsigned slot_grid(uint64_t np) {
-        const uint64_t b = (np * (uint64_t)Spec<N, V, MR>::MAXS + 255) / 256, cap = 256ull * 16ull;
-        return (unsigned)(b < cap ? (b ? b : 1) : cap);
-    }
-    static void elect(const KParams &P, uint64_t np, hipStream_t s) {
-        hipLaunchKernelGGL((k_elect<N, V, MR>), dim3(slot_grid(np)), dim3(256), 0, s, P);
-    }
     static void wincount(const KParams &P, uint64_t np, hipStream_t s) {
         const uint64_t tiles = (np + WTILE - 1) / WTILE;
         hipLaunchKernelGGL((k_wincount<N, V, MR>), dim3(tiles ? (unsigned)tiles : 1u), dim3(1024), 0, s, P);
@@ -1330,7 +1329,6 @@ static void fill(KernelSet *ks) {
     ks->materialize = &Launch<N, V, MR>::mat;
     ks->single = &Launch<N, V, MR>::single;
     ks->fused = &Launch<N, V, MR>::fused;
-    ks->elect = &Launch<N, V, MR>::elect;
     ks->wincount = &Launch<N, V, MR>::wincount;
     ks->commit = &Launch<N, V, MR>::commit;
     ks->fp_states = &Launch<N, V, MR>::fps;
