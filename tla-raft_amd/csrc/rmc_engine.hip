@@ -168,7 +168,7 @@ struct Shard {
     uint32_t lxy_epoch0 = 0;    // epoch of the last LXY clear (16-bit tags repeat after 65535 epochs)
     // fused single-shard level: sparse successor staging (slot q = chunk parent * maxsucc + rank)
     uint4 *score = nullptr, *saux = nullptr;
-    uint32_t *wcnt = nullptr, *wacc = nullptr, *bw = nullptr, *bg = nullptr, *boff = nullptr, *tickets = nullptr;
+    uint32_t *wcnt = nullptr, *wacc = nullptr, *ctick = nullptr, *bw = nullptr, *bg = nullptr, *boff = nullptr, *tickets = nullptr;
     // device-driven level loop: control block, per-level records, and their pinned host copies
     LevelCtl *ctl = nullptr, *hctl = nullptr, *hsnap = nullptr;
     LevelRec *lrec = nullptr, *hlrec = nullptr;
@@ -270,7 +270,7 @@ struct rmc_ctx {
         KParams Q = base(s);
         Q.front = front; Q.next = next;
         Q.cnt = s.cnt; Q.fp = s.fp; Q.wpos = s.wpos; Q.wcnt = s.wcnt; Q.wacc = s.wacc;
-        Q.bw = s.bw; Q.bg = s.bg; Q.boff = s.boff; Q.tickets = s.tickets; Q.sum = s.sum;
+        Q.bw = s.bw; Q.bg = s.bg; Q.boff = s.boff; Q.tickets = s.tickets; Q.ctick = s.ctick; Q.sum = s.sum;
         Q.score = s.score; Q.saux = s.saux; Q.lslot = s.lslot; Q.L = s.L; Q.LXY = s.LXY;
         return Q;
     }
@@ -530,6 +530,8 @@ struct rmc_ctx {
             s.saux = dmalloc<uint4>(Gcap);
             s.wcnt = dmalloc<uint32_t>(chunk_parents + 1);
             s.wacc = dmalloc<uint32_t>(chunk_parents + 1);
+            s.ctick = dmalloc<uint32_t>(33 * 32);
+            HIPCHK(hipMemsetAsync(s.ctick, 0, 33 * 32 * 4, stream));
             HIPCHK(hipMemsetAsync(s.wacc, 0, (chunk_parents + 1) * 4, stream));
             s.bw = dmalloc<uint32_t>(1024);
             s.bg = dmalloc<uint32_t>(1024);
@@ -584,7 +586,7 @@ struct rmc_ctx {
         dfree(s.okey2); dfree(s.iota); dfree(s.perm); dfree(s.sflag); dfree(s.spos); dfree(s.sfp); dfree(s.ocnt);
         dfree(s.rfp); dfree(s.rlslot); dfree(s.rflag); dfree(s.rpos); dfree(s.rcount); dfree(s.sx); dfree(s.rx);
         dfree(s.pick_idx); dfree(s.err); dfree(s.sum); dfree(s.flags);
-        dfree(s.score); dfree(s.saux); dfree(s.wcnt); dfree(s.wacc); dfree(s.bw); dfree(s.bg); dfree(s.boff); dfree(s.tickets);
+        dfree(s.score); dfree(s.saux); dfree(s.wcnt); dfree(s.wacc); dfree(s.ctick); dfree(s.bw); dfree(s.bg); dfree(s.boff); dfree(s.tickets);
         dfree(s.ctl); dfree(s.lrec);
         if (s.hsum) (void)hipHostFree(s.hsum);
         if (s.hctl) (void)hipHostFree(s.hctl);

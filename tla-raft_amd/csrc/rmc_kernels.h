@@ -95,6 +95,7 @@ struct KParams {
     uint32_t *wacc;            // winners per parent as the election counts them (0 between chunks)
     uint32_t *bw, *bg, *boff;  // per tile: winners, successors generated, first winner's offset
     uint32_t *tickets;         // [0] winner-count pass: last-block counter (0 between launches)
+    uint32_t *ctick;           // commit pass: arrival counters (last_commit_block; 0 between launches)
     unsigned long long *sum;   // chunk summary {generated, winners, error keys[ERR_NSLOTS], flags}
     LevelCtl *ctl;             // device-driven level loop (nullptr: the host drives the chunk)
     LevelRec *lrec;            // statistics of each level the device loop commits

@@ -1119,46 +1119,79 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
     }
 }
 
-// Chunk summary, after the commit pass: {generated, winners} (from the winner
+// Chunk summary, by the last block of the commit pass (one wave): {generated, winners} (from the winner
 // count pass), the error keys and flags (then re-armed).  In device-loop mode it also
 // records the level and advances the control block to the next one -- or stops the loop.
 template <int MAXS>
 __device__ void finish_level(const KParams &P) {
+    // one wave, everything it reads in flight at once: lanes 0..3 take the error slots, lane 4
+    // the flags, lane 0 the summary and the control block
+    const int lane = threadIdx.x;
+    unsigned long long e = 0;
+    if (lane < ERR_NSLOTS)
+        e = __hip_atomic_exchange(&P.err[lane], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (lane == ERR_NSLOTS)
+        e = __hip_atomic_exchange(&P.flags[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool bad = __ballot(lane < ERR_NSLOTS ? e != ~0ull : (lane == ERR_NSLOTS && e != 0)) != 0;
     unsigned long long *sm = P.sum;
+    if (lane <= ERR_NSLOTS) sm[2 + lane] = e;
+    if (lane != 0) return;
     const unsigned long long G = sm[0], Wn = sm[1];
-    bool bad = false;
-    for (int k = 0; k < ERR_NSLOTS; k++) {
-        const unsigned long long e = __hip_atomic_exchange(&P.err[k], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sm[2 + k] = e;
-        bad |= e != ~0ull;
+    if (!P.ctl) return;
+    LevelCtl c = *P.ctl;
+    if (bad) {  // the host reports the error from this level's buffers
+        P.ctl->stop = CTL_ERROR;
+        return;
     }
-    const uint32_t fl = __hip_atomic_exchange(&P.flags[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sm[2 + ERR_NSLOTS] = fl;
-    bad |= fl != 0;
-    LevelCtl *c = P.ctl;
-    if (!c) return;
-    if (bad) { c->stop = CTL_ERROR; return; }  // the host reports the error from this level's buffers
-    if (c->done_levels < (uint32_t)LREC_CAP) {
-        LevelRec &r = P.lrec[c->done_levels];
-        r.expanded = c->cur_n;
+    if (c.done_levels < (uint32_t)LREC_CAP) {
+        LevelRec &r = P.lrec[c.done_levels];
+        r.expanded = c.cur_n;
         r.generated = G;
         r.new_states = Wn;
     }
-    c->done_levels++;
-    c->gid_cur += c->cur_n;
-    c->cur_n = Wn;
-    c->T_count += Wn;
-    c->level++;
-    c->epoch++;
+    c.done_levels++;
+    c.gid_cur += c.cur_n;
+    c.cur_n = Wn;
+    c.T_count += Wn;
+    c.level++;
+    c.epoch++;
     const unsigned long long Gub = Wn * (unsigned long long)MAXS;
     unsigned long long lc = 1;
     while (lc < 2 * Gub) lc <<= 1;
-    c->Lmask = (lc < c->Lcap_max ? lc : c->Lcap_max) - 1;
+    c.Lmask = (lc < c.Lcap_max ? lc : c.Lcap_max) - 1;
     if (Wn == 0)
-        c->stop = CTL_DONE;
-    else if (c->done_levels >= c->batch || c->done_levels >= (uint32_t)LREC_CAP || Wn > c->chunk_parents ||
-             Gub > c->nxt_cap || c->gid_cur + Wn + Gub > c->trace_cap || 2 * (c->T_count + Gub) > c->T_cap)
-        c->stop = CTL_HOST;  // the next level is not known to fit the buffers: the host grows them
+        c.stop = CTL_DONE;
+    else if (c.done_levels >= c.batch || c.done_levels >= (uint32_t)LREC_CAP || Wn > c.chunk_parents ||
+             Gub > c.nxt_cap || c.gid_cur + Wn + Gub > c.trace_cap || 2 * (c.T_count + Gub) > c.T_cap)
+        c.stop = CTL_HOST;  // the next level is not known to fit the buffers: the host grows them
+    *P.ctl = c;
+}
+
+// True in the last one-wave block of the commit pass to get here, among the nb blocks that had a
+// parent (the others leave without arriving).  Arrivals go to CTICK_SUB counters (block b to
+// b % CTICK_SUB, each on its own 128-B line) and the last arriver of each to one top counter, so
+// no counter sees more than nb / CTICK_SUB atomics.  No fence: the last
+// block reads nothing that this launch wrote except the error words, and those are atomics that
+// every wave has completed (vmcnt(0)) before its arrival.  Counters re-arm themselves.
+constexpr uint32_t CTICK_SUB = 32, CTICK_STRIDE = 32;
+__device__ __forceinline__ bool last_commit_block(uint32_t *tick, uint32_t nb) {
+    if (blockIdx.x >= nb) return false;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t last = 0;
+    if (threadIdx.x == 0) {
+        const uint32_t g = nb, b = blockIdx.x, sub = b % CTICK_SUB;
+        const uint32_t nsub = g < CTICK_SUB ? g : CTICK_SUB;
+        const uint32_t expect = (g - sub + CTICK_SUB - 1) / CTICK_SUB;  // blocks with b % CTICK_SUB == sub
+        uint32_t *c = tick + sub * CTICK_STRIDE, *top = tick + CTICK_SUB * CTICK_STRIDE;
+        if (__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == expect - 1) {
+            __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsub - 1) {
+                __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = 1;
+            }
+        }
+    }
+    return __builtin_amdgcn_readfirstlane(last) != 0;
 }
 
 // Write the staged successor held by lane t as a record at rec_out (whole wave): core words
@@ -1270,15 +1303,10 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
             done += (uint32_t)__popcll(m);
         }
     }
-}
-
-// The chunk summary / device-loop step as its own one-lane launch: a last-block hand-off in the
-// commit pass would put every one of its (up to 8192) blocks through one arrival counter.
-template <int N, int V, int MR>
-__global__ __launch_bounds__(64) void k_finish(KParams P) {
-    if (threadIdx.x != 0) return;
-    if (P.ctl && P.ctl->stop != CTL_RUN) return;
-    finish_level<Spec<N, V, MR>::MAXS>(P);
+    // the last block to leave finishes the level (finish_level)
+    const uint64_t np = P.p_end - P.p_begin;
+    const uint32_t nb = np < gridDim.x ? (np ? (uint32_t)np : 1u) : gridDim.x;
+    if (last_commit_block(P.ctick, nb)) finish_level<S::MAXS>(P);
 }
 
 static inline unsigned grid_for(uint64_t n) {
@@ -1309,7 +1337,6 @@ struct Launch {
     }
     static void commit(const KParams &P, hipStream_t s) {
         hipLaunchKernelGGL((k_commit<N, V, MR>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
-        hipLaunchKernelGGL((k_finish<N, V, MR>), dim3(1), dim3(64), 0, s, P);
     }
     static void fps(const KParams &P, uint64_t n, hipStream_t s) {
         hipLaunchKernelGGL((k_fp_states<N, V, MR>), dim3(grid_for(n)), dim3(64), 0, s, P, n);
