@@ -47,12 +47,14 @@ TIMING_EVERY = 4
 def alg_bytes(phase, F, G, N, S, CWB):
     """Algorithmic HBM bytes of one phase of the fused single-GPU level (DESIGN.md "Kernels"):
     F parents of S-byte records, G generated successors, N new states, CWB core bytes."""
-    if phase == "expand_hash":   # k_expand<FUSED>: parents in; per successor: staged core + aux + fp + slot, one seen-set probe
-        return F * S + F * 8 + G * (CWB + 16 + 16 + 4) + G * 16
-    if phase == "dedup":         # k_elect + k_wincount + scan: fp, slot, election word per successor; counts per parent
-        return G * (4 + 16 + 8 + 4 + 8) + F * (4 + 4 + 8)
-    if phase == "materialize":   # k_commit: per parent wpos/cnt + parent ids; per new state: staging in, record out,
-        return F * (8 + 4) + F * (S - CWB) + N * (CWB + 16 + 4 + 8 + 16 + S + 16 + 10)  # seen insert, trace
+    if phase == "expand_hash":   # k_expand<FUSED>: parents in, successor count out; per successor: staged core + aux +
+        # fp + slot, one 16-B seen-set probe; per new fingerprint at least one election (16-B slot, 8-B word, count)
+        return F * S + F * 4 + G * (CWB + 16 + 16 + 4) + G * 16 + N * (16 + 8 + 4)
+    if phase == "dedup":         # k_wincount: per parent successor count, winner count (read + re-arm), its scan
+        return F * (4 + 4 + 4 + 4 + 4)
+    if phase == "materialize":   # k_commit: per parent wcnt/offsets/count + its message ids; per slot of a parent
+        # with winners its election slot + word; per new state: staging in, seen insert, trace, record out
+        return F * (4 + 8 + 4) + F * (S - CWB) + G * (4 + 8) + N * (CWB + 16 + 16 + 16 + 8 + 2 + S)
     return 0
 
 
@@ -91,6 +93,7 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe-peak", action="store_true")
+    ap.add_argument("--no-scale", action="store_true", help="skip the at-scale reference exhaustion (N=1)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -225,6 +228,8 @@ def main():
         "roofline": roof,
         "seen_set": seen,
     }
+    if rank == 0 and world == 1 and not args.no_scale:
+        line["at_scale"] = at_scale(local, S, CWB)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(w)
     if rank == 0:
@@ -234,7 +239,38 @@ def main():
         dist.destroy_process_group()
 
 
+def at_scale(device, S, CWB, workload="n3v2e2"):
+    """One exhaustion of a larger configuration (not the headline): levels of up to ~10^6 states,
+    where the level loop is throughput-bound rather than latency-bound.  Reports the run's
+    distinct states/s and the fused expansion kernel's algorithmic GB/s over the whole run."""
+    import raftmc
+    w = WORKLOADS[workload]
+    cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
+                             invariants=("Inv",), check_deadlock=False, device=device, timing_phases=TIMED_PHASES)
+    with raftmc.ModelChecker(cfg) as mc:
+        mc.set_timing(0)
+        mc.run()  # warm: buffers grown to the run's size
+        mc.reset()
+        t0 = time.perf_counter()
+        res = mc.run()
+        dt = time.perf_counter() - t0
+        mc.reset()
+        mc.set_timing(TIMED_PHASES)
+        timed = mc.run()
+    ms = sum(ls.kernel_ms[PHASES.index("expand_hash")] for ls in timed.levels)
+    F = sum(ls.expanded for ls in timed.levels)
+    G = sum(ls.generated for ls in timed.levels)
+    N = sum(ls.new_states for ls in timed.levels)
+    gbs = alg_bytes("expand_hash", F, G, N, S, CWB) / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    return {"workload": w["desc"], "distinct_states": res.distinct, "states_generated": res.generated,
+            "depth": res.depth, "seconds": round(dt, 4), "distinct_per_s": round(res.distinct / dt, 1),
+            "generated_per_s": round(res.generated / dt, 1),
+            "expand_kernel_ms": round(ms, 3), "expand_alg_GBps": round(gbs, 1),
+            "expand_frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
+
+
 KERNEL_NAME = {"expand_hash": "void rmc::k_expand<{n}, {V}, {mr}, 4>(rmc::KParams)",
+               "dedup": "void rmc::k_wincount<{n}, {V}, {mr}>(rmc::KParams)",
                "materialize": "void rmc::k_commit<{n}, {V}, {mr}>(rmc::KParams)"}
 
 
