@@ -17,7 +17,7 @@ timeout -k 10 300 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> 
 cat gpurun_out/bench.json
 if [ -n "$PROFILE" ]; then
   step rocprof
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-probe-peak > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-probe-peak --no-scale > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
   find gpurun_out/prof -name "*stats*" | head
 fi
 if [ -n "$EXPLORE" ]; then

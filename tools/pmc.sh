@@ -4,7 +4,7 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 cd "$R" || exit 1
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-ARGS="--steps 5 --warmup 1 --no-cpu-baseline --no-probe-peak ${BENCH_ARGS:-}"
+ARGS="--steps 5 --warmup 1 --no-cpu-baseline --no-probe-peak --no-scale ${BENCH_ARGS:-}"
 pass() {
   name=$1; shift
   echo "== pmc $name ($(date +%T))"
