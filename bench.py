@@ -14,11 +14,16 @@ MaxElection, MaxLogLen is |Vals|+1).  configs[2]/[3] (Raft.cfg as shipped, 5 ser
 not fit one GPU (>2.1e9 states by BFS level 37, still growing).
 
 N>1 (torchrun, one process per GPU): the same workload is exhausted ONCE by all ranks
-together -- seen set and frontier sharded by fingerprint owner, one RCCL exchange of
-fingerprints / winner flags / winner records per chunk; value =
-distinct states of the whole run / max-over-ranks time, scaling "strong" (total work
-fixed).  If the RCCL path fails to initialise, each rank exhausts its own copy instead
-and the line says "replicas" with the error.
+together through the engine's multi-GPU mode: levels below
+rmc_config.shard_min_states (default 2^20 states) are expanded whole on every rank --
+replicated, no exchange, TLC order -- and from the first level that reaches it the seen
+set and frontier are sharded by fingerprint owner with one RCCL exchange of fingerprints /
+winner flags / winner records per chunk.  configs[1]'s levels never exceed ~2*10^4 states,
+so at this workload every level is replicated and the whole-node rate is the one-GPU rate
+(a per-level exchange would cost more than the level: tools/shard_timing.py).  value =
+distinct states of the run / max-over-ranks time, scaling "strong" (total work fixed).  If
+the RCCL communicator fails to initialise, each rank exhausts its own copy instead and the
+line says "replicas" with the error.
 """
 import argparse
 import ctypes
@@ -118,7 +123,8 @@ def main():
             idt = torch.tensor(list(raftmc.comm_unique_id()), dtype=torch.uint8)
         dist.broadcast(idt, 0)
         cfg.rank, cfg.world_size, cfg.comm_unique_id = rank, world, bytes(idt.tolist())
-        parallelism = f"sharded-rccl-{world}"
+        parallelism = (f"rccl-{world}: fingerprint-owner sharding from the first level of >= 2^20 states, "
+                       f"smaller levels replicated on every GPU (all of this workload's)")
     mc, err = None, ""
     try:
         mc = raftmc.ModelChecker(cfg)

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RMC_ABI_VERSION 1
+#define RMC_ABI_VERSION 2
 
 /* ---- return codes ---------------------------------------------------------- */
 #define RMC_OK 0
@@ -83,6 +83,10 @@ typedef struct rmc_config {
     uint32_t timing_phases;    /* bit i: HIP-event time phase i into rmc_level_stats.kernel_ms (0 = all) */
     uint32_t device_levels;    /* single GPU: BFS levels enqueued per host round trip by rmc_run /
                                   rmc_run_levels (0 = auto, 1 = the host drives every level) */
+    uint64_t shard_min_states; /* world_size or virtual_shards > 1: levels with fewer states than this are
+                                  expanded whole on every shard (replicated, no exchange, TLC order); the run
+                                  switches to fingerprint-owner sharding at the first level that reaches it
+                                  and stays sharded (0 = auto: 2^20; 1 = sharded from Init's level) */
 } rmc_config;
 
 /* Statistics of one BFS level (what TLC's progress line reports). */

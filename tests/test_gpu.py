@@ -189,24 +189,27 @@ def test_seeded_trace_independent_of_chunking():
 SHARDED = ["n3_v1_e1_r3", "n3_v2_e1_r3", "n2_v2_e3_r3", "n4_v1_e1_r3", "n3_v1_e2_r3", "n5_v1_e1_r3", "n3_v3_e1_r3"]
 
 
+@pytest.mark.parametrize("shard_min", [1, 40])
 @pytest.mark.parametrize("shards", [2, 3, 8])
 @pytest.mark.parametrize("name", SHARDED)
-def test_sharded_bfs_matches_golden(name, shards):
+def test_sharded_bfs_matches_golden(name, shards, shard_min):
     """Owner-sharded exploration (order: chunk, source shard, TLC order) reaches the same
-    distinct/generated counts, depth and per-level sizes as TLC's -workers 1 order."""
+    distinct/generated counts, depth and per-level sizes as TLC's -workers 1 order -- sharded
+    from Init (shard_min 1), or replicated until a level reaches 40 states and sharded after."""
     g = LEVELS[name]
-    mc, res = run_cfg(g, virtual_shards=shards, chunk_successors=20000)
+    mc, res = run_cfg(g, virtual_shards=shards, chunk_successors=20000, shard_min_states=shard_min)
     check_levels(g, res)
     mc.close()
 
 
+@pytest.mark.parametrize("shard_min", [1, 30])
 @pytest.mark.parametrize("name", ["seeded_n3_v1_e2_r3", "seeded_n3_v2_e2_r3", "deadlock_n3_v1_e1_r3",
                                   "exist_lc_n3_v1_e2_r3"])
-def test_sharded_counterexample_is_valid_and_shortest(name):
+def test_sharded_counterexample_is_valid_and_shortest(name, shard_min):
     g = LEVELS[name]
     cfg = R.Config(n=g["n"], V=g["V"], max_election=g["E"], max_restart=g["R"], seeded=g["seeded"],
                    invariants=tuple(g["invariants"]), check_deadlock=g["check_deadlock"])
-    mc, res = run_cfg(g, virtual_shards=4, chunk_successors=20000)
+    mc, res = run_cfg(g, virtual_shards=4, chunk_successors=20000, shard_min_states=shard_min)
     assert res.status == {"ok": "done"}.get(g["verdict"], g["verdict"])
     assert res.trace_len == g["trace_len"]          # BFS: shortest counterexample, same length as TLC
     tr = mc.trace()

@@ -215,6 +215,10 @@ struct rmc_ctx {
 
     std::vector<Shard> sh;
     uint64_t chunk_parents = 0, Gcap = 0, Lcap_max = 0;
+    // W > 1: levels below shard_min states are expanded whole on every shard with the fused
+    // single-GPU level (replicated: no exchange); the run shards from the first level that reaches it
+    uint64_t shard_min = 0;
+    bool replicated = false;
 
     std::vector<hipEvent_t> evpool;
     std::vector<hipEvent_t> gev;  // device-loop group snapshots
@@ -491,11 +495,13 @@ struct rmc_ctx {
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 31)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^31");
         chunk_parents = Gcap / ks.maxsucc;
-        if (W == 1) chunk_parents = std::min<uint64_t>(chunk_parents, (uint64_t)WTILE * 1024);  // winner-count tiles
+        shard_min = W > 1 ? (cfg.shard_min_states ? cfg.shard_min_states : (1ull << 20)) : 0;
+        const bool fused_ok = W == 1 || shard_min > 1;  // shard 0 runs the fused single-GPU level
+        if (fused_ok) chunk_parents = std::min<uint64_t>(chunk_parents, (uint64_t)WTILE * 1024);  // winner-count tiles
         Lcap_max = next_pow2(2 * Gcap);
 
         sh.resize(virt ? W : 1);
-        for (size_t i = 0; i < sh.size(); i++) alloc_shard(sh[i], virt ? (int)i : rank);
+        for (size_t i = 0; i < sh.size(); i++) alloc_shard(sh[i], virt ? (int)i : rank, fused_ok && i == 0);
 
         d_one = dmalloc<uint32_t>(RECW);
         d_out = dmalloc<uint32_t>((size_t)ks.maxsucc * RECW);
@@ -510,7 +516,7 @@ struct rmc_ctx {
         HIPCHK(hipStreamSynchronize(stream));
     }
 
-    void alloc_shard(Shard &s, int id) {
+    void alloc_shard(Shard &s, int id, bool fused) {
         s.id = id;
         s.cnt = dmalloc<uint32_t>(chunk_parents + 1);
         s.off = dmalloc<uint32_t>(chunk_parents + 1);
@@ -521,9 +527,10 @@ struct rmc_ctx {
         HIPCHK(hipMemsetAsync(s.cnt, 0, (chunk_parents + 1) * 4, stream));
         HIPCHK(hipMemsetAsync(s.wflag, 0, (Gcap + 1) * 4, stream));
         s.L = dmalloc<unsigned long long>(Lcap_max);
-        // fused path: an all-ones election word is older than every epoch's (elect_key)
-        HIPCHK(hipMemsetAsync(s.L, W == 1 ? 0xFF : 0, Lcap_max * 8, stream));
-        if (W == 1) {
+        // an all-ones election word is older than every epoch's (elect_key) and, for the sharded
+        // path's (epoch << 32) | j words, of no epoch
+        HIPCHK(hipMemsetAsync(s.L, 0xFF, Lcap_max * 8, stream));
+        if (fused) {
             s.LXY = dmalloc<ulonglong2>(Lcap_max);
             HIPCHK(hipMemsetAsync(s.LXY, 0, Lcap_max * 16, stream));
             s.score = dmalloc<uint4>(Gcap * (uint64_t)(ks.CW / 4));
@@ -834,7 +841,8 @@ struct rmc_ctx {
         ks.fp_states(P, 1, stream);
         ks.inv_states(P, 1, d_inv, stream);
         uint32_t owner = 0;
-        if (W > 1) {
+        replicated = W > 1 && shard_min > 1;
+        if (W > 1 && !replicated) {
             launch_owner_of(d_fp1, (uint32_t)W, d_cnt1, stream);
             owner = d2h(d_cnt1);
         }
@@ -845,7 +853,7 @@ struct rmc_ctx {
         for (Shard &s : sh) {
             s.level_start = {0};
             s.cur_n = 0;
-            if ((uint32_t)s.id != owner) continue;
+            if (replicated ? &s != &sh[0] : (uint32_t)s.id != owner) continue;
             HIPCHK(hipMemcpyAsync(s.cur, d_one, RECW * 4, hipMemcpyDeviceToDevice, stream));
             launch_insert_fps(d_fp1, 1, s.T, s.T_cap - 1, stream);
             HIPCHK(hipMemcpyAsync(s.par, &none, 8, hipMemcpyHostToDevice, stream));
@@ -892,7 +900,55 @@ struct rmc_ctx {
         rmc_level_stats local;
         if (!st) st = &local;
         std::memset(st, 0, sizeof *st);
-        return W == 1 ? step_single(st) : step_sharded(st);
+        if (replicated && sh[0].cur_n >= shard_min) enter_sharded();
+        return (W == 1 || replicated) ? step_single(st) : step_sharded(st);
+    }
+
+    // Replicated -> sharded, at the start of the first level with >= shard_min states.  Every
+    // shard holds that level whole (and every state seen so far in its seen set); shard i keeps
+    // parents [F*i/W, F*(i+1)/W) as its frontier, so parent references of the next level,
+    // (i << 48 | gid), name shard i's copy of them.  Earlier replicated levels are referenced as
+    // shard 0's (tag 0), whose copy stays intact: each shard writes new states only past its range.
+    void enter_sharded() {
+        Shard &s0 = sh[0];
+        const size_t L = s0.level_start.size();
+        const uint64_t F = s0.cur_n, base = s0.level_start[L - 1];
+        auto off = [&](int i) { return F * (uint64_t)i / (uint64_t)W; };
+        if (virt) {
+            for (int i = 1; i < W; i++) {
+                Shard &t = sh[i];
+                const uint64_t o = off(i), n = off(i + 1) - o;
+                if (t.T_cap != s0.T_cap) {
+                    dfree(t.T);
+                    t.T = dmalloc<ulonglong2>(s0.T_cap);
+                    t.T_cap = s0.T_cap;
+                }
+                HIPCHK(hipMemcpyAsync(t.T, s0.T, s0.T_cap * 16, hipMemcpyDeviceToDevice, stream));
+                t.T_count = s0.T_count;
+                t.level_start = s0.level_start;
+                t.level_start.back() = base + o;
+                grow_records(t.cur, t.cur_cap, 0, std::max<uint64_t>(n, 1), RECW);
+                grow_trace(t, base + o + n + 1);
+                if (n) {
+                    HIPCHK(hipMemcpyAsync(t.cur, s0.cur + o * RECW, n * RECW * 4, hipMemcpyDeviceToDevice, stream));
+                    HIPCHK(hipMemcpyAsync(t.par + base + o, s0.par + base + o, n * 8, hipMemcpyDeviceToDevice, stream));
+                    HIPCHK(hipMemcpyAsync(t.pslot + base + o, s0.pslot + base + o, n * 2, hipMemcpyDeviceToDevice, stream));
+                }
+                t.cur_n = n;
+                t.epoch = std::max(t.epoch, s0.epoch);
+            }
+            s0.cur_n = off(1);
+        } else {
+            const uint64_t o = off(rank), n = off(rank + 1) - o;
+            grow_records(s0.nxt, s0.nxt_cap, 0, std::max<uint64_t>(n, 1), RECW);
+            if (n) HIPCHK(hipMemcpyAsync(s0.nxt, s0.cur + o * RECW, n * RECW * 4, hipMemcpyDeviceToDevice, stream));
+            std::swap(s0.cur, s0.nxt);
+            std::swap(s0.cur_cap, s0.nxt_cap);
+            s0.cur_n = n;
+            s0.level_start.back() = base + o;
+        }
+        HIPCHK(hipStreamSynchronize(stream));
+        replicated = false;
     }
 
     // First error in TLC order among the error slots: smaller (parent, slot) first; on a
@@ -1009,8 +1065,8 @@ struct rmc_ctx {
     int batch_levels() const { return cfg.device_levels ? (int)cfg.device_levels : LREC_CAP; }
     uint64_t dev_parents() const { return std::min<uint64_t>(chunk_parents, 1ull << 15); }
     bool batch_ok() const {
-        return W == 1 && inited && !finished && cfg.device_levels != 1 && sh[0].cur_n > 0 &&
-               sh[0].cur_n <= dev_parents();
+        return (W == 1 || (replicated && sh[0].cur_n < shard_min)) && inited && !finished && cfg.device_levels != 1 &&
+               sh[0].cur_n > 0 && sh[0].cur_n <= dev_parents();
     }
 
     // Returns the number of level stats written to out[0..maxl] (the error level included).
@@ -1036,7 +1092,7 @@ struct rmc_ctx {
         h.nxt_cap = std::min(s.cur_cap, s.nxt_cap);
         h.trace_cap = s.trace_cap;
         h.T_cap = s.T_cap;
-        h.chunk_parents = DP;
+        h.chunk_parents = replicated ? std::min<uint64_t>(DP, shard_min - 1) : DP;  // stop before sharding starts
         h.Lcap_max = Lcap_max;
         h.level = (uint32_t)L0;
         renew_election_tags(s, K + 1);
@@ -1575,6 +1631,7 @@ int rmc_comm_unique_id(void *out128) {
     ncclUniqueId id;
     if (ncclGetUniqueId(&id) != ncclSuccess) return RMC_E_COMM;
     static_assert(sizeof(id) <= 128, "ncclUniqueId larger than 128 bytes");
+    static_assert(sizeof(rmc_config) == 96, "rmc_config layout (ABI 2) changed: update INTEGRATION.md and raftmc");
     std::memset(out128, 0, 128);
     std::memcpy(out128, &id, sizeof id);
     return RMC_OK;

@@ -47,7 +47,7 @@ class _Config(ctypes.Structure):
         ("seen_log2", ctypes.c_int32), ("no_symmetry", ctypes.c_int32), ("chunk_successors", ctypes.c_uint64),
         ("rank", ctypes.c_int32), ("world_size", ctypes.c_int32), ("comm_unique_id", ctypes.c_void_p),
         ("virtual_shards", ctypes.c_int32), ("timing_phases", ctypes.c_uint32),
-        ("device_levels", ctypes.c_uint32),
+        ("device_levels", ctypes.c_uint32), ("shard_min_states", ctypes.c_uint64),
     ]
 
 
@@ -129,6 +129,7 @@ class ModelConfig:
     comm_unique_id: Optional[bytes] = None  # 128 bytes from comm_unique_id() on rank 0
     timing_phases: int = 0           # bit i: time phase i with HIP events (0 = all phases)
     device_levels: int = 0           # levels per host round trip in run() (0 = auto, 1 = host-driven)
+    shard_min_states: int = 0        # >1 shards: replicate levels below this size (0 = auto 2^20, 1 = always shard)
 
     def to_c(self) -> _Config:
         c = _Config()
@@ -149,6 +150,7 @@ class ModelConfig:
         c.virtual_shards = self.virtual_shards
         c.timing_phases = self.timing_phases
         c.device_levels = self.device_levels
+        c.shard_min_states = self.shard_min_states
         if self.comm_unique_id is not None:
             self._idbuf = ctypes.create_string_buffer(bytes(self.comm_unique_id), 128)
             c.comm_unique_id = ctypes.cast(self._idbuf, ctypes.c_void_p)
