@@ -691,13 +691,13 @@ __device__ __forceinline__ unsigned long long elect_key(uint32_t epoch, uint64_t
 // once the launch is done wacc holds winners per parent.
 template <int MAXS>
 __device__ __forceinline__ uint32_t elect_slot(ulonglong2 *LXY, unsigned long long *L, uint32_t *wacc, uint64_t mask,
-                                               uint32_t epoch, const ulonglong2 f, uint64_t q) {
+                                               uint32_t epoch, const ulonglong2 f, uint64_t q, uint64_t g,
+                                               unsigned long long v) {
+    // g = l_index(f, mask) and v = its x word, loaded by the caller together with the seen-set probe
     const unsigned long long tag = elect_tag(epoch);
     const unsigned long long xk = (f.x & ~0xFFFFull) | tag, yk = (f.y & ~0xFFFFull) | tag;
-    uint64_t g = l_index(f, mask);
     for (;;) {
         unsigned long long *px = &LXY[g].x, *py = &LXY[g].y;
-        unsigned long long v = __hip_atomic_load(px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((v & 0xFFFFull) != tag) {
             const unsigned long long prev = atomicCAS(px, v, xk);
             if (prev == v) {
@@ -709,10 +709,14 @@ __device__ __forceinline__ uint32_t elect_slot(ulonglong2 *LXY, unsigned long lo
         }
         if (v == xk) {
             const unsigned long long y = __hip_atomic_load(py, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((y & 0xFFFFull) != tag) continue;  // the claimer's y is not visible yet: this slot again
+            if ((y & 0xFFFFull) != tag) {  // the claimer's y is not visible yet: this slot again
+                v = __hip_atomic_load(px, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                continue;
+            }
             if (y == yk) break;
         }
         g = (g + 1) & mask;
+        v = __hip_atomic_load(&LXY[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const unsigned long long mine = elect_key(epoch, q);
     const unsigned long long old = atomicMin(&L[g], mine);
@@ -941,8 +945,14 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
                         // the seen set is read-only in this launch (commit inserts)
                         const uint64_t q = pl * (uint64_t)S::MAXS + lo;
                         P.fp[q] = f;
-                        P.lslot[q] = t_contains(P.T, P.Tmask, f) ? LS_SEEN
-                                                                 : elect_slot<S::MAXS>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q);
+                        // the election slot's first word goes out with the seen-set probe: one
+                        // round trip fewer for a new fingerprint
+                        const uint64_t g0 = l_index(f, P.Lmask);
+                        const unsigned long long v0 =
+                            __hip_atomic_load(&P.LXY[g0].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        P.lslot[q] = t_contains(P.T, P.Tmask, f)
+                                         ? LS_SEEN
+                                         : elect_slot<S::MAXS>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, g0, v0);
                     } else {
                         P.fp[((MODE == M_HASH) ? (uint64_t)P.off[pl] : 0ull) + lo] = f;
                     }
