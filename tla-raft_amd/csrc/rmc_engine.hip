@@ -102,10 +102,9 @@ struct Universe {
         for (size_t id = 0; id < items.size(); id++) {
             info[id] = items[id].info;
             nat2id[items[id].nat] = (uint16_t)id;
-            // per-message hash of everything but src/dst (those are positions in the pair sums)
-            const uint64_t body = items[id].info & ~0xFCull;
-            gmsg[id].x = mix64(SEED_MSG ^ mix64(body * 0x9e3779b97f4a7c15ULL + 1));
-            gmsg[id].y = mix64((SEED_MSG + 0x632be59bd9b4e019ULL) ^ mix64(body * 0xc2b2ae3d27d4eb4fULL + 7));
+            const MsgHash h = msg_hash(items[id].info);  // rmc_spec.h: the kernels' definition too
+            gmsg[id].x = h.x;
+            gmsg[id].y = h.y;
         }
         if (info.empty()) { info.push_back(0); gmsg.push_back(make_ulonglong2(0, 0)); }
     }

@@ -309,7 +309,7 @@ struct Wave {
 // Evaluate the message lane (round r) -> at most one successor.
 template <int N, int V, int MR>
 __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> &W, const uint16_t *ids, int r, int lane,
-                         Succ<N, V, MR> &o, uint32_t &assert_key) {
+                         Succ<N, V, MR> &o, uint32_t &assert_key, uint32_t *ainf) {
     using Lo = Layout<N, V>;
     o.key = KEY_NONE;
     o.nadd = 0;
@@ -352,6 +352,7 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
         if (has_id(ids, W.nm, g)) return;
         o.c[Lo::W_VF] = setnib(o.c[Lo::W_VF], s, src);
         o.add[0] = g; o.nadd = 1;
+        ainf[0] = minfo(VRESP, s, src, mt, 0, 0, 0, 0, 0, 0);
         o.key = slot_key(s, RV, k);
         return;
     }
@@ -378,12 +379,16 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
                 o.lw = nlw;
                 o.c[Lo::W_LL] = setnib(o.c[Lo::W_LL], s, nl);
             }
-            if (!has_id(ids, W.nm, resp)) { o.add[0] = resp; o.nadd = 1; }
+            if (!has_id(ids, W.nm, resp)) {
+                o.add[0] = resp; o.nadd = 1;
+                ainf[0] = minfo(ARESP, s, src, mt, pli + ent, 1, 0, 0, 0, 0);
+            }
             o.key = slot_key(s, FAE, k);
         } else {
             const uint32_t resp = P.t.nat2id[nat_aresp(P.d, s, src, mt, pli, 0)];
             if (has_id(ids, W.nm, resp)) return;
             o.add[0] = resp; o.nadd = 1;
+            ainf[0] = minfo(ARESP, s, src, mt, pli, 0, 0, 0, 0, 0);
             o.key = slot_key(s, FRE, k);
         }
         return;
@@ -421,7 +426,7 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
 // Evaluate the non-message slot owned by this lane (last round).
 template <int N, int V, int MR>
 __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR> &W, const uint16_t *ids, int lane,
-                          Succ<N, V, MR> &o) {
+                          Succ<N, V, MR> &o, uint32_t *ainf) {
     using Lo = Layout<N, V>;
     using S = Spec<N, V, MR>;
     o.key = KEY_NONE;
@@ -458,6 +463,7 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
             if (!has_id(ids, W.nm, id)) {
 #pragma unroll
                 for (int a = 0; a < S::NADD; a++) o.add[a] = ((uint32_t)a == na) ? id : o.add[a];
+                ainf[na] = minfo(VREQ, s, (uint32_t)p, term, ll, llt, 0, 0, 0, 0);
                 na++;
             }
         }
@@ -521,6 +527,7 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
         o.c[Lo::W_PEND] = W.c[Lo::W_PEND] | (1u << pb);
         o.add[0] = id;
         o.nadd = 1;
+        ainf[0] = minfo(AREQ, s, dst, ct, pli, plt, ci, ent, eb & 15u, eb >> 4);
         o.key = slot_key(s, LAE, dst);
         return;
     }
@@ -593,16 +600,18 @@ __device__ __forceinline__ void load_parent(const KParams &P, const uint32_t *re
 
 // hash row of the acting server: parent sums + the messages this successor adds
 template <int N, int V, int MR>
-__device__ __forceinline__ void succ_row(const KParams &P, const Succ<N, V, MR> &o, const uint64_t *M0,
-                                         const uint64_t *M1, uint64_t *row0, uint64_t *row1) {
+__device__ __forceinline__ void succ_row(const Succ<N, V, MR> &o, const uint64_t *M0, const uint64_t *M1,
+                                         const uint32_t *ainf, uint64_t *row0, uint64_t *row1) {
 #pragma unroll
     for (int j = 0; j < N; j++) { row0[j] = M0[o.s * N + j]; row1[j] = M1[o.s * N + j]; }
 #pragma unroll
     for (int a = 0; a < Spec<N, V, MR>::NADD; a++) {
         if ((uint32_t)a >= o.nadd) break;
-        const uint32_t id = o.add[a];
-        const uint32_t dst = mi_dst(P.t.info[id]);
-        const ulonglong2 g = P.t.gmsg[id];
+        // the added message's hash from its info word, built where it was generated: no
+        // dependent table loads after the id lookup
+        const uint32_t inf = ainf[a];
+        const uint32_t dst = mi_dst(inf);
+        const MsgHash g = msg_hash(inf);
 #pragma unroll
         for (int j = 0; j < N; j++) {
             row0[j] += ((uint32_t)j == dst) ? g.x : 0ull;
@@ -737,7 +746,7 @@ __device__ __forceinline__ void t_insert(ulonglong2 *T, uint64_t mask, ulonglong
 }
 
 template <int N, int V, int MR, int MODE>
-__global__ __launch_bounds__(64) void k_expand(KParams P) {
+__global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
     constexpr bool SUMS = (MODE == M_HASH || MODE == M_SINGLE || MODE == M_FUSED);
@@ -752,6 +761,7 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
     __shared__ uint8_t pimg[NPM * N];                   // permutation images
     __shared__ uint64_t sU[MAXS], sX[2][MAXS * N];      // compacted successor rows
     __shared__ uint32_t sS[MAXS];
+    __shared__ uint32_t sAinf[(MR + 1) * 64 * S::NADD];  // info words of the messages each candidate adds
     if (MODE == M_FUSED && !level_args(P)) return;
     const int lane = threadIdx.x;
     if (SUMS) {
@@ -773,8 +783,9 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
         Succ<N, V, MR> cand[MR + 1];
         uint32_t akey = KEY_NONE;
 #pragma unroll
-        for (int r = 0; r < MR; r++) eval_msg<N, V, MR>(P, W, ids, r, lane, cand[r], akey);
-        eval_slot<N, V, MR>(P, W, ids, lane, cand[MR]);
+        for (int r = 0; r < MR; r++)
+            eval_msg<N, V, MR>(P, W, ids, r, lane, cand[r], akey, &sAinf[(r * 64 + lane) * S::NADD]);
+        eval_slot<N, V, MR>(P, W, ids, lane, cand[MR], &sAinf[(MR * 64 + lane) * S::NADD]);
         // rank of every enabled successor in TLC order
         uint64_t en[MR + 1];
         uint32_t total = 0;
@@ -873,7 +884,7 @@ __global__ __launch_bounds__(64) void k_expand(KParams P) {
                 const Succ<N, V, MR> &o = cand[r];
                 const uint32_t sl = rank[r];
                 uint64_t row0[N], row1[N];
-                succ_row<N, V, MR>(P, o, M0, M1, row0, row1);
+                succ_row<N, V, MR>(o, M0, M1, &sAinf[(r * 64 + lane) * S::NADD], row0, row1);
                 const uint32_t vfs = nib(o.c[Lo::W_VF], o.s);
                 sU[sl] = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI], o.c[Lo::W_LL],
                                      o.lw, o.mirow, o.nirow, o.s);

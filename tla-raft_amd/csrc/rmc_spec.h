@@ -147,6 +147,16 @@ constexpr uint64_t SEED_PAIR = 0x9a1b2c3d4e5f6071ULL;
 constexpr uint64_t SEED_MSG = 0x0123456789abcdefULL;
 constexpr uint64_t PAIR_K0 = 0x9e3779b97f4a7c15ULL, PAIR_K1 = 0xc2b2ae3d27d4eb4fULL;
 
+// per-message hash pair of everything but src/dst (those are positions in the pair sums),
+// from the message's info word: the host's table (Universe::gmsg) and the expansion kernel's
+// added messages use this one definition
+struct MsgHash { uint64_t x, y; };
+RMC_HD MsgHash msg_hash(uint32_t info) {
+    const uint64_t body = (uint64_t)info & ~0xFCull;
+    return {mix64(SEED_MSG ^ mix64(body * 0x9e3779b97f4a7c15ULL + 1)),
+            mix64((SEED_MSG + 0x632be59bd9b4e019ULL) ^ mix64(body * 0xc2b2ae3d27d4eb4fULL + 7))};
+}
+
 // slot key (16 bit): server<<11 | action<<7 | witness -- increasing in TLC order
 RMC_HD uint32_t slot_key(uint32_t s, uint32_t a, uint32_t w) { return (s << 11) | (a << 7) | w; }
 RMC_HD uint32_t key_server(uint32_t k) { return k >> 11; }
