@@ -1267,25 +1267,31 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
     const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
     for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
         const uint64_t pl = p - P.p_begin;
-        if (!P.wcnt[pl]) continue;
-        const uint32_t w0 = P.boff[pl / WTILE] + P.wpos[pl];
+        // every load of the parent that depends on no other load goes out at once: its winner
+        // count, offsets, successor count, record word, message ids and first 64 election
+        // slots (read ahead of knowing whether they are needed; all in bounds)
+        const uint32_t wc = P.wcnt[pl];
+        const uint32_t bo = P.boff[pl / WTILE], wp = P.wpos[pl], t = P.cnt[pl];
         const uint32_t *rec = P.front + p * (uint64_t)S::RECW;
-        const uint32_t nm = (rec[Lo::W_MISC] >> 16) & 0xFFu;
+        const uint32_t misc = rec[Lo::W_MISC];
         const uint16_t *rid = reinterpret_cast<const uint16_t *>(rec + S::CW);
+        uint32_t idr[MR];
+#pragma unroll
+        for (int r = 0; r < MR; r++) idr[r] = rid[r * 64 + lane];
+        const uint32_t g0 = lane < S::MAXS ? P.lslot[pl * (uint64_t)S::MAXS + lane] : LS_SEEN;
+        if (!wc) continue;
+        const uint32_t w0 = bo + wp;
+        const uint32_t nm = (misc >> 16) & 0xFFu;
         uint32_t id[MR];
 #pragma unroll
-        for (int r = 0; r < MR; r++) {
-            const uint32_t k = (uint32_t)(r * 64 + lane);
-            id[r] = k < nm ? (uint32_t)rid[k] : 0xFFFFu;
-        }
-        const uint32_t t = P.cnt[pl];
+        for (int r = 0; r < MR; r++) id[r] = (uint32_t)(r * 64 + lane) < nm ? idr[r] : 0xFFFFu;
         uint32_t done = 0;
         for (uint32_t r0 = 0; r0 < t; r0 += 64) {
             const uint32_t r = r0 + (uint32_t)lane;
             const uint64_t q = pl * (uint64_t)S::MAXS + r;
             bool win = false;
             if (r < t) {
-                const uint32_t g = P.lslot[q];
+                const uint32_t g = r0 == 0 ? g0 : P.lslot[q];
                 win = g < LS_ELECT && (uint32_t)P.L[g] == (uint32_t)q;
             }
             const uint64_t m = __ballot(win);
