@@ -156,6 +156,15 @@ int rmc_set_timing(void *ctx, uint32_t phases);
  * buffers, so the next rmc_init starts a fresh run (TLC: a new invocation). */
 int rmc_reset(void *ctx);
 
+/* Checkpoint / resume between BFS levels (TLC's states/ metadir and -recover, .gitignore:2;
+ * SURVEY 8(f) item 4).  rmc_checkpoint writes the seen set, the current level, every state's
+ * parent reference and TLC's counters to `path`; single GPU (world_size 1, no virtual shards),
+ * after rmc_init and before the run finishes.  rmc_resume loads such a file into a context
+ * created with the same configuration and not yet initialised; rmc_step / rmc_run then carry
+ * on as if the run had never stopped (same counts, same TLC order, same counterexample). */
+int rmc_checkpoint(void *ctx, const char *path);
+int rmc_resume(void *ctx, const char *path);
+
 /* Loop rmc_step until done or an error; fills the final result. */
 int rmc_run(void *ctx, rmc_result *res);
 int rmc_get_result(void *ctx, rmc_result *res);

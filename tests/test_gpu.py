@@ -222,3 +222,70 @@ def test_sharded_counterexample_is_valid_and_shortest(name, shard_min):
     if g["verdict"] == "deadlock":
         assert R.successors(cfg, last) == []
     mc.close()
+
+
+# ---- checkpoint / resume (TLC's states/ metadir + -recover) ----------
+@pytest.mark.parametrize("name", ["n3_v1_e2_r3", "n3_v2_e1_r3", "seeded_n3_v1_e2_r3", "deadlock_n3_v1_e1_r3"])
+def test_checkpoint_resume_matches_uninterrupted(name, tmp_path):
+    """Stop after a few levels, checkpoint, and finish the run twice: in the same checker and in
+    a fresh one resumed from the file.  Both must give the golden counts, the golden per-level
+    sizes of the remaining levels and the identical counterexample."""
+    g = LEVELS[name]
+    cfg = dict(n_servers=g["n"], n_vals=g["V"], max_election=g["E"], max_restart=g["R"],
+               invariants=tuple(g["invariants"]), check_deadlock=g["check_deadlock"],
+               spec_variant=raftmc.SPEC_SEEDED if g["seeded"] else raftmc.SPEC_RAFT)
+    path = str(tmp_path / "run.ckpt")
+    a = raftmc.ModelChecker(raftmc.ModelConfig(**cfg))
+    a.init()
+    k = 0
+    while k < 6 and a.step().status == "ok":
+        k += 1
+    assert k == 6, "the configuration must run past the checkpoint level"
+    a.checkpoint(path)
+    done = len(a.levels)
+    res_a = a.run()
+    b = raftmc.ModelChecker(raftmc.ModelConfig(**cfg))
+    b.resume(path)
+    res_b = b.run()
+    check_levels(g, res_a)
+    for f in ("status", "generated", "distinct", "depth", "queue", "violated", "trace_len"):
+        assert getattr(res_b, f) == getattr(res_a, f), f
+    assert [ls.new_states for ls in res_b.levels] == [ls.new_states for ls in res_a.levels[done:]]
+    assert b.trace() == a.trace()
+    a.close()
+    b.close()
+
+
+def test_resume_rejects_another_configuration(tmp_path):
+    path = str(tmp_path / "run.ckpt")
+    with raftmc.ModelChecker(raftmc.ModelConfig(n_servers=3, n_vals=1, max_election=1, max_restart=3)) as a:
+        a.init()
+        a.step()
+        a.checkpoint(path)
+    with raftmc.ModelChecker(raftmc.ModelConfig(n_servers=3, n_vals=1, max_election=2, max_restart=3)) as b:
+        with pytest.raises(raftmc.RmcError, match="not a checkpoint of this configuration"):
+            b.resume(path)
+
+
+def test_launcher_checkpoint_and_recover(tmp_path):
+    """raftmc -checkpoint / -metadir / -recover (TLC's flags): a run checkpointed after its first
+    batch of levels, recovered in a second process, ends with the uninterrupted run's counts."""
+    import subprocess
+    from test_host import LAUNCHER, cfg_text
+    g = LEVELS["n3_v1_e2_r3"]
+    (tmp_path / "Raft.cfg").write_text(cfg_text(E=2, R=3, vals="v1"))
+    env = dict(os.environ, RMC_SKIP_SPEC_CHECK="1")
+    # a small initial seen set makes the device loop hand back to the host every few levels
+    base = [LAUNCHER, "-deadlock", "-seenlog2", "10", "-config", str(tmp_path / "Raft.cfg")]
+    meta = str(tmp_path / "states")
+    r1 = subprocess.run(base + ["-checkpoint", "0.000001", "-metadir", meta, str(tmp_path / "Raft.tla")],
+                        capture_output=True, text=True, env=env, timeout=120)
+    assert r1.returncode == 0, r1.stdout + r1.stderr
+    assert "Checkpointing completed" in r1.stdout and os.path.exists(os.path.join(meta, "raftmc.ckpt"))
+    want = f"{g['generated']} states generated, {g['distinct']} distinct states found, 0 states left on queue."
+    assert want in r1.stdout
+    r2 = subprocess.run(base + ["-checkpoint", "0", "-recover", meta, str(tmp_path / "Raft.tla")],
+                        capture_output=True, text=True, env=env, timeout=120)
+    assert r2.returncode == 0, r2.stdout + r2.stderr
+    assert "Recovery completed" in r2.stdout and want in r2.stdout
+    assert f"The depth of the complete state graph search is {g['depth']}." in r2.stdout

@@ -1569,6 +1569,124 @@ struct rmc_ctx {
     }
 
     // Forget every explored state but keep all device buffers (repeat runs, benchmarks).
+    // ---- checkpoint / resume (rmc_checkpoint, rmc_resume) --------------------------------
+    struct CkptHeader {
+        uint64_t magic;
+        uint32_t abi, recw;
+        int32_t n, v, e, r;
+        uint32_t invariants;
+        int32_t check_deadlock, spec_variant, no_symmetry, msg_cap, depth;
+        uint64_t total_generated, total_distinct, T_cap, T_count, cur_n, n_levels, trace_n;
+        uint32_t epoch, pad;
+        double seconds;
+    };
+    static constexpr uint64_t CKPT_MAGIC = 0x3150434b434d52ull;  // "RMCKCP1"
+
+    CkptHeader ckpt_header() const {
+        CkptHeader h{};
+        h.magic = CKPT_MAGIC;
+        h.abi = RMC_ABI_VERSION;
+        h.recw = (uint32_t)RECW;
+        h.n = cfg.n_servers; h.v = cfg.n_vals; h.e = cfg.max_election; h.r = cfg.max_restart;
+        h.invariants = cfg.invariants;
+        h.check_deadlock = cfg.check_deadlock; h.spec_variant = cfg.spec_variant;
+        h.no_symmetry = cfg.no_symmetry; h.msg_cap = ks.MCAP;
+        return h;
+    }
+
+    // device <-> file in bounded pieces through one pinned-free host buffer
+    template <class F>
+    void stream_bytes(void *dev, uint64_t bytes, F &&io) {
+        std::vector<char> buf((size_t)std::min<uint64_t>(bytes, 64ull << 20));
+        for (uint64_t o = 0; o < bytes; o += buf.size()) {
+            const size_t k = (size_t)std::min<uint64_t>(buf.size(), bytes - o);
+            io((char *)dev + o, buf.data(), k);
+        }
+    }
+
+    void checkpoint(const char *path) {
+        if (W != 1) throw Fail(RMC_E_ARG, "checkpoint: single-GPU runs only");
+        if (!inited || finished) throw Fail(RMC_E_STATE, "checkpoint: between levels of a started, unfinished run");
+        Shard &s = sh[0];
+        HIPCHK(hipStreamSynchronize(stream));
+        CkptHeader h = ckpt_header();
+        h.depth = depth;
+        h.total_generated = total_generated; h.total_distinct = total_distinct;
+        h.T_cap = s.T_cap; h.T_count = s.T_count; h.cur_n = s.cur_n;
+        h.n_levels = s.level_start.size();
+        h.trace_n = s.level_start.back() + s.cur_n;  // every state found so far has a global id below
+        h.epoch = s.epoch;
+        h.seconds = seconds;
+        FILE *f = std::fopen(path, "wb");
+        if (!f) throw Fail(RMC_E_ARG, std::string("checkpoint: cannot write ") + path);
+        bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 &&
+                  std::fwrite(s.level_start.data(), 8, s.level_start.size(), f) == s.level_start.size();
+        auto out = [&](void *dev, char *host, size_t k) {
+            HIPCHK(hipMemcpy(host, dev, k, hipMemcpyDeviceToHost));
+            ok = ok && std::fwrite(host, 1, k, f) == k;
+        };
+        stream_bytes(s.T, h.T_cap * 16, out);
+        stream_bytes(s.cur, h.cur_n * RECW * 4, out);
+        stream_bytes(s.par, h.trace_n * 8, out);
+        stream_bytes(s.pslot, h.trace_n * 2, out);
+        ok = (std::fclose(f) == 0) && ok;
+        if (!ok) throw Fail(RMC_E_ARG, std::string("checkpoint: short write to ") + path);
+    }
+
+    void resume(const char *path) {
+        if (W != 1) throw Fail(RMC_E_ARG, "resume: single-GPU runs only");
+        if (inited) throw Fail(RMC_E_STATE, "resume: needs a context not yet initialised (rmc_create or rmc_reset)");
+        FILE *f = std::fopen(path, "rb");
+        if (!f) throw Fail(RMC_E_ARG, std::string("resume: cannot read ") + path);
+        CkptHeader h{};
+        const CkptHeader want = ckpt_header();
+        bool ok = std::fread(&h, sizeof h, 1, f) == 1;
+        if (!ok || h.magic != CKPT_MAGIC || h.abi != want.abi || h.recw != want.recw || h.n != want.n ||
+            h.v != want.v || h.e != want.e || h.r != want.r || h.invariants != want.invariants ||
+            h.check_deadlock != want.check_deadlock || h.spec_variant != want.spec_variant ||
+            h.no_symmetry != want.no_symmetry || h.msg_cap != want.msg_cap || h.n_levels == 0 ||
+            (h.T_cap & (h.T_cap - 1)) != 0) {
+            std::fclose(f);
+            throw Fail(RMC_E_ARG, std::string("resume: ") + path + " is not a checkpoint of this configuration");
+        }
+        Shard &s = sh[0];
+        std::vector<uint64_t> ls(h.n_levels);
+        ok = std::fread(ls.data(), 8, ls.size(), f) == ls.size();
+        if (s.T_cap != h.T_cap) {
+            dfree(s.T);
+            s.T = dmalloc<ulonglong2>(h.T_cap);
+            s.T_cap = h.T_cap;
+        }
+        grow_records(s.cur, s.cur_cap, 0, std::max<uint64_t>(h.cur_n, 1), RECW);
+        grow_trace(s, h.trace_n + 1);
+        auto in = [&](void *dev, char *host, size_t k) {
+            ok = ok && std::fread(host, 1, k, f) == k;
+            if (ok) HIPCHK(hipMemcpy(dev, host, k, hipMemcpyHostToDevice));
+        };
+        stream_bytes(s.T, h.T_cap * 16, in);
+        stream_bytes(s.cur, h.cur_n * RECW * 4, in);
+        stream_bytes(s.par, h.trace_n * 8, in);
+        stream_bytes(s.pslot, h.trace_n * 2, in);
+        std::fclose(f);
+        if (!ok) throw Fail(RMC_E_ARG, std::string("resume: ") + path + " is truncated");
+        s.level_start = ls;
+        s.cur_n = h.cur_n;
+        s.T_count = h.T_count;
+        s.epoch = std::max(s.epoch, h.epoch);
+        total_generated = h.total_generated;
+        total_distinct = h.total_distinct;
+        depth = h.depth;
+        seconds = h.seconds;
+        trace.clear();
+        status = RMC_OK;
+        violated = -1;
+        err_ref = 0;
+        err_last_slot = KEY_NONE;
+        inited = true;
+        finished = s.cur_n == 0;
+        if (finished) { status = RMC_DONE; queue_at_end = 0; }
+    }
+
     void reset() {
         for (Shard &s : sh) {
             HIPCHK(hipMemsetAsync(s.T, 0, s.T_cap * 16, stream));
@@ -1717,6 +1835,24 @@ int rmc_reset(void *ctx) {
     rmc_ctx *c = (rmc_ctx *)ctx;
     return guarded(c, [&] {
         c->reset();
+        return RMC_OK;
+    });
+}
+
+int rmc_checkpoint(void *ctx, const char *path) {
+    rmc_ctx *c = (rmc_ctx *)ctx;
+    if (!path) return RMC_E_ARG;
+    return guarded(c, [&] {
+        c->checkpoint(path);
+        return RMC_OK;
+    });
+}
+
+int rmc_resume(void *ctx, const char *path) {
+    rmc_ctx *c = (rmc_ctx *)ctx;
+    if (!path) return RMC_E_ARG;
+    return guarded(c, [&] {
+        c->resume(path);
         return RMC_OK;
     });
 }

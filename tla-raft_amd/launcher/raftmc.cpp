@@ -35,6 +35,14 @@ std::string now_str() {
     return buf;
 }
 
+// TLC's metadir name: states/YY-MM-DD-HH-MM-SS
+std::string stamp_str() {
+    char buf[64];
+    std::time_t t = std::time(nullptr);
+    std::strftime(buf, sizeof buf, "%y-%m-%d-%H-%M-%S", std::localtime(&t));
+    return buf;
+}
+
 bool read_file(const std::string &path, std::string *out) {
     std::ifstream f(path, std::ios::binary);
     if (!f) return false;
@@ -188,7 +196,7 @@ struct Printer {
 
 int usage(const char *msg) {
     std::fprintf(stderr, "raftmc: %s\nusage: raftmc [-deadlock] [-workers N] [-config FILE.cfg] [-device D] "
-                         "[-msgcap C] [-seenlog2 K] FILE.tla\n", msg);
+                         "[-msgcap C] [-seenlog2 K] [-checkpoint MIN] [-metadir DIR] [-recover DIR] FILE.tla\n", msg);
     return 150;
 }
 
@@ -197,6 +205,8 @@ int usage(const char *msg) {
 int main(int argc, char **argv) {
     std::string tla_path, cfg_path;
     int check_deadlock = 1, device = -1, msgcap = 0, seenlog2 = 0, workers = 1;
+    double ckpt_minutes = 30.0;         // TLC -checkpoint: minutes between checkpoints (0 = never)
+    std::string metadir, recover_dir;   // TLC -metadir / -recover: where checkpoints go / come from
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto need = [&](const char *f) -> const char * {
@@ -209,6 +219,9 @@ int main(int argc, char **argv) {
         else if (a == "-device") device = std::atoi(need("-device"));
         else if (a == "-msgcap") msgcap = std::atoi(need("-msgcap"));
         else if (a == "-seenlog2") seenlog2 = std::atoi(need("-seenlog2"));
+        else if (a == "-checkpoint") ckpt_minutes = std::atof(need("-checkpoint"));
+        else if (a == "-metadir") metadir = need("-metadir");
+        else if (a == "-recover") recover_dir = need("-recover");
         else if (a.size() > 4 && a.compare(a.size() - 4, 4, ".tla") == 0) tla_path = a;
         else if (a[0] != '-' && tla_path.empty()) tla_path = a + ".tla";
         else return usage(("unsupported option " + a).c_str());
@@ -249,11 +262,27 @@ int main(int argc, char **argv) {
     void *ctx = nullptr;
     int rc = rmc_create(&cfg, &ctx);
     if (rc != RMC_OK) { std::printf("Error: could not start the GPU model checker (code %d)\n", rc); return 75; }
-    std::printf("Computing initial states...\n");
     rmc_level_stats st;
-    rc = rmc_init(ctx, &st);
-    if (rc < 0) { std::printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 75; }
-    std::printf("Finished computing initial states: 1 distinct state generated at %s.\n", now_str().c_str());
+    if (!recover_dir.empty()) {
+        // TLC -recover: carry on from the checkpoint in that directory (rmc_resume)
+        const std::string f = recover_dir + "/raftmc.ckpt";
+        std::printf("Starting recovery from checkpoint %s\n", recover_dir.c_str());
+        rc = rmc_resume(ctx, f.c_str());
+        if (rc < 0) { std::printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 75; }
+        rmc_result r0;
+        rmc_get_result(ctx, &r0);
+        std::printf("Recovery completed. %llu states examined. %llu states on queue.\n",
+                    (unsigned long long)r0.distinct, (unsigned long long)r0.queue);
+        if (metadir.empty()) metadir = recover_dir;
+        rc = r0.status;
+    } else {
+        std::printf("Computing initial states...\n");
+        rc = rmc_init(ctx, &st);
+        if (rc < 0) { std::printf("Error: %s\n", rmc_last_error(ctx)); rmc_destroy(ctx); return 75; }
+        std::printf("Finished computing initial states: 1 distinct state generated at %s.\n", now_str().c_str());
+    }
+    if (metadir.empty()) metadir = "states/" + stamp_str();
+    auto last_ckpt = std::chrono::steady_clock::now();
     double gpu_seconds = 0;
     std::vector<rmc_level_stats> lv(65);
     while (rc == RMC_OK) {
@@ -271,6 +300,16 @@ int main(int argc, char **argv) {
                         q.total_distinct / el * 60.0, (unsigned long long)q.queue);
         }
         std::fflush(stdout);
+        const double since = std::chrono::duration<double>(std::chrono::steady_clock::now() - last_ckpt).count();
+        if (rc == RMC_OK && ckpt_minutes > 0 && since >= ckpt_minutes * 60.0) {
+            // TLC -checkpoint: the run so far, between two levels (rmc_checkpoint)
+            std::printf("Checkpointing of run %s\n", metadir.c_str());
+            (void)std::system(("mkdir -p '" + metadir + "'").c_str());
+            const std::string f = metadir + "/raftmc.ckpt";
+            if (rmc_checkpoint(ctx, f.c_str()) < 0) std::printf("Warning: checkpoint failed: %s\n", rmc_last_error(ctx));
+            else std::printf("Checkpointing completed at (%s)\n", now_str().c_str());
+            last_ckpt = std::chrono::steady_clock::now();
+        }
     }
     if (rc < 0) {
         std::printf("Error: %s\n", rmc_last_error(ctx));

@@ -91,6 +91,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.rmc_probe_peak.argtypes = [i32, u32, u64, P(ctypes.c_double), P(ctypes.c_double)]
     lib.rmc_run.argtypes = [vp, P(_Result)]
     lib.rmc_reset.argtypes = [vp]
+    lib.rmc_checkpoint.argtypes = [vp, ctypes.c_char_p]
+    lib.rmc_resume.argtypes = [vp, ctypes.c_char_p]
     lib.rmc_run_levels.argtypes = [vp, P(_LevelStats), u32, P(u32), P(_Result)]
     lib.rmc_comm_unique_id.argtypes = [vp]
     lib.rmc_get_result.argtypes = [vp, P(_Result)]
@@ -358,6 +360,15 @@ class ModelChecker:
         self._check(self.lib.rmc_reset(self.h))
         self.levels = []
         self._inited = False
+
+    def checkpoint(self, path: str) -> None:
+        """Write the run so far (seen set, current level, parent references, counters) to path."""
+        self._check(self.lib.rmc_checkpoint(self.h, os.fsencode(path)))
+
+    def resume(self, path: str) -> None:
+        """Continue a checkpointed run of the same configuration (on a fresh or reset checker)."""
+        self._check(self.lib.rmc_resume(self.h, os.fsencode(path)))
+        self._inited = True
 
     def step(self) -> LevelStats:
         st = _LevelStats()
