@@ -50,7 +50,7 @@ extern "C" {
 #define RMC_INV_RAFT_CAN_COMMIT (1u << 2)          /* RaftCanCommt, Raft.tla:434 */
 #define RMC_INV_FOLLOWER_CAN_COMMIT (1u << 3)      /* Raft.tla:436-439 */
 #define RMC_INV_COMMIT_ALL (1u << 4)               /* Raft.tla:442 */
-#define RMC_INV_NO_ALL_COMMIT (1u << 5)            /* Raft.tla:451-481 (not yet compiled: rejected) */
+#define RMC_INV_NO_ALL_COMMIT (1u << 5)            /* Raft.tla:451-481 (reads msgs) */
 #define RMC_INV_EXIST_LEADER_AND_CANDIDATE (1u << 6) /* Raft.tla:483-487 */
 
 /* ---- spec variants ------------------------------------------------------------ */

@@ -3,6 +3,7 @@
 Bit-exact bar: identical successor lists (TLC order, keys and concrete states), identical
 symmetry classes, identical invariant values, identical per-level distinct/generated
 counts, depth, verdict and counterexample traces (tests/golden/, from oracle/)."""
+import dataclasses
 import json
 import os
 
@@ -67,7 +68,8 @@ def test_invariants_match_oracle(name):
     g = SAMPLES[name]
     cfg = R.Config(n=g["n"], V=g["V"], max_election=g["E"], max_restart=g["R"])
     mc = checker(g["n"], g["V"], g["E"], g["R"])
-    names = ["Inv", "NoSplitVote", "RaftCanCommt", "FollowerCanCommit", "CommitAll", "ExistLeaderAndCandidate"]
+    names = ["Inv", "NoSplitVote", "RaftCanCommt", "FollowerCanCommit", "CommitAll", "NoAllCommit",
+             "ExistLeaderAndCandidate"]
     for it in g["items"]:
         for sc in [it] + it["successors"][:4]:
             st = R.state_from_json(sc["state"])
@@ -77,6 +79,57 @@ def test_invariants_match_oracle(name):
                 except R.EvalError:
                     exp = None
                 assert mc.eval_invariant(sc["state"], nm) == exp, nm
+
+
+def _no_all_commit_state(msgs):
+    """n3 V1: s1 leads at term 1 with commitIndex 2, s2 committed, s3 not yet (tla:451-466)."""
+    e = (1, 0)
+    return R.State(votedFor=(0, 0, 0), currentTerm=(1, 1, 1), logs=(((0, -1), e),) * 3,
+                   matchIndex=((2, 2, 2), (1, 1, 1), (1, 1, 1)), nextIndex=((3, 3, 3), (2, 2, 2), (2, 2, 2)),
+                   commitIndex=(2, 2, 1), msgs=frozenset(msgs), role=(R.LEADER, R.FOLLOWER, R.FOLLOWER),
+                   electionCount=1, restartCount=0, pendingResponse=((False,) * 3,) * 3, valSent=(0,))
+
+
+def test_no_all_commit_reads_msgs():
+    """NoAllCommit (tla:451-481), the one invariant over msgs: TRUE with its three messages,
+    FALSE as soon as any one is missing or differs in a field the formula tests."""
+    cfg = R.Config(n=3, V=1, max_election=2, max_restart=3)
+    mc = checker(3, 1, 2, 3)
+    req1 = R.append_req(0, 2, 1, 1, 0, ((1, 0),), 1)
+    resp1 = R.append_resp(2, 0, 1, 1, True)
+    req2 = R.append_req(0, 2, 1, 2, 1, (), 2)
+    noise = [R.append_req(0, 1, 1, 1, 0, ((1, 0),), 1), R.append_resp(1, 0, 1, 2, True)]
+    cases = [
+        [req1, resp1, req2], [req1, resp1, req2] + noise, [resp1, req2], [req1, req2], [req1, resp1],
+        [R.append_req(0, 2, 2, 1, 0, ((1, 0),), 1), resp1, req2],   # term # currentTerm[s3]
+        [req1, R.append_resp(2, 0, 1, 1, False), req2],               # succ FALSE
+        [req1, R.append_resp(1, 0, 1, 1, True), req2],                # wrong src
+        [req1, resp1, R.append_req(0, 1, 1, 2, 1, (), 2)],            # wrong dst
+    ]
+    seen = set()
+    for msgs in cases:
+        st = _no_all_commit_state(msgs)
+        exp = R.INV_FUNCS["NoAllCommit"](cfg, st)
+        seen.add(exp)
+        assert mc.eval_invariant(R.state_to_json(st), "NoAllCommit") == exp, msgs
+    assert seen == {True, False}
+    # the state conjuncts: commitIndex of s3 must be 1
+    st = dataclasses.replace(_no_all_commit_state([req1, resp1, req2]), commitIndex=(2, 2, 2))
+    assert R.INV_FUNCS["NoAllCommit"](cfg, st) is False
+    assert mc.eval_invariant(R.state_to_json(st), "NoAllCommit") is False
+
+
+def test_no_all_commit_run_matches_oracle():
+    """INVARIANT NoAllCommit: FALSE at Init, so TLC stops there with a 1-state trace."""
+    cfg = R.Config(n=3, V=1, max_election=1, max_restart=3, invariants=("NoAllCommit",))
+    p = R.bfs(cfg)
+    mc = raftmc.ModelChecker(raftmc.ModelConfig(n_servers=3, n_vals=1, max_election=1, max_restart=3,
+                                                invariants=("NoAllCommit",)))
+    res = mc.run()
+    assert (res.status, res.generated, res.distinct) == (p.verdict, p.generated, p.distinct)
+    assert res.violated == p.violated == "NoAllCommit"
+    assert res.trace_len == len(p.trace) == 1
+    mc.close()
 
 
 def test_eval_error_state():

@@ -114,6 +114,7 @@ static const std::pair<const char *, uint32_t> kInvNames[] = {
     {"RaftCanCommt", RMC_INV_RAFT_CAN_COMMIT},
     {"FollowerCanCommit", RMC_INV_FOLLOWER_CAN_COMMIT},
     {"CommitAll", RMC_INV_COMMIT_ALL},
+    {"NoAllCommit", RMC_INV_NO_ALL_COMMIT},
     {"ExistLeaderAndCandidate", RMC_INV_EXIST_LEADER_AND_CANDIDATE},
 };
 

@@ -421,7 +421,6 @@ struct rmc_ctx {
         if (cfg.n_vals < 0 || cfg.n_vals > MAXV) throw Fail(RMC_E_ARG, "n_vals must be 0..3");
         if (cfg.max_election < 0 || cfg.max_election > 7) throw Fail(RMC_E_ARG, "max_election must be 0..7");
         if (cfg.max_restart < 0 || cfg.max_restart > 15) throw Fail(RMC_E_ARG, "max_restart must be 0..15");
-        if (cfg.invariants & RMC_INV_NO_ALL_COMMIT) throw Fail(RMC_E_ARG, "invariant NoAllCommit is not compiled");
         if (cfg.invariants & ~0x7Fu) throw Fail(RMC_E_ARG, "unknown invariant bits");
         const int ws = cfg.world_size > 1 ? cfg.world_size : 1;
         if (cfg.virtual_shards > 1 && ws > 1) throw Fail(RMC_E_ARG, "virtual_shards and world_size > 1 are exclusive");

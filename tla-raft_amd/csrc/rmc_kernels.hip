@@ -82,6 +82,15 @@ struct Succ {
     uint32_t lw, mirow, nirow;  // logs[s], matchIndex[s][*], nextIndex[s][*] of the successor
 };
 
+template <int N, int V, int MR>
+__device__ __forceinline__ void succ_adds(const Succ<N, V, MR> &o, uint32_t *a01, uint32_t *a23) {
+    uint32_t a[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < Spec<N, V, MR>::NADD; k++) a[k] = o.add[k];
+    *a01 = a[0] | (a[1] << 16);
+    *a23 = a[2] | (a[3] << 16);
+}
+
 // ---- log helpers (logs[i][x], tla:97, 1-based) ---------------------------------------
 template <int N, int V>
 __device__ __forceinline__ uint32_t log_word(const uint32_t *c, int i) {
@@ -149,11 +158,63 @@ __device__ __forceinline__ int inv_lhace(const uint32_t *c) {  // LeaderHasAllCo
     return 0;
 }
 
+// The message set of the state an invariant is checked on: msgs only grow (SendMsg, tla:77-78),
+// so a successor's set is its parent's sorted id list plus the ids its action added.
+struct MsgView {
+    const uint16_t *ids;  // parent's ids in HBM (record word CW on)
+    uint32_t nm;
+    uint32_t add0, add1;  // added ids, two u16 each (saux layout)
+    uint32_t nadd;
+    const uint32_t *info; // message info word by id
+};
+
+__device__ __forceinline__ uint32_t mv_id(const MsgView &mv, uint32_t k) {
+    if (k < mv.nm) return mv.ids[k];
+    k -= mv.nm;
+    const uint32_t w = k < 2 ? mv.add0 : mv.add1;
+    return (k & 1u) ? (w >> 16) : (w & 0xFFFFu);
+}
+
+// NoAllCommit tla:451-481.  The state conjuncts come first in the formula, so the message scans
+// (three \E m \in msgs, each short-circuiting on type before prevLogIndex/succ: no evaluation
+// error is possible) run only for a (s1, s2, s3) that passes them.
 template <int N, int V>
-__device__ __forceinline__ int inv_eval(const uint32_t *c, int id) {
+__device__ __noinline__ int inv_nac(const uint32_t *c, const MsgView &mv) {
+    using Lo = Layout<N, V>;
+    for (int s1 = 0; s1 < N; s1++) {
+        if (nib(c[Lo::W_ROLE], s1) != LEA || nib(c[Lo::W_CI], s1) != 2) continue;
+        for (int s2 = 0; s2 < N; s2++) {
+            if (s2 == s1 || nib(c[Lo::W_ROLE], s2) != FOL || nib(c[Lo::W_CI], s2) != 2 ||
+                nib(c[Lo::W_MI + s1], s2) != 2)
+                continue;
+            for (int s3 = 0; s3 < N; s3++) {
+                if (s3 == s2 || nib(c[Lo::W_ROLE], s3) != FOL) continue;
+                const uint32_t t3 = nib(c[Lo::W_CT], s3);
+                if (nib(c[Lo::W_CT], s1) != t3 || nib(c[Lo::W_CI], s3) != 1 || nib(c[Lo::W_MI + s1], s3) != 2)
+                    continue;
+                bool c1 = false, c2 = false, c3 = false;
+                for (uint32_t k = 0; k < mv.nm + mv.nadd; k++) {
+                    const uint32_t m = mv.info[mv_id(mv, k)];
+                    const uint32_t ty = mi_type(m), sr = mi_src(m), ds = mi_dst(m);
+                    if (ds == (uint32_t)s3 && sr == (uint32_t)s1 && mi_term(m) == t3 && ty == AREQ && mi_x1(m) == 1) c1 = true;
+                    if (ds == (uint32_t)s1 && sr == (uint32_t)s3 && mi_term(m) == t3 && ty == ARESP && mi_x1(m) == 1 &&
+                        mi_x2(m) == 1)
+                        c2 = true;
+                    if (ds == (uint32_t)s3 && sr == (uint32_t)s1 && ty == AREQ && mi_x1(m) == 2) c3 = true;
+                }
+                if (c1 && c2 && c3) return 1;
+            }
+        }
+    }
+    return 0;
+}
+
+template <int N, int V>
+__device__ __forceinline__ int inv_eval(const uint32_t *c, int id, const MsgView &mv) {
     using Lo = Layout<N, V>;
     switch (id) {
     case 0: return inv_lhace<N, V>(c);
+    case 5: return inv_nac<N, V>(c, mv);
     case 1: {  // NoSplitVote tla:444-448
 #pragma unroll
         for (int a = 0; a < N; a++)
@@ -193,10 +254,10 @@ __device__ __forceinline__ int inv_eval(const uint32_t *c, int id) {
 
 // all selected invariants in bit order; returns 1 ok, 0 violated, -1 eval error; *which = bit
 template <int N, int V>
-__device__ __forceinline__ int check_invs(const uint32_t *c, uint32_t mask, int *which) {
+__device__ __forceinline__ int check_invs(const uint32_t *c, uint32_t mask, int *which, const MsgView &mv) {
     for (int i = 0; i < 7; i++) {
         if (!(mask & (1u << i))) continue;
-        int r = inv_eval<N, V>(c, i);
+        int r = inv_eval<N, V>(c, i, mv);
         if (r != 1) { *which = i; return r; }
     }
     return 1;
@@ -975,7 +1036,9 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
                             side[3] = 0;
                         }
                         int which = 0;
-                        const int iv = check_invs<N, V>(cand[r].c, P.inv_mask, &which);
+                        MsgView mv{reinterpret_cast<const uint16_t *>(rec + S::CW), W.nm, 0u, 0u, cand[r].nadd, P.t.info};
+                        succ_adds(cand[r], &mv.add0, &mv.add1);
+                        const int iv = check_invs<N, V>(cand[r].c, P.inv_mask, &which, mv);
                         if (iv != 1) {
                             const unsigned long long ek =
                                 ((((unsigned long long)p << 16) | cand[r].key) << 8) | (unsigned long long)which;
@@ -992,7 +1055,9 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
                         P.par[gid] = P.gid_parent_base + p;
                         P.pslot[gid] = (uint16_t)cand[r].key;
                         int which = 0;
-                        const int iv = check_invs<N, V>(cand[r].c, P.inv_mask, &which);
+                        MsgView mv{reinterpret_cast<const uint16_t *>(rec + S::CW), W.nm, 0u, 0u, cand[r].nadd, P.t.info};
+                        succ_adds(cand[r], &mv.add0, &mv.add1);
+                        const int iv = check_invs<N, V>(cand[r].c, P.inv_mask, &which, mv);
                         if (iv != 1) {
                             const unsigned long long ek =
                                 ((((unsigned long long)p << 16) | cand[r].key) << 8) | (unsigned long long)which;
@@ -1042,7 +1107,9 @@ __global__ __launch_bounds__(64) void k_inv_states(KParams P, uint64_t n, int32_
     uint32_t c[Lo::NW];
 #pragma unroll
     for (int w = 0; w < Lo::NW; w++) c[w] = rec[w];
-    for (int b = 0; b < 7; b++) out[i * 7 + b] = inv_eval<N, V>(c, b);
+    const MsgView mv{reinterpret_cast<const uint16_t *>(rec + S::CW), (c[Lo::W_MISC] >> 16) & 0xFFu, 0u, 0u, 0u,
+                     P.t.info};
+    for (int b = 0; b < 7; b++) out[i * 7 + b] = inv_eval<N, V>(c, b, mv);
 }
 
 // ---- fused level: winner counts, commit --------------------------------------------------------
@@ -1308,7 +1375,8 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
                 P.par[gid] = P.gid_parent_base + p;
                 P.pslot[gid] = (uint16_t)key;
                 int which = 0;
-                const int iv = check_invs<N, V>(c, P.inv_mask, &which);
+                const MsgView mv{rid, nm, ax.y, ax.z, ax.x >> 16, P.t.info};
+                const int iv = check_invs<N, V>(c, P.inv_mask, &which, mv);
                 if (iv != 1) {
                     const unsigned long long ek = ((((unsigned long long)p << 16) | key) << 8) | (unsigned long long)which;
                     atomicMin(&P.err[iv == 0 ? ERR_INV : ERR_EVAL], ek);
