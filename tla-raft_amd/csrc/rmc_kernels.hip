@@ -801,6 +801,8 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
     __shared__ uint32_t sS[MAXS];
     __shared__ uint32_t sAinf[(MR + 1) * 64 * S::NADD];  // info words of the messages each candidate adds
     if (MODE == M_FUSED && !level_args(P)) return;
+    // device-loop grids are sized on a bound of the level: blocks past it leave before the LDS setup
+    if (MODE == M_FUSED && P.p_begin + blockIdx.x >= P.p_end) return;
     const int lane = threadIdx.x;
     if (SUMS) {
         for (int i = lane; i < P.t.np * N; i += 64) pimg[i] = P.t.perms[(i / N) * MAXN + (i % N)];
