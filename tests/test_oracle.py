@@ -140,3 +140,29 @@ def test_shuffled_order_gives_same_counts_small():
     a = R.bfs(cfg)
     b = R.bfs(cfg, order="shuffle", seed=7)
     assert (a.distinct, a.levels) == (b.distinct, b.levels)
+
+
+def test_no_all_commit_c_and_python_agree(corc):
+    """NoAllCommit (tla:451-481) reads msgs: both restatements agree on a state that satisfies
+    it and on each variant that drops or alters one of its three messages."""
+    import raftmc
+    lib = ctypes.CDLL(ORC_SO)
+    lib.orc_inv.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
+    cfg = R.Config(n=3, V=1, max_election=2, max_restart=3)
+    e = (1, 0)
+    req1 = R.append_req(0, 2, 1, 1, 0, (e,), 1)
+    resp1 = R.append_resp(2, 0, 1, 1, True)
+    req2 = R.append_req(0, 2, 1, 2, 1, (), 2)
+    got = []
+    for msgs in ([req1, resp1, req2], [resp1, req2], [req1, req2], [req1, resp1],
+                 [req1, R.append_resp(2, 0, 1, 1, False), req2], [req1, resp1, R.append_req(0, 1, 1, 2, 1, (), 2)]):
+        st = R.State(votedFor=(0, 0, 0), currentTerm=(1, 1, 1), logs=(((0, -1), e),) * 3,
+                     matchIndex=((2, 2, 2), (1, 1, 1), (1, 1, 1)), nextIndex=((3, 3, 3), (2, 2, 2), (2, 2, 2)),
+                     commitIndex=(2, 2, 1), msgs=frozenset(msgs), role=(R.LEADER, R.FOLLOWER, R.FOLLOWER),
+                     electionCount=1, restartCount=0, pendingResponse=((False,) * 3,) * 3, valSent=(0,))
+        u = raftmc.state_to_unpacked(R.state_to_json(st), 3, 1)
+        arr = (ctypes.c_int32 * len(u))(*u)
+        exp = R.INV_FUNCS["NoAllCommit"](cfg, st)
+        assert lib.orc_inv(3, 1, arr, 5) == int(exp), msgs
+        got.append(exp)
+    assert got == [True, False, False, False, False, False]
