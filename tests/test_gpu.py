@@ -22,6 +22,7 @@ def load(name):
 
 
 LEVELS = load("levels.json")
+LEVELS_BIG = load("levels_big.json") if os.path.exists(os.path.join(GOLDEN, "levels_big.json")) else {}
 SAMPLES = load("successors.json")
 TRACES = load("traces.json")
 
@@ -167,6 +168,15 @@ def check_levels(g, res):
 @pytest.mark.parametrize("name", sorted(LEVELS))
 def test_bfs_matches_golden_levels(name):
     g = LEVELS[name]
+    mc, res = run_cfg(g)
+    check_levels(g, res)
+    mc.close()
+
+
+@pytest.mark.parametrize("name", sorted(LEVELS_BIG))
+def test_bfs_matches_golden_levels_at_scale(name):
+    """bench.py's at-scale workload (10^7 states) against the C oracle's full BFS, level by level."""
+    g = LEVELS_BIG[name]
     mc, res = run_cfg(g)
     check_levels(g, res)
     mc.close()

@@ -18,7 +18,8 @@ cat gpurun_out/bench.json
 if [ -n "$PROFILE" ]; then
   step rocprof
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o bench -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-probe-peak --no-scale > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
-  find gpurun_out/prof -name "*stats*" | head
+  find gpurun_out/prof -name "*stats*"
+  python tools/prof_levels.py gpurun_out/prof/bench_kernel_trace.csv > gpurun_out/prof_levels.txt && cat gpurun_out/prof_levels.txt
 fi
 if [ -n "$EXPLORE" ]; then
   step explore
