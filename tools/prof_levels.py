@@ -3,7 +3,7 @@
 The device-driven loop enqueues levels in groups, so each exhaustion ends with a few no-op
 launches (the loop has stopped; every block returns at once).  bench.py's HIP-event figure
 averages only launches that expanded a level; this script gives rocprof's average over the
-same set: runs are split at host gaps, and the first `depth` launches of each kernel per run
+same set: runs are split at Init's fingerprint launch, and the first `depth` launches of each kernel per run
 are the real levels.
 
 usage: python tools/prof_levels.py gpurun_out/prof/bench_kernel_trace.csv [depth=37]
@@ -13,17 +13,16 @@ import sys
 from collections import defaultdict
 
 
-def main(path, depth=37, gap_ns=30000):
+def main(path, depth=37):
     rows = [r for r in csv.DictReader(open(path)) if "rmc::k_" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    runs, cur, last_end = [], [], None
+    # every exhaustion starts by fingerprinting Init (k_fp_states): that launch splits the runs
+    runs, cur = [], []
     for r in rows:
-        s = int(r["Start_Timestamp"])
-        if last_end is not None and s - last_end > gap_ns and "k_expand" in r["Kernel_Name"]:
+        if "k_fp_states" in r["Kernel_Name"] and cur:
             runs.append(cur)
             cur = []
         cur.append(r)
-        last_end = int(r["End_Timestamp"])
     runs.append(cur)
     tot, cnt, noop, nnoop = defaultdict(int), defaultdict(int), defaultdict(int), defaultdict(int)
     for run in runs:
