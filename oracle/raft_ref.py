@@ -71,6 +71,7 @@ ACTIONS = (
     "Restart",              # tla:409
 )
 A_BC, A_UT, A_RV, A_BL, A_CR, A_LAE, A_FAE, A_FRE, A_HAR, A_LCC, A_RS = range(11)
+A_FAPP = 11  # FollowerAppendEntry (tla:323), in Next only in the tla:425 variant
 
 INVARIANTS = ("Inv", "LeaderHasAllCommittedEntries", "NoSplitVote", "RaftCanCommt",
               "FollowerCanCommit", "CommitAll", "NoAllCommit", "ExistLeaderAndCandidate")
@@ -176,6 +177,7 @@ class Config:
     invariants: Tuple[str, ...] = ("Inv",)   # cfg:33-34
     check_deadlock: bool = False             # myrun.sh passes -deadlock (run:3)
     seeded: bool = False       # RaftSeeded: Median threshold Cardinality(Servers)
+    follower_append_entry: bool = False  # variant: tla:425's `\/ FollowerAppendEntry(s)` uncommented
     symmetry: bool = True      # SYMMETRY symmServers (cfg:24)
     view: bool = True          # VIEW view (cfg:26)
 
@@ -408,6 +410,52 @@ def follower_accept_entry(cfg, st: State, s, msgs_sorted):
             pendingResponse=st.pendingResponse, valSent=st.valSent)
 
 
+# how often FollowerAppendEntry reached its closing UNCHANGED (tla:371): the variant test uses it
+# to show the check is exercised, not vacuous
+FAPP_STATS = {"reached_unchanged": 0, "enabled": 0}
+
+
+def follower_append_entry(cfg, st: State, s, msgs_sorted):
+    """FollowerAppendEntry(s) (tla:323-371), commented out of Next at tla:425.
+
+    Restated as TLC evaluates the conjunction left to right: each IF/ELSE branch assigns
+    commitIndex' (IF only), logs' and msgs' (SendMsg, tla:77-78), and the action's last
+    top-level conjunct, tla:371's UNCHANGED << votedFor, currentTerm, msgs, matchIndex,
+    nextIndex, commitIndex, logs, ... >>, then *tests* msgs' = msgs, commitIndex' =
+    commitIndex and logs' = logs.  The ELSE branch requires resp \notin msgs (so msgs'
+    differs); the IF branch requires resp \notin msgs or a larger commitIndex (so msgs' or
+    commitIndex' differs): the action is never enabled, and the variant's state graph is
+    Raft.tla's."""
+    if st.role[s] != FOLLOWER:
+        return
+    for w, m in enumerate(msgs_sorted):
+        if mdst(m) != s or mterm(m) != st.currentTerm[s] or mtype(m) != "AppendReq":
+            continue
+        f = mfields(m)
+        log, ci = st.logs[s], st.commitIndex[s]
+        if log_match(st, s, f):
+            ent = m[2]
+            resp = append_resp(s, f["src"], f["term"], f["prevLogIndex"] + len(ent), True)
+            new_log = log[:f["prevLogIndex"]] + ent
+            new_ci = max(ci, min(f["leaderCommit"], len(new_log)))
+            if not (resp not in st.msgs or new_ci > ci):
+                continue
+            append_new = len(new_log) > len(log)
+            truncated = len(new_log) <= len(log) and new_log != log[:len(new_log)]
+            logs2, ci2 = (new_log if (append_new or truncated) else log), new_ci
+        else:
+            resp = append_resp(s, f["src"], f["term"], f["prevLogIndex"] - 1, False)
+            if resp in st.msgs:
+                continue
+            logs2, ci2 = log, ci
+        msgs2 = st.msgs | {resp}
+        FAPP_STATS["reached_unchanged"] += 1
+        if msgs2 != st.msgs or ci2 != ci or logs2 != log:  # tla:371
+            continue
+        FAPP_STATS["enabled"] += 1
+        yield w, st
+
+
 def follower_reject_entry(cfg, st: State, s, msgs_sorted):
     """FollowerRejectEntry(s) (tla:302-321)."""
     if st.role[s] != FOLLOWER:
@@ -511,6 +559,8 @@ def successor_batches(cfg: Config, st: State):
             (A_BL, lambda: become_leader(cfg, st, s)),
             (A_CR, lambda: client_req(cfg, st, s)),
             (A_LAE, lambda: leader_append_entry(cfg, st, s)),
+            # variant only (tla:425); never enabled, so its key index (A_FAPP) never appears
+            (A_FAPP, lambda: follower_append_entry(cfg, st, s, msgs_sorted)),
             (A_FAE, lambda: follower_accept_entry(cfg, st, s, msgs_sorted)),
             (A_FRE, lambda: follower_reject_entry(cfg, st, s, msgs_sorted)),
             (A_HAR, lambda: handle_append_resp(cfg, st, s, msgs_sorted)),
@@ -518,6 +568,8 @@ def successor_batches(cfg: Config, st: State):
             (A_RS, lambda: restart(cfg, st, s)),
         )
         for a, mk in gens:
+            if a == A_FAPP and not cfg.follower_append_entry:
+                continue
             yield s, a, list(mk())
 
 

@@ -22,7 +22,7 @@ def main():
     if len(sys.argv) > 1:
         a = list(map(int, sys.argv[1:]))
         cfgs = [tuple(a[i:i + 4]) for i in range(0, len(a), 4)]
-    path = os.path.join(HERE, "levels_big.json")
+    path = os.environ.get("GOLDEN_BIG_OUT", os.path.join(HERE, "levels_big.json"))
     out = json.load(open(path)) if os.path.exists(path) else {}
     for (n, V, E, Rr) in cfgs:
         t = time.time()

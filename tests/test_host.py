@@ -94,6 +94,9 @@ def test_spec_identification():
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import make_seeded_spec
     assert raftmc.parse_config(cfg_text(), make_seeded_spec.seeded(tla)).spec_variant == raftmc.SPEC_SEEDED
+    import make_variant_spec  # Next with FollowerAppendEntry (tla:425): never enabled, Raft.tla's model
+    assert raftmc.parse_config(cfg_text(), make_variant_spec.follower_append_entry(tla)).spec_variant == \
+        raftmc.SPEC_RAFT
     with pytest.raises(raftmc.RmcError, match="not kikimo"):
         raftmc.parse_config(cfg_text(), tla.replace("MaxElection", "MaxElections"))
 

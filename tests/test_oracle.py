@@ -166,3 +166,17 @@ def test_no_all_commit_c_and_python_agree(corc):
         assert lib.orc_inv(3, 1, arr, 5) == int(exp), msgs
         got.append(exp)
     assert got == [True, False, False, False, False, False]
+
+
+@pytest.mark.parametrize("n,V,E,Rr", [(3, 1, 1, 3), (2, 1, 2, 3), (3, 2, 1, 2)])
+def test_follower_append_entry_variant_is_raft(n, V, E, Rr):
+    """Uncommenting `\\/ FollowerAppendEntry(s)` in Next (tla:425): restated as TLC evaluates
+    it, the action's closing UNCHANGED (tla:371) tests msgs' = msgs and commitIndex' =
+    commitIndex after its own SendMsg, so it is never enabled -- the variant explores exactly
+    Raft.tla's state graph.  The 371 check is reached (not vacuous) and never passes."""
+    base = R.bfs(R.Config(n=n, V=V, max_election=E, max_restart=Rr))
+    R.FAPP_STATS.update(reached_unchanged=0, enabled=0)
+    var = R.bfs(R.Config(n=n, V=V, max_election=E, max_restart=Rr, follower_append_entry=True))
+    assert R.FAPP_STATS["reached_unchanged"] > 0 and R.FAPP_STATS["enabled"] == 0
+    assert (var.verdict, var.generated, var.distinct, var.depth, var.levels, var.generated_per_level) == (
+        base.verdict, base.generated, base.distinct, base.depth, base.levels, base.generated_per_level)

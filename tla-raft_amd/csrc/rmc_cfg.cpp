@@ -17,6 +17,11 @@ namespace rmc {
 
 static const uint64_t FNV_RAFT = 0x0a385fb43445e617ULL;         // kikimo/tla-raft Raft.tla
 static const uint64_t FNV_RAFT_SEEDED = 0xc2b84ca613379636ULL;  // tools/make_seeded_spec.py output
+// Raft.tla with Next's `\/ FollowerAppendEntry(s)` uncommented (tla:425; tools/make_variant_spec.py).
+// The action is never enabled as TLC evaluates it (its closing UNCHANGED, tla:371, tests msgs' =
+// msgs after its own SendMsg; oracle/raft_ref.py:follower_append_entry), so this text runs the
+// Raft.tla model unchanged.
+static const uint64_t FNV_RAFT_FAPP = 0x1319b28a1b001651ULL;
 
 uint64_t fnv1a_spec(const std::string &text) {
     uint64_t h = 0xcbf29ce484222325ULL;
@@ -251,12 +256,12 @@ bool parse_model(const std::string &cfg_text, const char *tla_text, ParsedModel 
     }
     if (tla_text) {
         const uint64_t h = fnv1a_spec(tla_text);
-        if (h == FNV_RAFT) { pm->cfg.spec_variant = RMC_SPEC_RAFT; pm->module = "Raft"; }
+        if (h == FNV_RAFT || h == FNV_RAFT_FAPP) { pm->cfg.spec_variant = RMC_SPEC_RAFT; pm->module = "Raft"; }
         else if (h == FNV_RAFT_SEEDED) { pm->cfg.spec_variant = RMC_SPEC_SEEDED; pm->module = "RaftSeeded"; }
         else {
             char buf[64];
             snprintf(buf, sizeof buf, "%016llx", (unsigned long long)h);
-            err = std::string("the .tla file is not kikimo/tla-raft's Raft.tla nor its seeded variant (fnv1a64 ") +
+            err = std::string("the .tla file is not kikimo/tla-raft's Raft.tla nor one of its variants (fnv1a64 ") +
                   buf + "): only those specs are compiled into this checker";
             return false;
         }
