@@ -950,6 +950,8 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
             //     partial minima of a successor meet in LDS.  PB = 64 / total (at most |perms|)
             //     keeps all 64 lanes busy when a parent has few successors -- the common case.
             const uint32_t npu = (uint32_t)np;
+            constexpr bool TWO_PASS = N >= 4;
+            static_assert(!TWO_PASS || factorial(N) <= 128, "two-pass tie mask holds 128 permutations per lane");
             uint32_t PB = 1;
             if (total > 0 && total < 64) PB = min(64u / total, npu);
             const uint32_t SB = 64u / PB;  // successors per round
@@ -957,7 +959,66 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
             for (uint32_t b0 = 0; b0 < total; b0 += SB) {
                 const uint32_t l = b0 + li;
                 uint64_t m0 = ~0ull, m1 = ~0ull;
-                if (li < SB && l < total) {
+                if (TWO_PASS) {
+                    // n >= 4: family 1 first over every permutation of the block, remembering
+                    // which ones reach the lane's minimum; family 0 then only for the permutations
+                    // that reach the successor's minimum (one, or an automorphism group) -- the
+                    // same lexicographic minimum of (H1, H0) with about half the mixes
+                    const bool act = li < SB && l < total;
+                    uint32_t sv = 0;
+                    uint64_t u = 0, x0[N], x1[N], tm[2] = {0ull, 0ull};
+                    if (act) {
+                        sv = sS[l];
+                        u = sU[l];
+#pragma unroll
+                        for (int j = 0; j < N; j++) { x0[j] = sX[0][l * N + j]; x1[j] = sX[1][l * N + j]; }
+                        uint32_t it = 0;
+                        for (uint32_t pp = blk; pp < npu; pp += PB, it++) {
+                            uint32_t img[N];
+#pragma unroll
+                            for (int j = 0; j < N; j++) img[j] = pimg[pp * N + j];
+                            uint32_t imgs = img[0];
+#pragma unroll
+                            for (int j = 1; j < N; j++) imgs = ((uint32_t)j == sv) ? img[j] : imgs;
+                            uint64_t h1 = Tt[1][pp] - Rt[1][pp * N + sv] + mix64(u ^ sdS[1][imgs]);
+#pragma unroll
+                            for (int j = 0; j < N; j++) {
+                                if ((uint32_t)j == sv) continue;
+                                h1 += mix64(x1[j] ^ sdP[1][imgs * N + img[j]]);
+                            }
+                            if (h1 < m1) { m1 = h1; tm[0] = 0ull; tm[1] = 0ull; }
+                            if (h1 == m1) tm[it >> 6] |= 1ull << (it & 63u);
+                        }
+                    }
+                    sPart[lane] = make_ulonglong2(0ull, m1);
+                    __syncthreads();
+                    uint64_t M1 = ~0ull;
+                    if (act)
+                        for (uint32_t k = 0; k < PB; k++) M1 = min(M1, (uint64_t)sPart[li * PB + k].y);
+                    __syncthreads();
+                    if (act && m1 == M1) {
+#pragma unroll
+                        for (int w = 0; w < 2; w++) {
+                            for (uint64_t bits = tm[w]; bits; bits &= bits - 1) {
+                                const uint32_t it = (uint32_t)(w * 64 + __ffsll((unsigned long long)bits) - 1);
+                                const uint32_t pp = blk + it * PB;
+                                uint32_t img[N];
+#pragma unroll
+                                for (int j = 0; j < N; j++) img[j] = pimg[pp * N + j];
+                                uint32_t imgs = img[0];
+#pragma unroll
+                                for (int j = 1; j < N; j++) imgs = ((uint32_t)j == sv) ? img[j] : imgs;
+                                uint64_t h0 = Tt[0][pp] - Rt[0][pp * N + sv] + mix64(u ^ sdS[0][imgs]);
+#pragma unroll
+                                for (int j = 0; j < N; j++) {
+                                    if ((uint32_t)j == sv) continue;
+                                    h0 += mix64(x0[j] ^ sdP[0][imgs * N + img[j]]);
+                                }
+                                m0 = min(m0, h0);
+                            }
+                        }
+                    }
+                } else if (li < SB && l < total) {
                     const uint32_t sv = sS[l];
                     const uint64_t u = sU[l];
                     uint64_t x0[N], x1[N];
