@@ -123,7 +123,8 @@ int rmc_comm_unique_id(void *out128);
 
 /* Parse Raft.cfg text (replaces TLC's ModelConfig for the subset Raft.cfg uses,
  * Raft.cfg:1-34) and validate Raft.tla text by content (replaces SANY; only
- * Raft.tla and the documented RaftSeeded variant are compiled in).  tla_text
+ * Raft.tla, the documented RaftSeeded variant and Raft.tla with FollowerAppendEntry
+ * uncommented in Next -- never enabled, so RMC_SPEC_RAFT -- are recognised).  tla_text
  * may be NULL to skip the spec check (then spec_variant is left unchanged). */
 int rmc_parse_config(const char *cfg_text, const char *tla_text, rmc_config *out, char *err, size_t err_cap);
 
