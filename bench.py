@@ -268,7 +268,16 @@ def at_scale(device, S, CWB, workload="n3v2e2"):
     G = sum(ls.generated for ls in timed.levels)
     N = sum(ls.new_states for ls in timed.levels)
     gbs = alg_bytes("expand_hash", F, G, N, S, CWB) / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    # the C oracle's full BFS of the same configuration (tests/golden/make_golden_big.py): data only
+    gold = {}
+    gpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "levels_big.json")
+    if os.path.exists(gpath):
+        with open(gpath) as f:
+            gold = json.load(f).get(f"n{w['n']}_v{w['V']}_e{w['E']}_r{w['R']}", {})
+    match = (res.distinct, res.generated, res.depth) == (gold.get("distinct"), gold.get("generated"),
+                                                         gold.get("depth")) if gold else None
     return {"workload": w["desc"], "distinct_states": res.distinct, "states_generated": res.generated,
+            "matches_c_oracle_golden": match,
             "depth": res.depth, "seconds": round(dt, 4), "distinct_per_s": round(res.distinct / dt, 1),
             "generated_per_s": round(res.generated / dt, 1),
             "expand_kernel_ms": round(ms, 3), "expand_alg_GBps": round(gbs, 1),
