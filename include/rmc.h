@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RMC_ABI_VERSION 2
+#define RMC_ABI_VERSION 3
 
 /* ---- return codes ---------------------------------------------------------- */
 #define RMC_OK 0
@@ -67,7 +67,7 @@ typedef struct rmc_config {
     int32_t n_vals;         /* |Vals|      Raft.cfg:21, 0..3 */
     int32_t max_election;   /* MaxElection Raft.cfg:4,  0..7 */
     int32_t max_restart;    /* MaxRestart  Raft.cfg:3,  0..15 */
-    uint32_t invariants;    /* RMC_INV_* bits, checked in bit order */
+    uint32_t invariants;    /* RMC_INV_* bits (order: invariant_order) */
     int32_t check_deadlock; /* 0 = TLC -deadlock (myrun.sh:3) */
     int32_t spec_variant;   /* RMC_SPEC_* */
     int32_t device;         /* HIP device ordinal (-1 = current) */
@@ -87,6 +87,17 @@ typedef struct rmc_config {
                                   expanded whole on every shard (replicated, no exchange, TLC order); the run
                                   switches to fingerprint-owner sharding at the first level that reaches it
                                   and stays sharded (0 = auto: 2^20; 1 = sharded from Init's level) */
+    /* ---- ABI 3 ---- */
+    uint32_t invariant_order;  /* the INVARIANTs in cfg order (Raft.cfg:33-34; TLC checks them in that order):
+                                  invariant bit index + 1 per 4-bit nibble, first in the low nibble;
+                                  0 = the bits of `invariants` in bit order */
+    uint32_t compact_log2;     /* seen set: 16-B slots {fp} while the table has at most 2^compact_log2 slots,
+                                  then one migration to 8-B slots sized from seen_mem_bytes and never grown
+                                  (0 = auto: 27) */
+    uint64_t seen_mem_bytes;   /* device bytes for the compact seen set (0 = auto: half of the free memory
+                                  at migration, per shard) */
+    uint64_t frontier_mem_bytes; /* device bytes for the frontier ring once the seen set is compact (0 = auto:
+                                  70 % of the free memory left then, per shard) */
 } rmc_config;
 
 /* Statistics of one BFS level (what TLC's progress line reports). */
@@ -102,6 +113,7 @@ typedef struct rmc_level_stats {
     double seconds;           /* wall time of this level */
     double kernel_ms[6];      /* expand-count, expand-hash, dedup, materialize, exchange, other */
     uint64_t kernel_launches[6];
+    uint64_t new_bytes;       /* ABI 3: bytes of the new states' frontier records (packed core + message ids) */
 } rmc_level_stats;
 
 /* Final result of a run: TLC's closing lines. */
@@ -112,6 +124,12 @@ typedef struct rmc_result {
     int32_t violated;         /* index (bit) of the violated invariant, -1 if none */
     uint32_t trace_len;
     double seconds;
+    /* ABI 3: memory of the run (this rank) */
+    uint64_t seen_slots;          /* seen-set capacity in slots */
+    int32_t seen_slot_bytes;      /* 16 (full fingerprints) or 8 (compact) */
+    int32_t pad_;
+    uint64_t frontier_ring_bytes; /* device bytes of the frontier ring */
+    uint64_t frontier_peak_bytes; /* largest live frontier (current + next level records) */
 } rmc_result;
 
 int rmc_abi_version(void);

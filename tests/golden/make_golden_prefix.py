@@ -1,0 +1,70 @@
+"""Prefix golden levels from the C oracle (oracle/raft_oracle.c, TLC -workers 1 BFS).
+
+For configurations whose full state space the single-threaded oracle cannot exhaust in
+reasonable time (Raft.cfg as shipped: n3 V2 E3 R3; the 5-server config n5 V1 E3 R3), run the
+oracle until `max_states` distinct states and keep only the levels it completed:
+
+  levels[k]        distinct states at BFS level k+1, for every level fully discovered
+  gen_per_level[k] successors generated while expanding level k+1, for every level fully
+                   expanded (one fewer than `levels`)
+
+The GPU test (tests/test_gpu.py::test_prefix_levels_match_c_oracle) runs the same configuration
+level by level and compares those prefixes exactly.
+
+usage: python tests/golden/make_golden_prefix.py MAX_STATES n V E R [n V E R ...]
+writes tests/golden/levels_prefix.json (merged with what is there)
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from make_golden import c_oracle  # noqa: E402
+
+V_LIMIT_NAMES = {0: "ok", 1: "invariant", 2: "assert", 3: "eval_error", 4: "deadlock"}
+
+
+def run_prefix(n, V, E, Rr, max_states):
+    lib = c_oracle()
+    h = lib.orc_create(n, V, E, Rr, 0, 0, 1, 0)
+    t = time.time()
+    v = lib.orc_run(h, max_states)
+    dt = time.time() - t
+    cap = 256
+    d = (ctypes.c_uint64 * cap)()
+    g = (ctypes.c_uint64 * cap)()
+    depth = lib.orc_levels(h, d, g, cap)
+    distinct = lib.orc_distinct(h)
+    max_nm = lib.orc_max_msgs(h)
+    lib.orc_destroy(h)
+    if v == 0:  # exhausted: every level is complete
+        levels, gens = list(d[:depth]), list(g[:depth])
+    else:
+        # stopped while expanding level `depth - 1` (its successors land in level `depth`):
+        # levels 1..depth-1 are fully discovered, levels 1..depth-2 fully expanded
+        levels, gens = list(d[:depth - 1]), list(g[:depth - 2])
+    return {"n": n, "V": V, "E": E, "R": Rr, "max_states": max_states, "stopped_at_distinct": distinct,
+            "exhausted": v == 0, "levels": levels, "gen_per_level": gens, "max_msgs_seen": max_nm,
+            "oracle_seconds": round(dt, 1), "source": "c", "invariants": ["Inv"], "check_deadlock": False}
+
+
+def main():
+    max_states = int(sys.argv[1])
+    a = list(map(int, sys.argv[2:]))
+    cfgs = [tuple(a[i:i + 4]) for i in range(0, len(a), 4)]
+    path = os.environ.get("GOLDEN_PREFIX_OUT", os.path.join(HERE, "levels_prefix.json"))
+    for (n, V, E, Rr) in cfgs:
+        r = run_prefix(n, V, E, Rr, max_states)
+        out = json.load(open(path)) if os.path.exists(path) else {}
+        out[f"n{n}_v{V}_e{E}_r{Rr}"] = r
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        print(n, V, E, Rr, "levels", len(r["levels"]), "states", sum(r["levels"]), r["oracle_seconds"], "s",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -198,8 +198,14 @@ bool parse_model(const std::string &cfg_text, const char *tla_text, ParsedModel 
             for (const auto &p : kInvNames)
                 if (t.s == p.first) bit = p.second;
             if (!bit) return fail(t, "invariant " + t.s + " is not compiled");
+            if (!(pm->cfg.invariants & bit)) {
+                // TLC checks the invariants in the order the cfg lists them: id + 1 per nibble
+                int id = 0;
+                while (!((bit >> id) & 1u)) id++;
+                pm->cfg.invariant_order |= (uint32_t)(id + 1) << (4 * pm->invariant_names.size());
+                pm->invariant_names.push_back(t.s);
+            }
             pm->cfg.invariants |= bit;
-            pm->invariant_names.push_back(t.s);
         } else {
             return fail(t, section.empty() ? "text before the first section" : section + " is not supported");
         }

@@ -1,15 +1,21 @@
 // rmc_engine.hip -- host orchestration of the level-synchronous GPU BFS behind the C-ABI.
 //
 // Replaces TLC's ModelChecker / Worker loop (run by myrun.sh:3) for Raft.tla:
-//   * level L's states live in HBM as packed records (rmc_spec.h), in TLC -workers 1
-//     FIFO order;
-//   * a level is expanded in chunks of parents: COUNT -> scan -> HASH -> dedup
-//     (seen set + first-in-TLC-order election) -> scan -> MATERIALIZE;
-//   * new states are appended to the next level in the order TLC would have
-//     enqueued them, so discovery order (and therefore which concrete state
-//     represents a VIEW class) matches TLC with one worker;
-//   * the first error in TLC order (invariant / eval error / Assert / deadlock)
-//     stops the search with TLC's counters at that point and a replayable trace.
+//   * level L's states live in HBM as variable-length packed records (rmc_spec.h Codec: packed
+//     core + sorted message ids) in a ring of 32-bit words, in TLC -workers 1 FIFO order, with a
+//     level-relative word offset per state; level L+1 is written right behind level L, and the
+//     space of the chunks of level L already expanded is reused once the ring is at its budget;
+//   * a level is expanded in chunks of parents by three fused launches (expand + fingerprint +
+//     seen-set probe + election + staging, winner count, commit);
+//   * new states are appended to the next level in the order TLC would have enqueued them, so
+//     discovery order (and therefore which concrete state represents a VIEW class, SURVEY
+//     App. D.2) matches TLC with one worker;
+//   * the seen set holds 128-bit fingerprints while small, then 64-bit words in a table sized
+//     once from the memory budget (the probe run from the home slot carries the rest);
+//   * every state's parent reference + slot key (the trace, TLC's states/ metadir) goes to host
+//     memory chunk by chunk;
+//   * the first error in TLC order (invariant / eval error / Assert / deadlock) stops the search
+//     with TLC's counters at that point and a replayable trace.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -18,8 +24,12 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
+
+#include <fcntl.h>
+#include <unistd.h>
 
 #include "rmc.h"
 #include "rmc_kernels.h"
@@ -115,8 +125,19 @@ T *dmalloc(size_t n) {
     void *p = nullptr;
     if (n == 0) n = 1;
     hipError_t e = hipMalloc(&p, n * sizeof(T));
-    if (e != hipSuccess)
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
         throw Fail(RMC_E_MEMORY, "hipMalloc(" + std::to_string(n * sizeof(T)) + " B): " + hipGetErrorString(e));
+    }
+    return (T *)p;
+}
+template <class T>
+T *dmalloc_try(size_t n) {  // nullptr instead of an exception
+    void *p = nullptr;
+    if (hipMalloc(&p, (n ? n : 1) * sizeof(T)) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
     return (T *)p;
 }
 template <class T>
@@ -131,6 +152,89 @@ uint64_t next_pow2(uint64_t x) {
     return p;
 }
 
+uint64_t free_device_bytes() {
+    size_t f = 0, t = 0;
+    if (hipMemGetInfo(&f, &t) != hipSuccess) return 0;
+    return f;
+}
+
+// Host array in pinned blocks (falls back to pageable blocks): the trace of every state the run
+// found, written by asynchronous device-to-host copies chunk by chunk, never reallocated.
+template <class T>
+struct HostArr {
+    static constexpr uint64_t B = 1ull << 22;
+    struct Blk {
+        T *p = nullptr;
+        bool pinned = false;
+    };
+    std::vector<Blk> blk;
+    uint64_t n = 0;
+    HostArr() = default;
+    HostArr(const HostArr &) = delete;
+    HostArr &operator=(const HostArr &) = delete;
+    HostArr(HostArr &&o) noexcept : blk(std::move(o.blk)), n(o.n) { o.blk.clear(); o.n = 0; }
+    HostArr &operator=(HostArr &&o) noexcept {
+        if (this != &o) { release(); blk = std::move(o.blk); n = o.n; o.blk.clear(); o.n = 0; }
+        return *this;
+    }
+    ~HostArr() { release(); }
+    void release() {
+        for (Blk &b : blk) {
+            if (b.pinned) (void)hipHostFree(b.p);
+            else delete[] b.p;
+        }
+        blk.clear();
+        n = 0;
+    }
+    void reserve_to(uint64_t m) {
+        while ((uint64_t)blk.size() * B < m) {
+            Blk b;
+            if (hipHostMalloc((void **)&b.p, B * sizeof(T), hipHostMallocDefault) == hipSuccess) {
+                b.pinned = true;
+            } else {
+                (void)hipGetLastError();
+                b.p = new T[B];
+            }
+            blk.push_back(b);
+        }
+    }
+    T get(uint64_t i) const { return blk[i / B].p[i % B]; }
+    void set(uint64_t i, T v) {
+        reserve_to(i + 1);
+        blk[i / B].p[i % B] = v;
+        n = std::max(n, i + 1);
+    }
+    // elements [at, at + cnt) from device memory, enqueued on `s` (the caller syncs before reading)
+    void from_device(const T *dev, uint64_t at, uint64_t cnt, hipStream_t s) {
+        reserve_to(at + cnt);
+        for (uint64_t i = 0; i < cnt;) {
+            const uint64_t g = at + i, k = std::min(cnt - i, B - g % B);
+            HIPCHK(hipMemcpyAsync(blk[g / B].p + g % B, dev + i, k * sizeof(T), hipMemcpyDeviceToHost, s));
+            i += k;
+        }
+        n = std::max(n, at + cnt);
+    }
+    void to_device(T *dev, uint64_t at, uint64_t cnt) const {
+        for (uint64_t i = 0; i < cnt;) {
+            const uint64_t g = at + i, k = std::min(cnt - i, B - g % B);
+            HIPCHK(hipMemcpy(dev + i, blk[g / B].p + g % B, k * sizeof(T), hipMemcpyHostToDevice));
+            i += k;
+        }
+    }
+    template <class F>
+    void for_range(uint64_t at, uint64_t cnt, F &&f) const {  // f(pointer, count) over contiguous pieces
+        for (uint64_t i = 0; i < cnt;) {
+            const uint64_t g = at + i, k = std::min(cnt - i, B - g % B);
+            f(blk[g / B].p + g % B, k);
+            i += k;
+        }
+    }
+    void copy_from(const HostArr &o, uint64_t at, uint64_t cnt) {
+        reserve_to(at + cnt);
+        for (uint64_t i = 0; i < cnt; i++) blk[(at + i) / B].p[(at + i) % B] = o.get(at + i);
+        n = std::max(n, at + cnt);
+    }
+};
 
 enum Phase { PH_COUNT = 0, PH_HASH = 1, PH_DEDUP = 2, PH_MAT = 3, PH_XCHG = 4, PH_OTHER = 5 };
 
@@ -147,16 +251,29 @@ struct TraceStep {
 // logic with device copies instead of RCCL (the multi-GPU parity tests use it).
 struct Shard {
     int id = 0;  // global shard index = owner id
-    // frontier: current and next level, packed records
-    uint32_t *cur = nullptr, *nxt = nullptr;
-    uint64_t cur_n = 0, cur_cap = 0, nxt_n = 0, nxt_cap = 0;
+    // frontier ring: record word k of level-local state p at R[wrap(cur_wbase + cur_off[p] + k)];
+    // the next level's records follow at nbase() (level-relative offsets in nxt_off)
+    uint32_t *R = nullptr;
+    uint64_t rcap = 0;
+    bool ring_fixed = false;            // sized from the budget: no further growth, consumed space reused
+    uint64_t cur_wbase = 0, cur_words = 0, nxt_words = 0, peak_words = 0;
+    uint64_t *cur_off = nullptr, *nxt_off = nullptr;
+    uint64_t cur_off_cap = 0, nxt_off_cap = 0;
+    uint64_t cur_n = 0, nxt_n = 0;
+    uint64_t nbase() const { return ring_wrap(cur_wbase + cur_words, rcap); }
     // seen-set shard
     ulonglong2 *T = nullptr;
+    unsigned long long *Tc = nullptr;
     uint64_t T_cap = 0, T_count = 0;
-    // trace: parent reference (shard << 48 | local gid) + slot key, per local gid
+    Seen seen() const { return Seen{Tc ? nullptr : T, Tc, T_cap - 1}; }
+    // trace: parent reference (shard << 48 | local gid) + slot key per local gid; the device
+    // buffers hold gids from tflushed on, the host arrays everything before
     uint64_t *par = nullptr;
     uint16_t *pslot = nullptr;
-    uint64_t trace_cap = 0;
+    uint64_t trace_cap = 0, tflushed = 0;
+    uint64_t tdev = 0;  // gid of device trace index 0 (set to tflushed when a kernel sequence starts)
+    HostArr<uint64_t> hpar;
+    HostArr<uint16_t> hslot;
     std::vector<uint64_t> level_start;  // local gid of the first state of each level
     // chunk buffers (source side)
     uint32_t *cnt = nullptr, *off = nullptr, *lslot = nullptr, *wflag = nullptr, *wpos = nullptr;
@@ -166,8 +283,9 @@ struct Shard {
     uint32_t epoch = 0;
     uint32_t lxy_epoch0 = 0;    // epoch of the last LXY clear (16-bit tags repeat after 65535 epochs)
     // fused single-shard level: sparse successor staging (slot q = chunk parent * maxsucc + rank)
-    uint4 *score = nullptr, *saux = nullptr;
-    uint32_t *wcnt = nullptr, *wacc = nullptr, *ctick = nullptr, *bw = nullptr, *bg = nullptr, *boff = nullptr, *tickets = nullptr;
+    uint4 *score = nullptr;
+    uint32_t *wcnt = nullptr, *wacc = nullptr, *pnm = nullptr, *wposw = nullptr, *ctick = nullptr;
+    uint32_t *bw = nullptr, *bg = nullptr, *boff = nullptr, *bww = nullptr, *boffw = nullptr, *tickets = nullptr;
     // device-driven level loop: control block, per-level records, and their pinned host copies
     LevelCtl *ctl = nullptr, *hctl = nullptr, *hsnap = nullptr;
     LevelRec *lrec = nullptr, *hlrec = nullptr;
@@ -179,7 +297,7 @@ struct Shard {
     unsigned long long *ocnt = nullptr;
     ulonglong2 *rfp = nullptr;
     uint32_t *rlslot = nullptr, *rflag = nullptr, *rpos = nullptr, *rcount = nullptr;
-    uint64_t rcap = 0;
+    uint64_t rcap_x = 0;
     uint32_t *sx = nullptr, *rx = nullptr;
     uint64_t sx_cap = 0, rx_cap = 0;
     uint64_t *pick_idx = nullptr;
@@ -188,7 +306,6 @@ struct Shard {
     uint32_t *flags = nullptr;
     // per-chunk host bookkeeping (sharded path)
     uint64_t p0 = 0, np = 0, G = 0;
-    std::vector<uint64_t> scnt, soff, rcnt, roff, swin, swoff, rwin, rwoff;
 };
 
 struct rmc_ctx {
@@ -197,7 +314,8 @@ struct rmc_ctx {
     Universe U;
     std::string err;
     hipStream_t stream = nullptr;
-    int N = 0, V = 0, RECW = 0;
+    int N = 0, V = 0, RECW = 0;  // RECW = the longest record (fixed-stride buffers)
+    uint32_t inv_order = 0;      // invariants in cfg order (check_invs)
     int W = 1, rank = 0;  // shards in the run, this process's first shard
     bool virt = false;    // all W shards live in this process
 #ifdef RMC_WITH_RCCL
@@ -211,6 +329,7 @@ struct rmc_ctx {
     uint8_t *d_perms = nullptr;
     uint64_t *d_seeds = nullptr;
     int np = 0;
+    uint64_t scheme_hash = 0;  // identifies the fingerprint scheme (seeds, message hashes): checkpoints
 
     std::vector<Shard> sh;
     uint64_t chunk_parents = 0, Gcap = 0, Lcap_max = 0;
@@ -253,61 +372,92 @@ struct rmc_ctx {
         P.seeded = cfg.spec_variant == RMC_SPEC_SEEDED;
         P.check_deadlock = cfg.check_deadlock;
         P.inv_mask = cfg.invariants;
+        P.inv_order = inv_order;
         P.t.info = d_info;
         P.t.nat2id = d_nat2id;
         P.t.gmsg = d_gmsg;
         P.t.perms = d_perms;
         P.t.seeds = d_seeds;
         P.t.np = np;
-        P.T = s.T;
-        P.Tmask = s.T_cap - 1;
+        P.seen = s.seen();
+        P.rcap = ~0ull;  // fixed-stride buffers unless a ring is set
         P.err = s.err;
         P.flags = s.flags;
         P.par = s.par;
         P.pslot = s.pslot;
+        P.trace_base = s.tdev;
         return P;
     }
 
+    // the current level in the shard's ring as the parents of a launch
+    void ring_params(const Shard &s, KParams &P) const {
+        P.front = s.R;
+        P.foff = s.cur_off;
+        P.fbase = s.cur_wbase;
+        P.rcap = s.rcap;
+        P.next = s.R;
+        P.noff = s.nxt_off;
+        P.nbase = s.nbase();
+    }
+
     // fused single-shard level: the chunk buffers every kernel of the level shares
-    KParams chunk_params(const Shard &s, const uint32_t *front, uint32_t *next) const {
+    KParams chunk_params(const Shard &s) const {
         KParams Q = base(s);
-        Q.front = front; Q.next = next;
-        Q.cnt = s.cnt; Q.fp = s.fp; Q.wpos = s.wpos; Q.wcnt = s.wcnt; Q.wacc = s.wacc;
-        Q.bw = s.bw; Q.bg = s.bg; Q.boff = s.boff; Q.tickets = s.tickets; Q.ctick = s.ctick; Q.sum = s.sum;
-        Q.score = s.score; Q.saux = s.saux; Q.lslot = s.lslot; Q.L = s.L; Q.LXY = s.LXY;
+        ring_params(s, Q);
+        Q.cnt = s.cnt; Q.fp = s.fp; Q.wpos = s.wpos; Q.wcnt = s.wcnt; Q.wacc = s.wacc; Q.pnm = s.pnm;
+        Q.wposw = s.wposw; Q.bw = s.bw; Q.bg = s.bg; Q.boff = s.boff; Q.bww = s.bww; Q.boffw = s.boffw;
+        Q.tickets = s.tickets; Q.ctick = s.ctick; Q.sum = s.sum;
+        Q.score = s.score; Q.lslot = s.lslot; Q.L = s.L; Q.LXY = s.LXY;
         return Q;
     }
 
     // ---- packing (unpacked int32 interchange <-> record) ------------------------------
+    // A fixed-stride record: packed core (ks.CCW words) + ids; RECW words.
     void pack(const int32_t *u, uint32_t *rec) const {
         const int n = N, Vv = V;
-        std::vector<uint32_t> w(RECW, 0);
+        std::vector<uint32_t> w(Layout<MAXN, MAXV>::NW + 8, 0);
         int k = 0;
         auto L_VF = 0, L_CT = 1, L_ROLE = 2, L_CI = 3, L_LL = 4, L_LOG = 5, L_MI = 5 + n, L_NI = 5 + 2 * n,
              L_PEND = 5 + 3 * n, L_MISC = 6 + 3 * n;
-        for (int i = 0; i < n; i++) w[L_VF] = setnib(w[L_VF], i, u[k + i] < 0 ? VF_NONE : (uint32_t)u[k + i]);
+        auto check = [](int v, int lo, int hi, const char *what) {
+            if (v < lo || v > hi) throw Fail(RMC_E_ARG, std::string("state field out of range: ") + what);
+        };
+        for (int i = 0; i < n; i++) {
+            check(u[k + i], -1, n - 1, "votedFor");
+            w[L_VF] = setnib(w[L_VF], i, u[k + i] < 0 ? VF_NONE : (uint32_t)u[k + i]);
+        }
         k += n;
-        for (int i = 0; i < n; i++) w[L_CT] = setnib(w[L_CT], i, u[k + i]);
+        for (int i = 0; i < n; i++) { check(u[k + i], 0, 7, "currentTerm"); w[L_CT] = setnib(w[L_CT], i, u[k + i]); }
         k += n;
-        for (int i = 0; i < n; i++) w[L_ROLE] = setnib(w[L_ROLE], i, u[k + i]);
+        for (int i = 0; i < n; i++) { check(u[k + i], 0, 2, "role"); w[L_ROLE] = setnib(w[L_ROLE], i, u[k + i]); }
         k += n;
-        for (int i = 0; i < n; i++) w[L_CI] = setnib(w[L_CI], i, u[k + i]);
+        for (int i = 0; i < n; i++) { check(u[k + i], 1, Vv + 1, "commitIndex"); w[L_CI] = setnib(w[L_CI], i, u[k + i]); }
         k += n;
         std::vector<int> ll(n);
-        for (int i = 0; i < n; i++) { ll[i] = u[k + i]; w[L_LL] = setnib(w[L_LL], i, u[k + i]); }
+        for (int i = 0; i < n; i++) {
+            check(u[k + i], 1, Vv + 1, "Len(logs)");
+            ll[i] = u[k + i];
+            w[L_LL] = setnib(w[L_LL], i, u[k + i]);
+        }
         k += n;
         for (int i = 0; i < n; i++)
             for (int x = 1; x <= Vv + 1; x++) {
                 const int t = u[k], v = u[k + 1];
                 k += 2;
-                if (x >= 2 && x <= ll[i]) w[L_LOG + i] |= (uint32_t)((t & 15) | ((v & 15) << 4)) << (8 * (x - 2));
+                if (x >= 2 && x <= ll[i]) {
+                    check(t, 0, 7, "log term");
+                    check(v, 0, Vv - 1, "log value");
+                    w[L_LOG + i] |= (uint32_t)((t & 15) | ((v & 15) << 4)) << (8 * (x - 2));
+                }
             }
         for (int i = 0; i < n; i++)
-            for (int j = 0; j < n; j++) w[L_MI + i] = setnib(w[L_MI + i], j, u[k++]);
+            for (int j = 0; j < n; j++) { check(u[k], 0, Vv + 1, "matchIndex"); w[L_MI + i] = setnib(w[L_MI + i], j, u[k++]); }
         for (int i = 0; i < n; i++)
-            for (int j = 0; j < n; j++) w[L_NI + i] = setnib(w[L_NI + i], j, u[k++]);
+            for (int j = 0; j < n; j++) { check(u[k], 0, Vv + 2, "nextIndex"); w[L_NI + i] = setnib(w[L_NI + i], j, u[k++]); }
         for (int i = 0; i < n; i++)
             for (int j = 0; j < n; j++) w[L_PEND] |= (u[k++] ? 1u : 0u) << (i * n + j);
+        check(u[k], 0, 7, "electionCount");
+        check(u[k + 1], 0, 15, "restartCount");
         uint32_t misc = (uint32_t)(u[k] & 15) | ((uint32_t)(u[k + 1] & 15) << 4);
         k += 2;
         for (int v = 0; v < Vv; v++) misc |= (u[k++] != -1 ? 1u : 0u) << (8 + v);
@@ -334,43 +484,46 @@ struct rmc_ctx {
         ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
         misc |= (uint32_t)ids.size() << 16;
         w[L_MISC] = misc;
-        std::memcpy(rec, w.data(), (size_t)ks.CW * 4);
-        uint16_t *rid = reinterpret_cast<uint16_t *>(rec + ks.CW);
-        for (int q = 0; q < ks.MCAP; q++) rid[q] = q < (int)ids.size() ? ids[q] : 0;
+        std::memset(rec, 0, (size_t)RECW * 4);
+        ks.encode(w.data(), rec);
+        uint16_t *rid = reinterpret_cast<uint16_t *>(rec + ks.CCW);
+        for (size_t q = 0; q < ids.size(); q++) rid[q] = ids[q];
     }
 
     std::vector<int32_t> unpack(const uint32_t *rec) const {
         const int n = N, Vv = V;
         const int L_VF = 0, L_CT = 1, L_ROLE = 2, L_CI = 3, L_LL = 4, L_LOG = 5, L_MI = 5 + n, L_NI = 5 + 2 * n,
                   L_PEND = 5 + 3 * n, L_MISC = 6 + 3 * n;
-        const uint32_t misc = rec[L_MISC];
+        std::vector<uint32_t> c(Layout<MAXN, MAXV>::NW + 8, 0);
+        ks.decode(rec, c.data());
+        const uint32_t misc = c[L_MISC];
         const int nm = (misc >> 16) & 0xFF;
         std::vector<int32_t> o;
         o.reserve(RMC_UNPACKED_INTS(n, Vv, nm));
-        for (int i = 0; i < n; i++) { uint32_t v = nib(rec[L_VF], i); o.push_back(v == VF_NONE ? -1 : (int)v); }
-        for (int i = 0; i < n; i++) o.push_back(nib(rec[L_CT], i));
-        for (int i = 0; i < n; i++) o.push_back(nib(rec[L_ROLE], i));
-        for (int i = 0; i < n; i++) o.push_back(nib(rec[L_CI], i));
-        for (int i = 0; i < n; i++) o.push_back(nib(rec[L_LL], i));
+        for (int i = 0; i < n; i++) { uint32_t v = nib(c[L_VF], i); o.push_back(v == VF_NONE ? -1 : (int)v); }
+        for (int i = 0; i < n; i++) o.push_back(nib(c[L_CT], i));
+        for (int i = 0; i < n; i++) o.push_back(nib(c[L_ROLE], i));
+        for (int i = 0; i < n; i++) o.push_back(nib(c[L_CI], i));
+        for (int i = 0; i < n; i++) o.push_back(nib(c[L_LL], i));
         for (int i = 0; i < n; i++)
             for (int x = 1; x <= Vv + 1; x++) {
                 if (x == 1) { o.push_back(0); o.push_back(-1); continue; }
-                if (x > (int)nib(rec[L_LL], i)) { o.push_back(0); o.push_back(0); continue; }
-                const uint32_t b = (rec[L_LOG + i] >> (8 * (x - 2))) & 0xFF;
+                if (x > (int)nib(c[L_LL], i)) { o.push_back(0); o.push_back(0); continue; }
+                const uint32_t b = (c[L_LOG + i] >> (8 * (x - 2))) & 0xFF;
                 o.push_back(b & 15);
                 o.push_back(b >> 4);
             }
         for (int i = 0; i < n; i++)
-            for (int j = 0; j < n; j++) o.push_back(nib(rec[L_MI + i], j));
+            for (int j = 0; j < n; j++) o.push_back(nib(c[L_MI + i], j));
         for (int i = 0; i < n; i++)
-            for (int j = 0; j < n; j++) o.push_back(nib(rec[L_NI + i], j));
+            for (int j = 0; j < n; j++) o.push_back(nib(c[L_NI + i], j));
         for (int i = 0; i < n; i++)
-            for (int j = 0; j < n; j++) o.push_back((rec[L_PEND] >> (i * n + j)) & 1);
+            for (int j = 0; j < n; j++) o.push_back((c[L_PEND] >> (i * n + j)) & 1);
         o.push_back(misc & 15);
         o.push_back((misc >> 4) & 15);
         for (int v = 0; v < Vv; v++) o.push_back(((misc >> (8 + v)) & 1) ? 0 : -1);
         o.push_back(nm);
-        const uint16_t *rid = reinterpret_cast<const uint16_t *>(rec + ks.CW);
+        const uint16_t *rid = reinterpret_cast<const uint16_t *>(rec + ks.CCW);
         for (int q = 0; q < nm; q++) {
             const uint32_t m = U.info[rid[q]];
             const int t = mi_type(m);
@@ -414,6 +567,11 @@ struct rmc_ctx {
         return rec;
     }
 
+    uint32_t record_words(const uint32_t *rec) const {
+        std::vector<uint32_t> c(Layout<MAXN, MAXV>::NW + 8, 0);
+        ks.decode(rec, c.data());
+        return (uint32_t)ks.CCW + ((((c[6 + 3 * N] >> 16) & 0xFFu) + 1u) >> 1);
+    }
 
     // ---- allocation -----------------------------------------------------------------
     void setup() {
@@ -422,6 +580,24 @@ struct rmc_ctx {
         if (cfg.max_election < 0 || cfg.max_election > 7) throw Fail(RMC_E_ARG, "max_election must be 0..7");
         if (cfg.max_restart < 0 || cfg.max_restart > 15) throw Fail(RMC_E_ARG, "max_restart must be 0..15");
         if (cfg.invariants & ~0x7Fu) throw Fail(RMC_E_ARG, "unknown invariant bits");
+        // invariant order: the cfg's, else bit order; every listed invariant must be selected
+        inv_order = 0;
+        if (cfg.invariant_order) {
+            uint32_t seen = 0;
+            int k = 0;
+            for (uint32_t o = cfg.invariant_order; o; o >>= 4, k++) {
+                const uint32_t id = (o & 15u) - 1u;
+                if ((o & 15u) == 0 || id >= 7 || !(cfg.invariants & (1u << id)) || (seen & (1u << id)) || k >= 7)
+                    throw Fail(RMC_E_ARG, "invariant_order does not list the selected invariants");
+                seen |= 1u << id;
+            }
+            if (seen != cfg.invariants) throw Fail(RMC_E_ARG, "invariant_order does not list every selected invariant");
+            inv_order = cfg.invariant_order;
+        } else {
+            int k = 0;
+            for (int b = 0; b < 7; b++)
+                if (cfg.invariants & (1u << b)) inv_order |= (uint32_t)(b + 1) << (4 * k++);
+        }
         const int ws = cfg.world_size > 1 ? cfg.world_size : 1;
         if (cfg.virtual_shards > 1 && ws > 1) throw Fail(RMC_E_ARG, "virtual_shards and world_size > 1 are exclusive");
         if (cfg.virtual_shards > 64 || ws > 64) throw Fail(RMC_E_ARG, "at most 64 shards");
@@ -435,7 +611,7 @@ struct rmc_ctx {
         if (!get_kernels(N, V, cap, &ks))
             throw Fail(RMC_E_ARG, "no compiled kernels for n_servers=" + std::to_string(N) + " n_vals=" +
                                       std::to_string(V) + " msg_cap=" + std::to_string(cap));
-        RECW = ks.RECW;
+        RECW = ks.RECW_MAX;
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
             throw Fail(RMC_E_DEVICE, "no HIP device: the model checker runs only on the GPU");
@@ -486,12 +662,19 @@ struct rmc_ctx {
         }
         d_seeds = dmalloc<uint64_t>(seeds.size());
         HIPCHK(hipMemcpy(d_seeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
+        // fingerprint scheme identity (checkpoints): seeds, message hashes, record codec, slot hash
+        scheme_hash = 0x5eed5c4e3e000003ull;
+        auto mixin = [&](uint64_t v) { scheme_hash = mix64(scheme_hash ^ (v + 0x9e3779b97f4a7c15ull)); };
+        for (uint64_t s : seeds) mixin(s);
+        for (const ulonglong2 &g : U.gmsg) { mixin(g.x); mixin(g.y); }
+        mixin((uint64_t)ks.CCW);
+        mixin((uint64_t)Codec<3, 2>::BITS);
 
         // successor slots per chunk: dense for the sharded path, sparse (parents x maxsucc) for
-        // the fused single-GPU path, whose staging holds CW*4 + 36 bytes per slot
-        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (W > 1 ? (virt ? (1ull << 23) : (1ull << 26)) : (1ull << 25));
+        // the fused single-GPU path, whose staging holds SW4 * 16 + 36 bytes per slot
+        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (W > 1 ? (virt ? (1ull << 23) : (1ull << 26)) : (1ull << 26));
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
-        if (Gcap >= (1ull << 31)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^31");
+        if (Gcap >= (1ull << 30)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^30");
         chunk_parents = Gcap / ks.maxsucc;
         shard_min = W > 1 ? (cfg.shard_min_states ? cfg.shard_min_states : (1ull << 20)) : 0;
         const bool fused_ok = W == 1 || shard_min > 1;  // shard 0 runs the fused single-GPU level
@@ -531,16 +714,20 @@ struct rmc_ctx {
         if (fused) {
             s.LXY = dmalloc<ulonglong2>(Lcap_max);
             HIPCHK(hipMemsetAsync(s.LXY, 0, Lcap_max * 16, stream));
-            s.score = dmalloc<uint4>(Gcap * (uint64_t)(ks.CW / 4));
-            s.saux = dmalloc<uint4>(Gcap);
+            int sw4 = ks.N >= 4 ? 3 : 2;
+            s.score = dmalloc<uint4>(Gcap * (uint64_t)sw4);
             s.wcnt = dmalloc<uint32_t>(chunk_parents + 1);
             s.wacc = dmalloc<uint32_t>(chunk_parents + 1);
+            s.pnm = dmalloc<uint32_t>(chunk_parents + 1);
+            s.wposw = dmalloc<uint32_t>(chunk_parents + 1);
             s.ctick = dmalloc<uint32_t>(33 * 32);
             HIPCHK(hipMemsetAsync(s.ctick, 0, 33 * 32 * 4, stream));
             HIPCHK(hipMemsetAsync(s.wacc, 0, (chunk_parents + 1) * 4, stream));
             s.bw = dmalloc<uint32_t>(1024);
             s.bg = dmalloc<uint32_t>(1024);
             s.boff = dmalloc<uint32_t>(1024);
+            s.bww = dmalloc<uint32_t>(1024);
+            s.boffw = dmalloc<uint32_t>(1024);
             s.tickets = dmalloc<uint32_t>(4);
             HIPCHK(hipMemsetAsync(s.tickets, 0, 16, stream));
             s.ctl = dmalloc<LevelCtl>(1);
@@ -577,30 +764,37 @@ struct rmc_ctx {
         HIPCHK(hipMemsetAsync(s.flags, 0, 16, stream));
         s.sum = dmalloc<unsigned long long>(160);
         HIPCHK(hipHostMalloc((void **)&s.hsum, 160 * 8, hipHostMallocDefault));
-        s.cur_cap = s.nxt_cap = 1 << 16;
-        s.cur = dmalloc<uint32_t>(s.cur_cap * RECW);
-        s.nxt = dmalloc<uint32_t>(s.nxt_cap * RECW);
+        s.rcap = 1ull << 18;
+        s.R = dmalloc<uint32_t>(s.rcap);
+        s.cur_off_cap = s.nxt_off_cap = 1 << 16;
+        s.cur_off = dmalloc<uint64_t>(s.cur_off_cap);
+        s.nxt_off = dmalloc<uint64_t>(s.nxt_off_cap);
         s.trace_cap = 1 << 20;
         s.par = dmalloc<uint64_t>(s.trace_cap);
         s.pslot = dmalloc<uint16_t>(s.trace_cap);
     }
 
     void free_shard(Shard &s) {
-        dfree(s.cur); dfree(s.nxt); dfree(s.T); dfree(s.par); dfree(s.pslot); dfree(s.cnt); dfree(s.off);
+        dfree(s.R); dfree(s.cur_off); dfree(s.nxt_off); dfree(s.T); dfree(s.Tc); dfree(s.par); dfree(s.pslot);
+        dfree(s.cnt); dfree(s.off);
         dfree(s.lslot); dfree(s.wflag); dfree(s.wpos); dfree(s.fp); dfree(s.L); dfree(s.LXY); dfree(s.tmp); dfree(s.okey);
         dfree(s.okey2); dfree(s.iota); dfree(s.perm); dfree(s.sflag); dfree(s.spos); dfree(s.sfp); dfree(s.ocnt);
         dfree(s.rfp); dfree(s.rlslot); dfree(s.rflag); dfree(s.rpos); dfree(s.rcount); dfree(s.sx); dfree(s.rx);
         dfree(s.pick_idx); dfree(s.err); dfree(s.sum); dfree(s.flags);
-        dfree(s.score); dfree(s.saux); dfree(s.wcnt); dfree(s.wacc); dfree(s.ctick); dfree(s.bw); dfree(s.bg); dfree(s.boff); dfree(s.tickets);
+        dfree(s.score); dfree(s.wcnt); dfree(s.wacc); dfree(s.pnm); dfree(s.wposw); dfree(s.ctick);
+        dfree(s.bw); dfree(s.bg); dfree(s.boff); dfree(s.bww); dfree(s.boffw); dfree(s.tickets);
         dfree(s.ctl); dfree(s.lrec);
         if (s.hsum) (void)hipHostFree(s.hsum);
         if (s.hctl) (void)hipHostFree(s.hctl);
         if (s.hsnap) (void)hipHostFree(s.hsnap);
         if (s.hlrec) (void)hipHostFree(s.hlrec);
         s.hsum = nullptr; s.hctl = nullptr; s.hsnap = nullptr; s.hlrec = nullptr;
+        s.hpar.release();
+        s.hslot.release();
     }
 
     void release() {
+        if (stream) (void)hipStreamSynchronize(stream);
         for (Shard &s : sh) free_shard(s);
         sh.clear();
         dfree(d_info); dfree(d_nat2id); dfree(d_gmsg); dfree(d_perms); dfree(d_seeds);
@@ -620,43 +814,126 @@ struct rmc_ctx {
         stream = nullptr;
     }
 
-    void grow_records(uint32_t *&buf, uint64_t &cap, uint64_t used, uint64_t need, uint64_t recw) {
+    // ---- frontier storage --------------------------------------------------------------------
+    // offsets array with `used` entries kept
+    void ensure_off(uint64_t *&p, uint64_t &cap, uint64_t used, uint64_t need) {
         if (need <= cap) return;
-        uint64_t nc = std::max<uint64_t>(need + need / 2, cap * 2);
-        uint32_t *nb = dmalloc<uint32_t>(nc * recw);
-        if (used) HIPCHK(hipMemcpyAsync(nb, buf, used * recw * 4, hipMemcpyDeviceToDevice, stream));
+        const uint64_t nc = std::max<uint64_t>(need + need / 2, cap * 2);
+        uint64_t *nb = dmalloc<uint64_t>(nc);
+        if (used) HIPCHK(hipMemcpyAsync(nb, p, used * 8, hipMemcpyDeviceToDevice, stream));
         HIPCHK(hipStreamSynchronize(stream));
-        dfree(buf);
-        buf = nb;
+        dfree(p);
+        p = nb;
         cap = nc;
     }
 
+    // copy `words` ring words starting at ring position `from` (wrapping) to dst (linear)
+    void ring_copy_out(const Shard &s, uint64_t from, uint64_t words, uint32_t *dst) {
+        const uint64_t n1 = std::min(words, s.rcap - from);
+        if (n1) HIPCHK(hipMemcpyAsync(dst, s.R + from, n1 * 4, hipMemcpyDeviceToDevice, stream));
+        if (words > n1) HIPCHK(hipMemcpyAsync(dst + n1, s.R, (words - n1) * 4, hipMemcpyDeviceToDevice, stream));
+    }
+
+    // replace the ring by one of `nc` words holding the live region (the current level and the
+    // next level so far) from position 0
+    bool ring_realloc(Shard &s, uint64_t nc) {
+        uint32_t *nr = dmalloc_try<uint32_t>(nc);
+        if (!nr) return false;
+        ring_copy_out(s, s.cur_wbase, s.cur_words + s.nxt_words, nr);
+        HIPCHK(hipStreamSynchronize(stream));
+        dfree(s.R);
+        s.R = nr;
+        s.rcap = nc;
+        s.cur_wbase = 0;
+        return true;
+    }
+
+    // Room for `extra` more words of the next level.  `consumed` = words at the start of the
+    // current level that are no longer needed (its chunks already expanded): a ring at its budget
+    // reuses them.
+    void ensure_ring(Shard &s, uint64_t extra, uint64_t consumed) {
+        const uint64_t live = s.cur_words + s.nxt_words;
+        if (live + extra <= s.rcap) return;
+        if (!s.ring_fixed) {
+            const uint64_t nc = std::max<uint64_t>(s.rcap * 2, (live + extra) + (live + extra) / 2);
+            if (ring_realloc(s, nc)) return;
+        }
+        if (live - consumed + extra <= s.rcap) return;
+        throw Fail(RMC_E_MEMORY, "frontier ring full: " + std::to_string((live - consumed + extra) * 4) +
+                                     " B of live frontier records needed, ring is " + std::to_string(s.rcap * 4) +
+                                     " B (rmc_config.frontier_mem_bytes, or more GPUs)");
+    }
+
+    // device trace buffer for `need` entries from tflushed on (everything earlier is on the host)
     void grow_trace(Shard &s, uint64_t need) {
         if (need <= s.trace_cap) return;
-        uint64_t nc = std::max<uint64_t>(need + need / 2, s.trace_cap * 2);
-        uint64_t *np_ = dmalloc<uint64_t>(nc);
-        uint16_t *ns = dmalloc<uint16_t>(nc);
-        HIPCHK(hipMemcpyAsync(np_, s.par, s.trace_cap * 8, hipMemcpyDeviceToDevice, stream));
-        HIPCHK(hipMemcpyAsync(ns, s.pslot, s.trace_cap * 2, hipMemcpyDeviceToDevice, stream));
-        HIPCHK(hipStreamSynchronize(stream));
+        HIPCHK(hipStreamSynchronize(stream));  // pending flushes read the old buffers
+        const uint64_t nc = std::max<uint64_t>(need + need / 2, s.trace_cap * 2);
         dfree(s.par);
         dfree(s.pslot);
-        s.par = np_;
-        s.pslot = ns;
+        s.par = dmalloc<uint64_t>(nc);
+        s.pslot = dmalloc<uint16_t>(nc);
         s.trace_cap = nc;
     }
 
+    // trace entries of gids [tflushed, upto) to the host (asynchronous, stream-ordered)
+    void flush_trace(Shard &s, uint64_t upto) {
+        if (upto <= s.tflushed) return;
+        const uint64_t n = upto - s.tflushed, at = s.tflushed - s.tdev;
+        s.hpar.from_device(s.par + at, s.tflushed, n, stream);
+        s.hslot.from_device(s.pslot + at, s.tflushed, n, stream);
+        s.tflushed = upto;
+    }
+    // the device trace buffer starts over at the first gid not yet on the host
+    void trace_restart(Shard &s) { s.tdev = s.tflushed; }
+
+    // Seen set: keep the load <= 1/2 in the full (16-B) table, grown x4 by rehash, up to
+    // 2^compact_log2 slots; then migrate once to the compact table sized from the budget, whose
+    // load may reach 0.9.
     void grow_seen(Shard &s, uint64_t need) {
-        if (need * 2 <= s.T_cap) return;  // keep the load factor <= 1/2
+        if (s.Tc) {
+            if ((double)need > 0.9 * (double)s.T_cap)
+                throw Fail(RMC_E_MEMORY, "seen set full: " + std::to_string(need) + " fingerprints in " +
+                                             std::to_string(s.T_cap) + " 8-B slots (rmc_config.seen_mem_bytes, or more GPUs)");
+            return;
+        }
+        if (need * 2 <= s.T_cap) return;
         uint64_t nc = s.T_cap;
         while (need * 2 > nc) nc *= 4;
+        const uint32_t full_max = cfg.compact_log2 ? cfg.compact_log2 : 27;
+        if (nc > (1ull << full_max)) { migrate_compact(s, need); return; }
         ulonglong2 *nT = dmalloc<ulonglong2>(nc);
         HIPCHK(hipMemsetAsync(nT, 0, nc * 16, stream));
-        launch_rehash(s.T, s.T_cap, nT, nc - 1, stream);
+        launch_rehash(s.T, s.T_cap, Seen{nT, nullptr, nc - 1}, stream);
         HIPCHK(hipStreamSynchronize(stream));
         dfree(s.T);
         s.T = nT;
         s.T_cap = nc;
+    }
+
+    void migrate_compact(Shard &s, uint64_t need) {
+        const uint64_t local = sh.size();
+        HIPCHK(hipStreamSynchronize(stream));
+        const uint64_t budget = cfg.seen_mem_bytes ? cfg.seen_mem_bytes : free_device_bytes() / 2 / local;
+        uint64_t slots = 1;
+        while (slots * 2 * 8 <= budget) slots *= 2;
+        if ((double)need > 0.85 * (double)slots)
+            throw Fail(RMC_E_MEMORY, "seen set: " + std::to_string(need) + " fingerprints do not fit the budget of " +
+                                         std::to_string(budget) + " B");
+        unsigned long long *Tc = dmalloc<unsigned long long>(slots);
+        HIPCHK(hipMemsetAsync(Tc, 0, slots * 8, stream));
+        launch_rehash(s.T, s.T_cap, Seen{nullptr, Tc, slots - 1}, stream);
+        HIPCHK(hipStreamSynchronize(stream));
+        dfree(s.T);
+        s.Tc = Tc;
+        s.T_cap = slots;
+        // the run is large: the frontier ring goes to its budget and stops growing
+        const uint64_t fb = cfg.frontier_mem_bytes ? cfg.frontier_mem_bytes
+                                                   : (uint64_t)((double)free_device_bytes() * 0.7) / local;
+        const uint64_t words = std::max<uint64_t>(fb / 4, s.rcap);
+        if (words > s.rcap && !ring_realloc(s, words))
+            throw Fail(RMC_E_MEMORY, "frontier ring of " + std::to_string(words * 4) + " B");
+        s.ring_fixed = true;
     }
 
     template <class T>
@@ -669,7 +946,7 @@ struct rmc_ctx {
     }
 
     void grow_recv(Shard &s, uint64_t need) {
-        if (need + 1 <= s.rcap) return;
+        if (need + 1 <= s.rcap_x) return;
         uint64_t nc = std::max<uint64_t>(need + need / 2 + 1, 1024);
         dfree(s.rfp); dfree(s.rlslot); dfree(s.rflag); dfree(s.rpos);
         s.rfp = dmalloc<ulonglong2>(nc);
@@ -677,7 +954,7 @@ struct rmc_ctx {
         s.rflag = dmalloc<uint32_t>(nc);
         s.rpos = dmalloc<uint32_t>(nc);
         HIPCHK(hipMemsetAsync(s.rflag, 0, nc * 4, stream));
-        s.rcap = nc;
+        s.rcap_x = nc;
         if (!s.rcount) s.rcount = dmalloc<uint32_t>(4);
     }
 
@@ -827,11 +1104,19 @@ struct rmc_ctx {
         return cnt;
     }
 
+    // level-local parent p of shard s (current level) -> d_one (RECW words, fixed stride)
+    void record_to_one(Shard &s, uint64_t p) {
+        const uint64_t o = d2h(s.cur_off + p);
+        ring_copy_out(s, ring_wrap(s.cur_wbase + o, s.rcap), std::min<uint64_t>(RECW, s.rcap), d_one);
+        HIPCHK(hipStreamSynchronize(stream));
+    }
+
     // ---- BFS --------------------------------------------------------------------------
     int init(rmc_level_stats *st) {
         if (inited) throw Fail(RMC_E_STATE, "rmc_init called twice");
         auto t0 = std::chrono::steady_clock::now();
         std::vector<uint32_t> rec = init_record();
+        const uint32_t rw = record_words(rec.data());
         HIPCHK(hipMemcpy(d_one, rec.data(), RECW * 4, hipMemcpyHostToDevice));
         KParams P = base(sh[0]);
         P.front = d_one;
@@ -847,15 +1132,20 @@ struct rmc_ctx {
         int32_t iv[7];
         HIPCHK(hipMemcpyAsync(iv, d_inv, sizeof iv, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
-        const uint64_t none = ~0ull;
+        const uint64_t zero = 0;
         for (Shard &s : sh) {
             s.level_start = {0};
             s.cur_n = 0;
+            s.cur_wbase = s.cur_words = s.nxt_words = 0;
             if (replicated ? &s != &sh[0] : (uint32_t)s.id != owner) continue;
-            HIPCHK(hipMemcpyAsync(s.cur, d_one, RECW * 4, hipMemcpyDeviceToDevice, stream));
-            launch_insert_fps(d_fp1, 1, s.T, s.T_cap - 1, stream);
-            HIPCHK(hipMemcpyAsync(s.par, &none, 8, hipMemcpyHostToDevice, stream));
+            HIPCHK(hipMemcpyAsync(s.R, d_one, rw * 4, hipMemcpyDeviceToDevice, stream));
+            HIPCHK(hipMemcpyAsync(s.cur_off, &zero, 8, hipMemcpyHostToDevice, stream));
+            launch_insert_fps(d_fp1, 1, s.seen(), stream);
+            s.hpar.set(0, ~0ull);
+            s.hslot.set(0, 0);
+            s.tflushed = 1;
             s.cur_n = 1;
+            s.cur_words = rw;
             s.T_count = 1;
         }
         HIPCHK(hipStreamSynchronize(stream));
@@ -864,8 +1154,8 @@ struct rmc_ctx {
         depth = 1;
         inited = true;
         status = RMC_OK;
-        for (int b = 0; b < 7; b++) {
-            if (!(cfg.invariants & (1u << b))) continue;
+        for (uint32_t o = inv_order; o; o >>= 4) {
+            const int b = (int)(o & 15u) - 1;
             if (iv[b] != 1) {
                 status = iv[b] == 0 ? RMC_VIOLATION : RMC_EVAL_ERROR;
                 violated = b;
@@ -888,6 +1178,7 @@ struct rmc_ctx {
             st->new_states = 1;
             st->expanded = 0;
             st->seconds = seconds;
+            st->new_bytes = rw * 4ull;
         }
         return status;
     }
@@ -902,6 +1193,31 @@ struct rmc_ctx {
         return (W == 1 || replicated) ? step_single(st) : step_sharded(st);
     }
 
+    // shard t takes over parents [o, o + n) of shard src's current level: records (their words)
+    // into t's ring from position 0, offsets rebased to the first of them
+    void take_parents(Shard &src, Shard &t, uint64_t o, uint64_t n) {
+        const uint64_t F = src.cur_n;
+        const uint64_t w_lo = o < F ? d2h(src.cur_off + o) : src.cur_words;
+        const uint64_t w_hi = o + n < F ? d2h(src.cur_off + o + n) : src.cur_words;
+        if (&src == &t) {
+            ensure_off(t.nxt_off, t.nxt_off_cap, 0, std::max<uint64_t>(n, 1));
+            launch_rebase(t.cur_off + o, n, w_lo, t.nxt_off, stream);
+            std::swap(t.cur_off, t.nxt_off);
+            std::swap(t.cur_off_cap, t.nxt_off_cap);
+            t.cur_wbase = ring_wrap(t.cur_wbase + w_lo, t.rcap);
+        } else {
+            t.cur_words = t.nxt_words = 0;
+            t.cur_wbase = 0;
+            ensure_ring(t, w_hi - w_lo, 0);
+            ring_copy_out(src, ring_wrap(src.cur_wbase + w_lo, src.rcap), w_hi - w_lo, t.R);
+            ensure_off(t.cur_off, t.cur_off_cap, 0, std::max<uint64_t>(n, 1));
+            launch_rebase(src.cur_off + o, n, w_lo, t.cur_off, stream);
+        }
+        t.cur_words = w_hi - w_lo;
+        t.cur_n = n;
+        HIPCHK(hipStreamSynchronize(stream));
+    }
+
     // Replicated -> sharded, at the start of the first level with >= shard_min states.  Every
     // shard holds that level whole (and every state seen so far in its seen set); shard i keeps
     // parents [F*i/W, F*(i+1)/W) as its frontier, so parent references of the next level,
@@ -912,38 +1228,43 @@ struct rmc_ctx {
         const size_t L = s0.level_start.size();
         const uint64_t F = s0.cur_n, base = s0.level_start[L - 1];
         auto off = [&](int i) { return F * (uint64_t)i / (uint64_t)W; };
+        HIPCHK(hipStreamSynchronize(stream));
         if (virt) {
             for (int i = 1; i < W; i++) {
                 Shard &t = sh[i];
                 const uint64_t o = off(i), n = off(i + 1) - o;
-                if (t.T_cap != s0.T_cap) {
-                    dfree(t.T);
-                    t.T = dmalloc<ulonglong2>(s0.T_cap);
-                    t.T_cap = s0.T_cap;
+                if (s0.Tc) {
+                    if (!t.Tc || t.T_cap != s0.T_cap) {
+                        dfree(t.T);
+                        dfree(t.Tc);
+                        t.Tc = dmalloc<unsigned long long>(s0.T_cap);
+                        t.T_cap = s0.T_cap;
+                    }
+                    HIPCHK(hipMemcpyAsync(t.Tc, s0.Tc, s0.T_cap * 8, hipMemcpyDeviceToDevice, stream));
+                } else {
+                    if (t.T_cap != s0.T_cap || !t.T) {
+                        dfree(t.T);
+                        t.T = dmalloc<ulonglong2>(s0.T_cap);
+                        t.T_cap = s0.T_cap;
+                    }
+                    HIPCHK(hipMemcpyAsync(t.T, s0.T, s0.T_cap * 16, hipMemcpyDeviceToDevice, stream));
                 }
-                HIPCHK(hipMemcpyAsync(t.T, s0.T, s0.T_cap * 16, hipMemcpyDeviceToDevice, stream));
                 t.T_count = s0.T_count;
                 t.level_start = s0.level_start;
                 t.level_start.back() = base + o;
-                grow_records(t.cur, t.cur_cap, 0, std::max<uint64_t>(n, 1), RECW);
-                grow_trace(t, base + o + n + 1);
-                if (n) {
-                    HIPCHK(hipMemcpyAsync(t.cur, s0.cur + o * RECW, n * RECW * 4, hipMemcpyDeviceToDevice, stream));
-                    HIPCHK(hipMemcpyAsync(t.par + base + o, s0.par + base + o, n * 8, hipMemcpyDeviceToDevice, stream));
-                    HIPCHK(hipMemcpyAsync(t.pslot + base + o, s0.pslot + base + o, n * 2, hipMemcpyDeviceToDevice, stream));
-                }
-                t.cur_n = n;
+                take_parents(s0, t, o, n);
+                t.hpar.copy_from(s0.hpar, base + o, n);
+                t.hslot.copy_from(s0.hslot, base + o, n);
+                t.tflushed = base + o + n;
                 t.epoch = std::max(t.epoch, s0.epoch);
             }
-            s0.cur_n = off(1);
+            take_parents(s0, s0, 0, off(1));
+            s0.tflushed = base + off(1);
         } else {
             const uint64_t o = off(rank), n = off(rank + 1) - o;
-            grow_records(s0.nxt, s0.nxt_cap, 0, std::max<uint64_t>(n, 1), RECW);
-            if (n) HIPCHK(hipMemcpyAsync(s0.nxt, s0.cur + o * RECW, n * RECW * 4, hipMemcpyDeviceToDevice, stream));
-            std::swap(s0.cur, s0.nxt);
-            std::swap(s0.cur_cap, s0.nxt_cap);
-            s0.cur_n = n;
+            take_parents(s0, s0, o, n);
             s0.level_start.back() = base + o;
+            s0.tflushed = base + o + n;
         }
         HIPCHK(hipStreamSynchronize(stream));
         replicated = false;
@@ -971,6 +1292,18 @@ struct rmc_ctx {
         s.lxy_epoch0 = s.epoch;
     }
 
+    void end_level(Shard &s, uint64_t gid_nxt, int L) {
+        std::swap(s.cur_off, s.nxt_off);
+        std::swap(s.cur_off_cap, s.nxt_off_cap);
+        s.cur_wbase = s.nbase();
+        s.cur_words = s.nxt_words;
+        s.nxt_words = 0;
+        s.cur_n = s.nxt_n;
+        s.nxt_n = 0;
+        if (s.cur_n) s.level_start.push_back(gid_nxt);
+        (void)L;
+    }
+
     int step_single(rmc_level_stats *st) {
         auto t0 = std::chrono::steady_clock::now();
         Shard &s = sh[0];
@@ -979,24 +1312,30 @@ struct rmc_ctx {
         st->expanded = s.cur_n;
         const uint64_t gid_cur = s.level_start[L - 1];
         const uint64_t gid_nxt = gid_cur + s.cur_n;
-        uint64_t nxt_n = 0, level_gen = 0;
+        uint64_t level_gen = 0;
+        s.nxt_n = 0;
+        s.nxt_words = 0;
+        const uint64_t MSW = (uint64_t)ks.maxsucc * (uint64_t)ks.RECW_MAX;
         for (uint64_t p0 = 0; p0 < s.cur_n; p0 += chunk_parents) {
             const uint64_t p1 = std::min(s.cur_n, p0 + chunk_parents), np_ = p1 - p0;
             // Small chunks size the next level, trace and seen set on the successor upper bound
             // without a host round trip; large ones read the winner count back before commit.
             const uint64_t Gub = np_ * (uint64_t)ks.maxsucc;
-            const bool small = Gub <= (1ull << 23);
+            const bool small = Gub <= (1ull << 20);
+            const uint64_t consumed = (s.ring_fixed && p0) ? d2h(s.cur_off + p0) : 0;
             if (small) {
-                grow_records(s.nxt, s.nxt_cap, nxt_n, nxt_n + Gub, RECW);
-                grow_trace(s, gid_nxt + nxt_n + Gub);
+                ensure_ring(s, np_ * MSW, consumed);
+                ensure_off(s.nxt_off, s.nxt_off_cap, s.nxt_n, s.nxt_n + Gub);
+                grow_trace(s, Gub);
                 grow_seen(s, s.T_count + Gub);
             }
             const uint64_t Lcap = std::min(next_pow2(2 * Gub), Lcap_max);
             renew_election_tags(s, 1);
             ++s.epoch;
+            trace_restart(s);
             auto params = [&] {
-                KParams Q = chunk_params(s, s.cur, s.nxt);
-                Q.p_begin = p0; Q.p_end = p1; Q.next_base = nxt_n;
+                KParams Q = chunk_params(s);
+                Q.p_begin = p0; Q.p_end = p1; Q.next_base = s.nxt_n; Q.next_wbase = s.nxt_words;
                 Q.gid_next_base = gid_nxt; Q.gid_parent_base = gid_cur;
                 Q.Lmask = Lcap - 1;
                 Q.epoch = s.epoch;
@@ -1006,10 +1345,13 @@ struct rmc_ctx {
             timed(PH_HASH, [&] { ks.fused(params(), stream); });
             timed(PH_DEDUP, [&] { ks.wincount(params(), np_, stream); });
             if (!small) {
-                const uint64_t Wub = d2h(s.sum + 1);
+                HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipStreamSynchronize(stream));
                 collect_times(st);
-                grow_records(s.nxt, s.nxt_cap, nxt_n, nxt_n + Wub, RECW);
-                grow_trace(s, gid_nxt + nxt_n + Wub);
+                const uint64_t Wub = s.hsum[1], Wwords = s.hsum[SUM_WORDS];
+                ensure_ring(s, Wwords, consumed);
+                ensure_off(s.nxt_off, s.nxt_off_cap, s.nxt_n, s.nxt_n + Wub);
+                grow_trace(s, Wub);
                 grow_seen(s, s.T_count + Wub);
             }
             timed(PH_MAT, [&] { ks.commit(params(), stream); });  // + chunk summary
@@ -1017,35 +1359,37 @@ struct rmc_ctx {
             HIPCHK(hipStreamSynchronize(stream));
             HIPCHK(hipGetLastError());
             collect_times(st);
-            const uint64_t G = s.hsum[0], Wn = s.hsum[1];
+            const uint64_t G = s.hsum[0], Wn = s.hsum[1], Ww = s.hsum[SUM_WORDS];
             if (s.hsum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
+            flush_trace(s, gid_nxt + s.nxt_n + Wn);
             level_gen += G;
             s.T_count += Wn;
             unsigned long long best;
             const int kind = first_error(s.hsum + 2, &best);
             if (kind >= 0) {
-                stop_on_error(kind, best, p0, nxt_n, gid_cur, gid_nxt, level_gen - G, st);
+                stop_on_error(kind, best, p0, s.nxt_n, gid_cur, gid_nxt, level_gen - G, st);
                 st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
                 seconds += st->seconds;
                 return status;
             }
-            nxt_n += Wn;
+            s.nxt_n += Wn;
+            s.nxt_words += Ww;
+            s.peak_words = std::max(s.peak_words, s.cur_words - consumed + s.nxt_words);
         }
         total_generated += level_gen;
-        total_distinct += nxt_n;
+        total_distinct += s.nxt_n;
         st->generated = level_gen;
-        st->new_states = nxt_n;
-        std::swap(s.cur, s.nxt);
-        std::swap(s.cur_cap, s.nxt_cap);
-        s.cur_n = nxt_n;
+        st->new_states = s.nxt_n;
+        st->new_bytes = s.nxt_words * 4;
+        end_level(s, gid_nxt, L);
         if (s.cur_n) {
-            s.level_start.push_back(gid_nxt);
             depth = L + 1;
         } else {
             finished = true;
             status = RMC_DONE;
             queue_at_end = 0;
         }
+        HIPCHK(hipStreamSynchronize(stream));  // the trace copies of the level
         st->total_generated = total_generated;
         st->total_distinct = total_distinct;
         st->queue = s.cur_n;
@@ -1057,9 +1401,10 @@ struct rmc_ctx {
 
     // ---- device-driven levels (single GPU) ---------------------------------------------
     // Up to `maxl` levels are enqueued with no host round trip: each level's commit writes the
-    // next level's parent count, id bases, epoch and table size into the control block that the
-    // following kernels read, and stops the loop on an empty level, an error, or a level whose
-    // successor bound might not fit the buffers (the host then grows them and carries on).
+    // next level's parent count, id bases, ring positions, epoch and table size into the control
+    // block that the following kernels read, and stops the loop on an empty level, an error, or a
+    // level whose successor bound might not fit the buffers (the host then grows them and
+    // carries on).
     int batch_levels() const { return cfg.device_levels ? (int)cfg.device_levels : LREC_CAP; }
     uint64_t dev_parents() const { return std::min<uint64_t>(chunk_parents, 1ull << 15); }
     bool batch_ok() const {
@@ -1075,21 +1420,28 @@ struct rmc_ctx {
         const int K = std::max(1, std::min(maxl, LREC_CAP));
         // capacities with headroom for several levels; the first level always fits
         const uint64_t target = std::min(std::max<uint64_t>(s.cur_n * MS * 32, 1ull << 16), DP * MS);
-        grow_records(s.cur, s.cur_cap, s.cur_n, target, RECW);
-        grow_records(s.nxt, s.nxt_cap, 0, target, RECW);
+        s.nxt_words = 0;
+        ensure_ring(s, target * (uint64_t)ks.RECW_MAX, 0);
+        ensure_off(s.cur_off, s.cur_off_cap, s.cur_n, target);
+        ensure_off(s.nxt_off, s.nxt_off_cap, 0, target);
         const int L0 = (int)s.level_start.size();
         const uint64_t gid0 = s.level_start[L0 - 1];
-        grow_trace(s, gid0 + s.cur_n + 4 * target);
+        grow_trace(s, 4 * target);
         grow_seen(s, s.T_count + 2 * target);
+        trace_restart(s);
         LevelCtl &h = *s.hctl;
         std::memset(&h, 0, sizeof h);
         h.cur_n = s.cur_n;
         h.gid_cur = gid0;
         h.T_count = s.T_count;
         h.Lmask = std::min(next_pow2(2 * s.cur_n * MS), Lcap_max) - 1;
-        h.nxt_cap = std::min(s.cur_cap, s.nxt_cap);
+        h.cur_wbase = s.cur_wbase;
+        h.cur_words = s.cur_words;
+        h.off_cap = std::min(s.cur_off_cap, s.nxt_off_cap);
+        h.rcap = s.rcap;
+        h.trace_base = s.tdev;
         h.trace_cap = s.trace_cap;
-        h.T_cap = s.T_cap;
+        h.T_cap = s.Tc ? (uint64_t)((double)s.T_cap * 0.9) * 2 / 2 : s.T_cap;
         h.chunk_parents = replicated ? std::min<uint64_t>(DP, shard_min - 1) : DP;  // stop before sharding starts
         h.Lcap_max = Lcap_max;
         h.level = (uint32_t)L0;
@@ -1098,7 +1450,7 @@ struct rmc_ctx {
         h.stop = CTL_RUN;
         h.batch = (uint32_t)K;
         HIPCHK(hipMemcpyAsync(s.ctl, &h, sizeof h, hipMemcpyHostToDevice, stream));
-        uint32_t *bufs[2] = {s.cur, s.nxt};
+        uint64_t *offs[2] = {s.cur_off, s.nxt_off};
         std::vector<size_t> mark(K);
         // Levels go in groups; after each group a snapshot of the control block is copied back
         // with an event.  Group g + 2 is enqueued only once group g's snapshot says the loop is
@@ -1113,7 +1465,9 @@ struct rmc_ctx {
         auto enqueue_group = [&](int g) {
             for (int i = g * GL; i < std::min(K, (g + 1) * GL); i++) {
                 mark[i] = evrecs.size();
-                KParams Q = chunk_params(s, bufs[i & 1], bufs[(i + 1) & 1]);
+                KParams Q = chunk_params(s);
+                Q.foff = offs[i & 1];
+                Q.noff = offs[(i + 1) & 1];
                 Q.ctl = s.ctl;
                 Q.lrec = s.lrec;
                 Q.p_begin = 0;
@@ -1178,6 +1532,7 @@ struct rmc_ctx {
             st->expanded = r.expanded;
             st->generated = r.generated;
             st->new_states = r.new_states;
+            st->new_bytes = r.words * 4;
             st->total_generated = total_generated;
             st->total_distinct = total_distinct;
             st->queue = r.new_states;
@@ -1185,12 +1540,18 @@ struct rmc_ctx {
             st->seconds = el / nst;
         }
         if (D & 1) {
-            std::swap(s.cur, s.nxt);
-            std::swap(s.cur_cap, s.nxt_cap);
+            std::swap(s.cur_off, s.nxt_off);
+            std::swap(s.cur_off_cap, s.nxt_off_cap);
         }
         s.cur_n = c.cur_n;
+        s.cur_wbase = c.cur_wbase;
+        s.cur_words = c.cur_words;
+        s.nxt_n = 0;
+        s.nxt_words = 0;
         s.epoch = c.epoch;
+        s.peak_words = std::max(s.peak_words, s.cur_words);
         if (s.T_count != c.T_count) throw Fail(RMC_E_STATE, "device level loop: seen-set count mismatch");
+        flush_trace(s, c.gid_cur + c.cur_n);
         seconds += el;
         if (c.stop == CTL_ERROR) {
             // the level the loop stopped in is intact: report its error as the host path does
@@ -1201,12 +1562,14 @@ struct rmc_ctx {
             st->level = L;
             st->expanded = s.cur_n;
             const uint64_t gid_cur = s.level_start[L - 1];
+            flush_trace(s, gid_cur + s.cur_n + s.hsum[1]);  // the error level's winners
             s.T_count += s.hsum[1];
             unsigned long long best;
             const int kind = first_error(s.hsum + 2, &best);
             if (kind < 0) throw Fail(RMC_E_STATE, "device level loop stopped without an error");
             stop_on_error(kind, best, 0, 0, gid_cur, gid_cur + s.cur_n, 0, st);
         }
+        HIPCHK(hipStreamSynchronize(stream));
         return nst;
     }
 
@@ -1214,6 +1577,7 @@ struct rmc_ctx {
     void stop_on_error(int kind, unsigned long long ek, uint64_t p0, uint64_t nxt_before, uint64_t gid_cur,
                        uint64_t gid_nxt, uint64_t gen_before_chunk, rmc_level_stats *st) {
         Shard &s = sh[0];
+        HIPCHK(hipStreamSynchronize(stream));
         const uint64_t p = ek >> 24;                       // level-local parent
         const uint32_t slot = (uint32_t)((ek >> 8) & 0xFFFF);
         const int which = (int)(ek & 0xFF);
@@ -1233,11 +1597,11 @@ struct rmc_ctx {
             HIPCHK(hipMemcpy(ls.data(), s.lslot + pl * ks.maxsucc, upto * 4, hipMemcpyDeviceToHost));
             uint64_t w = 0;
             for (uint32_t r = 0; r < upto; r++)
-                if (ls[r] < LS_ELECT && (uint32_t)d2h(s.L + ls[r]) == (uint32_t)(pl * ks.maxsucc + r)) w++;
+                if (ls[r] < LS_ELECT && ((uint32_t)d2h(s.L + ls[r]) >> 2) == (uint32_t)(pl * ks.maxsucc + r)) w++;
             return w;
         };
         // successors of p, in order, to find the sub-action batch boundaries
-        HIPCHK(hipMemcpy(d_one, s.cur + p * RECW, RECW * 4, hipMemcpyDeviceToDevice));
+        record_to_one(s, p);
         std::vector<uint32_t> keys;
         bool af = false;
         expand_one(&keys, nullptr, nullptr, &af);
@@ -1290,7 +1654,7 @@ struct rmc_ctx {
         st->level = L;
         uint64_t agg[2] = {0, 0};
         for (Shard &s : sh) agg[0] = std::max<uint64_t>(agg[0], (s.cur_n + chunk_parents - 1) / chunk_parents);
-        for (Shard &s : sh) { st->expanded += s.cur_n; s.nxt_n = 0; }
+        for (Shard &s : sh) { st->expanded += s.cur_n; s.nxt_n = 0; s.nxt_words = 0; }
         allreduce(agg, 1, true);
         const uint64_t nchunks = agg[0];
         const size_t NL = sh.size();
@@ -1312,7 +1676,8 @@ struct rmc_ctx {
                 std::fill(scnt[li].begin(), scnt[li].end(), 0);
                 if (!s.np) continue;
                 KParams Q = base(s);
-                Q.front = s.cur; Q.p_begin = s.p0; Q.p_end = s.p0 + s.np; Q.cnt = s.cnt; Q.off = s.off; Q.fp = s.fp;
+                ring_params(s, Q);
+                Q.p_begin = s.p0; Q.p_end = s.p0 + s.np; Q.cnt = s.cnt; Q.off = s.off; Q.fp = s.fp;
                 Q.gid_parent_base = gid_cur;
                 timed(PH_COUNT, [&] {
                     ks.count(Q, stream);
@@ -1361,7 +1726,7 @@ struct rmc_ctx {
                 if (R * 2 > Lcap_max) throw Fail(RMC_E_CAPACITY, "owner receive batch exceeds the election table");
                 ++o.epoch;
                 timed(PH_DEDUP, [&] {
-                    launch_dedup(o.rfp, o.rcount, R, o.T, o.T_cap - 1, o.L, Lcap - 1, o.epoch, o.rlslot, stream);
+                    launch_dedup(o.rfp, o.rcount, R, o.seen(), o.L, Lcap - 1, o.epoch, o.rlslot, stream);
                     launch_recv_flags(o.rlslot, o.L, R, o.rflag, stream);
                 });
                 HIPCHK(hipStreamSynchronize(stream));
@@ -1391,7 +1756,8 @@ struct rmc_ctx {
                 grow_plain(s.sx, s.sx_cap, swoff[li][W] * XW + 1);
                 launch_scatter_flags(s.perm, s.sflag, s.spos, s.G, s.wflag, s.wpos, stream);
                 KParams Q = base(s);
-                Q.front = s.cur; Q.p_begin = s.p0; Q.p_end = s.p0 + s.np; Q.cnt = s.cnt; Q.off = s.off; Q.fp = s.fp;
+                ring_params(s, Q);
+                Q.p_begin = s.p0; Q.p_end = s.p0 + s.np; Q.cnt = s.cnt; Q.off = s.off; Q.fp = s.fp;
                 Q.wflag = s.wflag; Q.wpos = s.wpos; Q.xrec = s.sx; Q.gid_parent_base = s.level_start[L - 1];
                 timed(PH_MAT, [&] { ks.materialize(Q, stream); });
             }
@@ -1410,20 +1776,25 @@ struct rmc_ctx {
                 const uint64_t n = rwoff[li][W];
                 const uint64_t gid_nxt = o.level_start[L - 1] + o.cur_n;
                 if (n) {
-                    grow_records(o.nxt, o.nxt_cap, o.nxt_n, o.nxt_n + n, RECW);
-                    grow_trace(o, gid_nxt + o.nxt_n + n);
+                    ensure_ring(o, n * (uint64_t)RECW, 0);
+                    ensure_off(o.nxt_off, o.nxt_off_cap, o.nxt_n, o.nxt_n + n);
+                    grow_trace(o, n);
                     grow_seen(o, o.T_count + n);
+                    trace_restart(o);
+                    const uint64_t tb = gid_nxt + o.nxt_n - o.tdev;  // == 0: everything earlier is flushed
                     timed(PH_OTHER, [&] {
                         for (int q = 0; q < W; q++) {
                             const uint64_t k = rwin[li][q];
                             if (!k) continue;
-                            launch_accept(o.rx + rwoff[li][q] * XW, k, (uint32_t)RECW, o.nxt + (o.nxt_n + rwoff[li][q]) * RECW,
-                                          o.par + gid_nxt + o.nxt_n + rwoff[li][q], o.pslot + gid_nxt + o.nxt_n + rwoff[li][q],
-                                          (uint64_t)q << 48, stream);
+                            launch_accept(o.rx + rwoff[li][q] * XW, k, (uint32_t)RECW, o.R, o.rcap, o.nbase(),
+                                          o.nxt_words + rwoff[li][q] * (uint64_t)RECW, o.nxt_off + o.nxt_n + rwoff[li][q],
+                                          o.par + tb + rwoff[li][q], o.pslot + tb + rwoff[li][q], (uint64_t)q << 48, stream);
                         }
-                        launch_insert_flagged(o.rfp, o.rflag, roff[li][W], o.T, o.T_cap - 1, stream);
+                        launch_insert_flagged(o.rfp, o.rflag, roff[li][W], o.seen(), stream);
                     });
+                    flush_trace(o, gid_nxt + o.nxt_n + n);
                     o.nxt_n += n;
+                    o.nxt_words += n * (uint64_t)RECW;
                     o.T_count += n;
                     level_new += n;
                 }
@@ -1466,12 +1837,12 @@ struct rmc_ctx {
         st->new_states = glob[1];
         for (Shard &s : sh) {
             const uint64_t gid_nxt = s.level_start[L - 1] + s.cur_n;
-            std::swap(s.cur, s.nxt);
-            std::swap(s.cur_cap, s.nxt_cap);
-            s.cur_n = s.nxt_n;
-            s.nxt_n = 0;
-            s.level_start.push_back(gid_nxt);
+            st->new_bytes += s.nxt_words * 4;
+            s.peak_words = std::max(s.peak_words, s.cur_words + s.nxt_words);
+            end_level(s, gid_nxt, L);
+            if (!s.cur_n) s.level_start.push_back(gid_nxt);  // every shard keeps the same level count
         }
+        HIPCHK(hipStreamSynchronize(stream));
         if (glob[1]) {
             depth = L + 1;
         } else {
@@ -1527,8 +1898,9 @@ struct rmc_ctx {
         uint64_t v[2] = {0, 0};
         for (Shard &s : sh)
             if (s.id == q) {
-                v[0] = d2h(s.par + gid) + 1;  // +1: the Init sentinel ~0 travels as 0
-                v[1] = d2h(s.pslot + gid);
+                if (gid >= s.tflushed) throw Fail(RMC_E_STATE, "trace entry not on the host");
+                v[0] = s.hpar.get(gid) + 1;  // +1: the Init sentinel ~0 travels as 0
+                v[1] = s.hslot.get(gid);
             }
         allreduce(v, 2, false);
         *par = v[0] - 1;
@@ -1537,6 +1909,7 @@ struct rmc_ctx {
 
     // Walk parent pointers from err_ref to Init, then replay the slots from Init.
     void build_trace() {
+        HIPCHK(hipStreamSynchronize(stream));  // pending trace copies
         std::vector<uint16_t> slots;
         if (err_last_slot != KEY_NONE) slots.push_back((uint16_t)err_last_slot);
         uint64_t g = err_ref;
@@ -1567,19 +1940,20 @@ struct rmc_ctx {
         }
     }
 
-    // Forget every explored state but keep all device buffers (repeat runs, benchmarks).
     // ---- checkpoint / resume (rmc_checkpoint, rmc_resume) --------------------------------
     struct CkptHeader {
         uint64_t magic;
         uint32_t abi, recw;
         int32_t n, v, e, r;
-        uint32_t invariants;
-        int32_t check_deadlock, spec_variant, no_symmetry, msg_cap, depth;
-        uint64_t total_generated, total_distinct, T_cap, T_count, cur_n, n_levels, trace_n;
+        uint32_t invariants, inv_order;
+        int32_t check_deadlock, spec_variant, no_symmetry, msg_cap, depth, compact;
+        uint64_t scheme;
+        uint64_t total_generated, total_distinct, T_cap, T_count, cur_n, cur_words, n_levels, trace_n;
         uint32_t epoch, pad;
         double seconds;
+        uint64_t check;  // checksum of every field above
     };
-    static constexpr uint64_t CKPT_MAGIC = 0x3150434b434d52ull;  // "RMCKCP1"
+    static constexpr uint64_t CKPT_MAGIC = 0x3250434b434d52ull;  // "RMCKCP2"
 
     CkptHeader ckpt_header() const {
         CkptHeader h{};
@@ -1588,12 +1962,20 @@ struct rmc_ctx {
         h.recw = (uint32_t)RECW;
         h.n = cfg.n_servers; h.v = cfg.n_vals; h.e = cfg.max_election; h.r = cfg.max_restart;
         h.invariants = cfg.invariants;
+        h.inv_order = inv_order;
         h.check_deadlock = cfg.check_deadlock; h.spec_variant = cfg.spec_variant;
         h.no_symmetry = cfg.no_symmetry; h.msg_cap = ks.MCAP;
+        h.scheme = scheme_hash;
         return h;
     }
+    static uint64_t header_check(const CkptHeader &h) {
+        const unsigned char *b = reinterpret_cast<const unsigned char *>(&h);
+        uint64_t x = 0xcbf29ce484222325ull;
+        for (size_t i = 0; i < offsetof(CkptHeader, check); i++) x = (x ^ b[i]) * 0x100000001b3ull;
+        return x;
+    }
 
-    // device <-> file in bounded pieces through one pinned-free host buffer
+    // device <-> file in bounded pieces through one host buffer
     template <class F>
     void stream_bytes(void *dev, uint64_t bytes, F &&io) {
         std::vector<char> buf((size_t)std::min<uint64_t>(bytes, 64ull << 20));
@@ -1603,6 +1985,8 @@ struct rmc_ctx {
         }
     }
 
+    // Written to path + ".tmp", flushed to disk, then renamed over path: the previous checkpoint
+    // survives until the new one is complete.
     void checkpoint(const char *path) {
         if (W != 1) throw Fail(RMC_E_ARG, "checkpoint: single-GPU runs only");
         if (!inited || finished) throw Fail(RMC_E_STATE, "checkpoint: between levels of a started, unfinished run");
@@ -1610,26 +1994,43 @@ struct rmc_ctx {
         HIPCHK(hipStreamSynchronize(stream));
         CkptHeader h = ckpt_header();
         h.depth = depth;
+        h.compact = s.Tc ? 1 : 0;
         h.total_generated = total_generated; h.total_distinct = total_distinct;
-        h.T_cap = s.T_cap; h.T_count = s.T_count; h.cur_n = s.cur_n;
+        h.T_cap = s.T_cap; h.T_count = s.T_count; h.cur_n = s.cur_n; h.cur_words = s.cur_words;
         h.n_levels = s.level_start.size();
         h.trace_n = s.level_start.back() + s.cur_n;  // every state found so far has a global id below
         h.epoch = s.epoch;
         h.seconds = seconds;
-        FILE *f = std::fopen(path, "wb");
-        if (!f) throw Fail(RMC_E_ARG, std::string("checkpoint: cannot write ") + path);
+        h.check = header_check(h);
+        if (s.tflushed != h.trace_n) throw Fail(RMC_E_STATE, "checkpoint: trace not flushed");
+        const std::string tmp = std::string(path) + ".tmp";
+        FILE *f = std::fopen(tmp.c_str(), "wb");
+        if (!f) throw Fail(RMC_E_ARG, std::string("checkpoint: cannot write ") + tmp);
         bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 &&
                   std::fwrite(s.level_start.data(), 8, s.level_start.size(), f) == s.level_start.size();
         auto out = [&](void *dev, char *host, size_t k) {
             HIPCHK(hipMemcpy(host, dev, k, hipMemcpyDeviceToHost));
             ok = ok && std::fwrite(host, 1, k, f) == k;
         };
-        stream_bytes(s.T, h.T_cap * 16, out);
-        stream_bytes(s.cur, h.cur_n * RECW * 4, out);
-        stream_bytes(s.par, h.trace_n * 8, out);
-        stream_bytes(s.pslot, h.trace_n * 2, out);
+        if (s.Tc) stream_bytes(s.Tc, h.T_cap * 8, out);
+        else stream_bytes(s.T, h.T_cap * 16, out);
+        // the current level, linearised
+        uint32_t *lin = dmalloc<uint32_t>(std::max<uint64_t>(h.cur_words, 1));
+        ring_copy_out(s, s.cur_wbase, h.cur_words, lin);
+        HIPCHK(hipStreamSynchronize(stream));
+        stream_bytes(lin, h.cur_words * 4, out);
+        dfree(lin);
+        stream_bytes(s.cur_off, h.cur_n * 8, out);
+        s.hpar.for_range(0, h.trace_n, [&](const uint64_t *p, uint64_t k) { ok = ok && std::fwrite(p, 8, k, f) == k; });
+        s.hslot.for_range(0, h.trace_n, [&](const uint16_t *p, uint64_t k) { ok = ok && std::fwrite(p, 2, k, f) == k; });
+        ok = std::fflush(f) == 0 && ok;
+        ok = ok && fsync(fileno(f)) == 0;
         ok = (std::fclose(f) == 0) && ok;
-        if (!ok) throw Fail(RMC_E_ARG, std::string("checkpoint: short write to ") + path);
+        if (!ok) {
+            std::remove(tmp.c_str());
+            throw Fail(RMC_E_ARG, std::string("checkpoint: short write to ") + tmp);
+        }
+        if (std::rename(tmp.c_str(), path) != 0) throw Fail(RMC_E_ARG, std::string("checkpoint: cannot rename to ") + path);
     }
 
     void resume(const char *path) {
@@ -1642,36 +2043,80 @@ struct rmc_ctx {
         bool ok = std::fread(&h, sizeof h, 1, f) == 1;
         if (!ok || h.magic != CKPT_MAGIC || h.abi != want.abi || h.recw != want.recw || h.n != want.n ||
             h.v != want.v || h.e != want.e || h.r != want.r || h.invariants != want.invariants ||
-            h.check_deadlock != want.check_deadlock || h.spec_variant != want.spec_variant ||
-            h.no_symmetry != want.no_symmetry || h.msg_cap != want.msg_cap || h.n_levels == 0 ||
-            (h.T_cap & (h.T_cap - 1)) != 0) {
+            h.inv_order != want.inv_order || h.check_deadlock != want.check_deadlock ||
+            h.spec_variant != want.spec_variant || h.no_symmetry != want.no_symmetry || h.msg_cap != want.msg_cap) {
             std::fclose(f);
             throw Fail(RMC_E_ARG, std::string("resume: ") + path + " is not a checkpoint of this configuration");
         }
-        Shard &s = sh[0];
+        if (h.scheme != want.scheme) {
+            std::fclose(f);
+            throw Fail(RMC_E_ARG, std::string("resume: ") + path + " was written with another fingerprint scheme");
+        }
+        // the header's own consistency, before anything is allocated from it
+        if (h.check != header_check(h) || h.n_levels == 0 || h.n_levels > 100000 || (h.T_cap & (h.T_cap - 1)) != 0 ||
+            h.T_count >= h.T_cap || h.T_count > h.trace_n || h.cur_words > h.cur_n * (uint64_t)RECW ||
+            h.cur_words < h.cur_n * (uint64_t)ks.CCW) {
+            std::fclose(f);
+            throw Fail(RMC_E_ARG, std::string("resume: ") + path + " has an inconsistent header");
+        }
         std::vector<uint64_t> ls(h.n_levels);
         ok = std::fread(ls.data(), 8, ls.size(), f) == ls.size();
-        if (s.T_cap != h.T_cap) {
-            dfree(s.T);
-            s.T = dmalloc<ulonglong2>(h.T_cap);
-            s.T_cap = h.T_cap;
+        for (size_t i = 1; ok && i < ls.size(); i++) ok = ls[i] > ls[i - 1];
+        if (!ok || ls.back() + h.cur_n != h.trace_n) {
+            std::fclose(f);
+            throw Fail(RMC_E_ARG, std::string("resume: ") + path + " has an inconsistent level table");
         }
-        grow_records(s.cur, s.cur_cap, 0, std::max<uint64_t>(h.cur_n, 1), RECW);
-        grow_trace(s, h.trace_n + 1);
+        Shard &s = sh[0];
+        dfree(s.T);
+        dfree(s.Tc);
+        if (h.compact) {
+            s.Tc = dmalloc<unsigned long long>(h.T_cap);
+            s.ring_fixed = false;  // re-derived below
+        } else {
+            s.T = dmalloc<ulonglong2>(h.T_cap);
+        }
+        s.T_cap = h.T_cap;
+        s.cur_wbase = 0;
+        s.cur_words = 0;
+        s.nxt_words = 0;
+        ensure_ring(s, h.cur_words + 1, 0);
+        ensure_off(s.cur_off, s.cur_off_cap, 0, std::max<uint64_t>(h.cur_n, 1));
         auto in = [&](void *dev, char *host, size_t k) {
             ok = ok && std::fread(host, 1, k, f) == k;
             if (ok) HIPCHK(hipMemcpy(dev, host, k, hipMemcpyHostToDevice));
         };
-        stream_bytes(s.T, h.T_cap * 16, in);
-        stream_bytes(s.cur, h.cur_n * RECW * 4, in);
-        stream_bytes(s.par, h.trace_n * 8, in);
-        stream_bytes(s.pslot, h.trace_n * 2, in);
+        if (s.Tc) stream_bytes(s.Tc, h.T_cap * 8, in);
+        else stream_bytes(s.T, h.T_cap * 16, in);
+        stream_bytes(s.R, h.cur_words * 4, in);
+        stream_bytes(s.cur_off, h.cur_n * 8, in);
+        s.hpar.reserve_to(h.trace_n);
+        s.hslot.reserve_to(h.trace_n);
+        for (uint64_t i = 0; ok && i < h.trace_n;) {
+            const uint64_t k = std::min<uint64_t>(h.trace_n - i, HostArr<uint64_t>::B - i % HostArr<uint64_t>::B);
+            ok = std::fread(s.hpar.blk[i / HostArr<uint64_t>::B].p + i % HostArr<uint64_t>::B, 8, k, f) == k;
+            i += k;
+        }
+        for (uint64_t i = 0; ok && i < h.trace_n;) {
+            const uint64_t k = std::min<uint64_t>(h.trace_n - i, HostArr<uint16_t>::B - i % HostArr<uint16_t>::B);
+            ok = std::fread(s.hslot.blk[i / HostArr<uint16_t>::B].p + i % HostArr<uint16_t>::B, 2, k, f) == k;
+            i += k;
+        }
         std::fclose(f);
         if (!ok) throw Fail(RMC_E_ARG, std::string("resume: ") + path + " is truncated");
+        s.hpar.n = s.hslot.n = h.trace_n;
+        s.tflushed = h.trace_n;
         s.level_start = ls;
         s.cur_n = h.cur_n;
+        s.cur_words = h.cur_words;
         s.T_count = h.T_count;
         s.epoch = std::max(s.epoch, h.epoch);
+        if (s.Tc) {  // a compact seen set means a large run: the ring goes to its budget
+            const uint64_t fb = cfg.frontier_mem_bytes ? cfg.frontier_mem_bytes
+                                                       : (uint64_t)((double)free_device_bytes() * 0.7);
+            const uint64_t words = std::max<uint64_t>(fb / 4, s.rcap);
+            if (words > s.rcap && !ring_realloc(s, words)) throw Fail(RMC_E_MEMORY, "frontier ring");
+            s.ring_fixed = true;
+        }
         total_generated = h.total_generated;
         total_distinct = h.total_distinct;
         depth = h.depth;
@@ -1686,11 +2131,17 @@ struct rmc_ctx {
         if (finished) { status = RMC_DONE; queue_at_end = 0; }
     }
 
+    // Forget every explored state but keep all device buffers (repeat runs, benchmarks).
     void reset() {
+        HIPCHK(hipStreamSynchronize(stream));
         for (Shard &s : sh) {
-            HIPCHK(hipMemsetAsync(s.T, 0, s.T_cap * 16, stream));
+            if (s.Tc) HIPCHK(hipMemsetAsync(s.Tc, 0, s.T_cap * 8, stream));
+            else HIPCHK(hipMemsetAsync(s.T, 0, s.T_cap * 16, stream));
             s.T_count = 0;
             s.cur_n = s.nxt_n = 0;
+            s.cur_wbase = s.cur_words = s.nxt_words = 0;
+            s.tflushed = 0;
+            s.hpar.n = s.hslot.n = 0;
             s.level_start.clear();
         }
         HIPCHK(hipStreamSynchronize(stream));
@@ -1717,6 +2168,12 @@ struct rmc_ctx {
         r->violated = violated;
         r->trace_len = (uint32_t)trace.size();
         r->seconds = seconds;
+        for (const Shard &s : sh) {
+            r->seen_slots += s.T_cap;
+            r->seen_slot_bytes = s.Tc ? 8 : 16;
+            r->frontier_ring_bytes += s.rcap * 4;
+            r->frontier_peak_bytes += s.peak_words * 4;
+        }
     }
 };
 
@@ -1747,7 +2204,7 @@ int rmc_comm_unique_id(void *out128) {
     ncclUniqueId id;
     if (ncclGetUniqueId(&id) != ncclSuccess) return RMC_E_COMM;
     static_assert(sizeof(id) <= 128, "ncclUniqueId larger than 128 bytes");
-    static_assert(sizeof(rmc_config) == 96, "rmc_config layout (ABI 2) changed: update INTEGRATION.md and raftmc");
+    static_assert(sizeof(rmc_config) == 120, "rmc_config layout (ABI 3) changed: update INTEGRATION.md and raftmc");
     std::memset(out128, 0, 128);
     std::memcpy(out128, &id, sizeof id);
     return RMC_OK;
@@ -1766,8 +2223,6 @@ int rmc_create(const rmc_config *cfg, void **out) {
         return RMC_OK;
     });
     if (rc != RMC_OK) {
-        static thread_local std::string last;
-        last = c->err;
         std::fprintf(stderr, "rmc_create: %s\n", c->err.c_str());
         c->release();
         delete c;

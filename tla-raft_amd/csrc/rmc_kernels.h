@@ -17,20 +17,32 @@ struct Tables {
     int np;
 };
 
+// Seen set (TLC's FPSet): open addressing over 128-bit fingerprints {x | 1, y}.
+//   full:    16-B slots {x, y} (T != nullptr), grown x4 by rehash while small;
+//   compact:  8-B slots holding x only (Tc != nullptr): the slot's probe run, which starts at the
+//             home index derived from y, carries the rest of the identity.  Used once the run is
+//             large (rmc_config.compact_log2); sized once from the memory budget, never grown.
+struct Seen {
+    ulonglong2 *T;
+    unsigned long long *Tc;
+    uint64_t mask;
+};
+
 enum ErrSlot { ERR_ASSERT = 0, ERR_DEADLOCK = 1, ERR_INV = 2, ERR_EVAL = 3, ERR_NSLOTS = 4 };
 
 // Device-driven level loop (single GPU): the host enqueues several BFS levels without
-// reading anything back.  Each level's kernels take their parent count, id bases,
-// election epoch and table size from this block, which the previous level's commit
-// wrote; once `stop` is set every later kernel returns at once.
+// reading anything back.  Each level's kernels take their parent count, id bases, election
+// epoch, table size and frontier ring positions from this block, which the previous level's
+// commit wrote; once `stop` is set every later kernel returns at once.
 enum CtlStop : uint32_t { CTL_RUN = 0, CTL_DONE = 1, CTL_ERROR = 2, CTL_HOST = 3 };
 struct LevelCtl {
     unsigned long long cur_n;    // parents of the level being expanded
     unsigned long long gid_cur;  // global id of its first state
     unsigned long long T_count;  // fingerprints in the seen set
     unsigned long long Lmask;    // election table mask for this level
+    unsigned long long cur_wbase, cur_words;  // ring position and words of the level being expanded
     // capacities (host-written before the batch)
-    unsigned long long nxt_cap, trace_cap, T_cap, chunk_parents, Lcap_max;
+    unsigned long long off_cap, rcap, trace_base, trace_cap, T_cap, chunk_parents, Lcap_max;
     uint32_t level;              // level being expanded (1 = Init's level)
     uint32_t epoch;              // election table epoch of this level
     uint32_t stop;               // CtlStop: RUN, DONE (empty level), ERROR, HOST (next level needs the host)
@@ -38,9 +50,10 @@ struct LevelCtl {
     uint32_t batch;              // levels the host enqueued: the loop hands back after that many
     uint32_t pad_;
 };
-struct LevelRec { unsigned long long expanded, generated, new_states; };
+struct LevelRec { unsigned long long expanded, generated, new_states, words; };
 constexpr int LREC_CAP = 1024;   // levels per batch at most
 constexpr uint32_t WTILE = 1024; // parents per tile of the winner-count scan (1024 tiles at most)
+constexpr int SUM_WORDS = 7;     // chunk summary slot of the new states' record words
 
 // In device-loop mode the host sizes every grid on a bound of the level's parents (p_end -
 // p_begin of the KParams it passes); the kernels read the real range from the LevelCtl.
@@ -50,9 +63,13 @@ struct KParams {
     Dims d;
     int E, R, seeded, check_deadlock;
     uint32_t inv_mask;
+    uint32_t inv_order;        // invariants in cfg order, 4 bits each (id + 1), 0 = end of list
     Tables t;
-    // current level
-    const uint32_t *front;     // records, RECW words each
+    // current level: records in the frontier ring, word k of parent p at
+    // front[ring_wrap(fbase + foff[p] + k, rcap)]; foff == nullptr: fixed stride RECW_MAX, no ring
+    const uint32_t *front;
+    const uint64_t *foff;
+    uint64_t fbase, rcap;
     uint64_t p_begin, p_end;   // parents of this chunk (level-local indices)
     // per parent (chunk-local: index p - p_begin)
     uint32_t *cnt;             // successor counts
@@ -61,42 +78,48 @@ struct KParams {
     ulonglong2 *fp;
     const uint32_t *wflag;     // 1 = winner (new, first in TLC order)
     uint32_t *wpos;            // exclusive scan of wflag (fused level: of wcnt inside a tile)
-    // seen set (open addressing, 16-B slots, lo word |= 1, 0 = empty)
-    ulonglong2 *T;
-    uint64_t Tmask;
-    // next level
-    uint32_t *next;            // records
+    Seen seen;
+    // next level: records in the same ring at nbase + noff[i]; noff holds level-relative offsets
+    uint32_t *next;            // ring (== front) or a fixed-stride buffer (noff == nullptr)
+    uint64_t *noff;
+    uint64_t nbase;            // ring position of the next level's first word
+    uint64_t next_wbase;       // level-relative word offset of this chunk's first winner
     uint64_t next_base;        // next-level index of this chunk's first winner
-    uint64_t *par;             // parent global id, indexed by global id
-    uint16_t *pslot;           // slot key, indexed by global id
+    // trace: parent global id + slot key, indexed by global id - trace_base
+    uint64_t *par;
+    uint16_t *pslot;
+    uint64_t trace_base;
     uint64_t gid_next_base;    // global id of next-level index 0
     uint64_t gid_parent_base;  // global id of level-local parent 0
     // errors: atomicMin keys (p << 16 | slot), level-local p
     unsigned long long *err;
     uint32_t *flags;           // [0] msg-cap overflow, [1] violated invariant bit, [2] eval-error invariant bit
-    // sharded mode: winners go to owner-grouped exchange records (RECW + 4 words each)
+    // sharded mode: winners go to owner-grouped exchange records (RECW_MAX + 4 words each)
     uint32_t *xrec;
     // fused single-shard level: expand (+hash, +seen-set probe, +election, +staging) -> wincount
-    // -> scan -> commit.  Successor slot q = (p - p_begin) * maxsucc + rank is sparse and
-    // increases in TLC order; it indexes fp, lslot, score (core words, CW/4 uint4 each) and
-    // saux {key | nadd << 16, add0 | add1 << 16, add2 | add3 << 16, 0}.  wpos is then the
-    // exclusive scan of wcnt (winners per parent) inside each WTILE-parent tile, and a
-    // parent's first winner lands at boff[tile] + wpos.
+    // -> commit.  Successor slot q = (p - p_begin) * maxsucc + rank is sparse and increases in
+    // TLC order; it indexes fp, lslot, score (packed core words, CCW4 uint4 each) and saux
+    // {key | nadd << 16, add0 | add1 << 16, add2 | add3 << 16, 0}.  wpos / wposw are then the
+    // exclusive scans of winners / their record words per parent inside each WTILE-parent tile,
+    // and a parent's first winner lands at boff[tile] + wpos (words boffw[tile] + wposw).
     uint4 *score;
     uint4 *saux;
     uint32_t *lslot;           // LS_SEEN, LS_ELECT, or the election slot in L
     unsigned long long *L;     // chunk election table: sharded path (epoch << 32) | q; fused path
-                               // the election word ((0xFFFFFFFF - epoch) << 32) | q (elect_key)
+                               // the election word ((0xFFFFFFFF - epoch) << 32) | q << 2 | e (elect_key)
     ulonglong2 *LXY;           // fused path: the fingerprint each election slot holds, both words
                                // tagged with the chunk's 16-bit tag (elect_tag) in their low bits
     uint64_t Lmask;
     uint32_t epoch;
     uint32_t *wcnt;            // winners per parent (chunk-local)
-    uint32_t *wacc;            // winners per parent as the election counts them (0 between chunks)
+    uint32_t *wacc;            // per parent, as the election counts them: winners | extra words << 12
+    uint32_t *pnm;             // |msgs| per parent (chunk-local)
+    uint32_t *wposw;           // record words of the parent's winners, exclusive scan inside the tile
     uint32_t *bw, *bg, *boff;  // per tile: winners, successors generated, first winner's offset
+    uint32_t *bww, *boffw;     // per tile: winners' record words, first winner's word offset
     uint32_t *tickets;         // [0] winner-count pass: last-block counter (0 between launches)
     uint32_t *ctick;           // commit pass: arrival counters (last_commit_block; 0 between launches)
-    unsigned long long *sum;   // chunk summary {generated, winners, error keys[ERR_NSLOTS], flags}
+    unsigned long long *sum;   // chunk summary {generated, winners, error keys[ERR_NSLOTS], flags, words}
     LevelCtl *ctl;             // device-driven level loop (nullptr: the host drives the chunk)
     LevelRec *lrec;            // statistics of each level the device loop commits
     // single-state hook outputs
@@ -105,7 +128,7 @@ struct KParams {
 };
 
 struct KernelSet {
-    int N, V, MR, MCAP, CW, RECW, maxsucc;
+    int N, V, MR, MCAP, CCW, RECW_MAX, maxsucc;
     void (*count)(const KParams &, hipStream_t);
     void (*hash)(const KParams &, hipStream_t);
     void (*materialize)(const KParams &, hipStream_t);
@@ -116,35 +139,35 @@ struct KernelSet {
                                                             // chunk summary (and the device loop's next level)
     void (*fp_states)(const KParams &, uint64_t n, hipStream_t);  // fp of front[0..n) -> fp
     void (*inv_states)(const KParams &, uint64_t n, int32_t *out, hipStream_t); // per state: 1/0/-1 for inv_mask bits
+    // host codec of the packed core (rmc_spec.h Codec)
+    void (*encode)(const uint32_t *nibble_core, uint32_t *packed);
+    void (*decode)(const uint32_t *packed, uint32_t *nibble_core);
 };
 
 // returns false if (N, V) has no compiled instantiation
 bool get_kernels(int N, int V, int msg_cap, KernelSet *ks);
 
 // generic (template-free) kernels
-void launch_dedup(const ulonglong2 *fp, const uint32_t *Gp, uint64_t Gub, const ulonglong2 *T, uint64_t Tmask,
+void launch_dedup(const ulonglong2 *fp, const uint32_t *Gp, uint64_t Gub, Seen seen,
                   unsigned long long *L, uint64_t Lmask, uint32_t epoch, uint32_t *lslot, hipStream_t s);
-void launch_winflag(const uint32_t *lslot, const unsigned long long *L, const uint32_t *Gp, uint64_t Gub,
-                    uint32_t *wflag, hipStream_t s);
-void launch_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned long long *err, const uint32_t *flags,
-                    unsigned long long *out, hipStream_t s);
 constexpr uint32_t LS_SEEN = 0xFFFFFFFFu, LS_ELECT = 0xFFFFFFFEu;
-void launch_scan_small(const uint32_t *in, uint64_t n, uint32_t *out, hipStream_t s);
-void launch_winscan_small(const uint32_t *lslot, const unsigned long long *L, const uint32_t *Gp, uint64_t Gub,
-                          uint32_t *wflag, uint32_t *wpos, hipStream_t s);
 void launch_owner_keys(const ulonglong2 *fp, uint64_t G, uint32_t W, uint32_t *key, uint32_t *iota,
                        unsigned long long *cnt, hipStream_t s);
 void launch_gather_fp(const ulonglong2 *fp, const uint32_t *perm, uint64_t G, ulonglong2 *out, hipStream_t s);
 void launch_recv_flags(const uint32_t *lslot, const unsigned long long *L, uint64_t R, uint32_t *flag, hipStream_t s);
 void launch_scatter_flags(const uint32_t *perm, const uint32_t *sflag, const uint32_t *spos, uint64_t G,
                           uint32_t *wflag, uint32_t *wpos, hipStream_t s);
-void launch_accept(const uint32_t *xrec, uint64_t n, uint32_t recw, uint32_t *next, uint64_t *par, uint16_t *pslot,
-                   uint64_t src_tag, hipStream_t s);
-void launch_insert_flagged(const ulonglong2 *fp, const uint32_t *flag, uint64_t n, ulonglong2 *T, uint64_t mask,
-                           hipStream_t s);
+// owner side: n exchange records (recw + 4 words each) -> the next level at ring position nbase,
+// level-relative word offsets rel0 + q * recw (noff), trace entries (par / pslot already offset)
+void launch_accept(const uint32_t *xrec, uint64_t n, uint32_t recw, uint32_t *ring, uint64_t rcap, uint64_t nbase,
+                   uint64_t rel0, uint64_t *noff, uint64_t *par, uint16_t *pslot, uint64_t src_tag, hipStream_t s);
+void launch_insert_flagged(const ulonglong2 *fp, const uint32_t *flag, uint64_t n, Seen seen, hipStream_t s);
 void launch_pick(const uint32_t *a, const uint64_t *idx, int n, unsigned long long *out, hipStream_t s);
 void launch_owner_of(const ulonglong2 *fp, uint32_t W, uint32_t *out, hipStream_t s);
-void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, ulonglong2 *Tnew, uint64_t new_mask, hipStream_t s);
-void launch_insert_fps(const ulonglong2 *fp, uint64_t n, ulonglong2 *T, uint64_t Tmask, hipStream_t s);
+// full-slot table -> (full or compact) table
+void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, Seen dst, hipStream_t s);
+void launch_insert_fps(const ulonglong2 *fp, uint64_t n, Seen seen, hipStream_t s);
+// out[i] = in[i] - sub (offset arrays rebased to a new level start)
+void launch_rebase(const uint64_t *in, uint64_t n, uint64_t sub, uint64_t *out, hipStream_t s);
 
 }  // namespace rmc

@@ -11,12 +11,17 @@
 // evaluated per lane; a ballot + in-wave rank by slot key puts the successors in
 // TLC's enumeration order (Next, tla:416-430) without any sort.
 //
+// Frontier records live in a ring of 32-bit words: packed core (rmc_spec.h Codec) + the
+// sorted u16 message ids, CCW + ceil(|msgs|/2) words each, located by a level-relative
+// word offset per state.
+//
 // Modes of the same expansion:
 //   COUNT        successors per parent (+ Assert tla:185 / deadlock detection)
 //   HASH         symmetry+view fingerprint of every successor -> fp[off[p] + rank]
-//   MATERIALIZE  winners (new states, first in TLC order) -> next frontier records,
-//                seen-set insert, parent pointers, INVARIANT check (Raft.cfg:33)
+//   MATERIALIZE  winners (new states, first in TLC order) -> owner exchange records,
+//                INVARIANT check (Raft.cfg:33)
 //   SINGLE       every successor of one state -> records (parity-test hook)
+//   FUSED        single-GPU level: expand + fingerprint + seen-set probe + election + staging
 #include <hip/hip_runtime.h>
 
 #include "rmc_kernels.h"
@@ -40,10 +45,22 @@ __device__ __forceinline__ uint64_t rdlane64(uint64_t v, int l) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// exclusive prefix sum over the wave's lanes
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane, uint32_t *total) {
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    *total = __shfl(x, 63, 64);
+    return x - v;
+}
+
 // ---- device-driven level loop -------------------------------------------------------------
-// With P.ctl set, a level's kernels take the parent range, id bases, election epoch and
-// table size from the control block the previous level's commit wrote (a kernel boundary
-// makes it visible); once the loop has stopped every block returns at once.
+// With P.ctl set, a level's kernels take the parent range, id bases, ring positions, election
+// epoch and table size from the control block the previous level's commit wrote (a kernel
+// boundary makes it visible); once the loop has stopped every block returns at once.
 __device__ __forceinline__ bool level_args(KParams &P) {
     if (!P.ctl) return true;
     const LevelCtl *c = P.ctl;
@@ -53,6 +70,9 @@ __device__ __forceinline__ bool level_args(KParams &P) {
     P.gid_parent_base = c->gid_cur;
     P.gid_next_base = c->gid_cur + c->cur_n;
     P.next_base = 0;
+    P.next_wbase = 0;
+    P.fbase = c->cur_wbase;
+    P.nbase = ring_wrap(c->cur_wbase + c->cur_words, P.rcap);
     P.epoch = c->epoch;
     P.Lmask = c->Lmask;
     return true;
@@ -62,13 +82,16 @@ template <int N, int V, int MR>
 struct Spec {
     using L = Layout<N, V>;
     static constexpr int NW = L::NW, CW = L::CW;
+    static constexpr int CCW = Codec<N, V>::CCW;               // packed core words
     static constexpr int MCAP = 64 * MR;
-    static constexpr int RECW = CW + MCAP / 2;
+    static constexpr int RECW_MAX = CCW + MCAP / 2;            // longest record
     static constexpr int NADD = (N > 1) ? N - 1 : 1;
     static constexpr int SLOTS_PER_SERVER = 4 + V + (N - 1);  // BC BL CR*V LAE*(N-1) LCC RS
     static_assert(N * SLOTS_PER_SERVER <= 64, "non-message slots must fit one wave");
     static constexpr int MAXS = MCAP + N * SLOTS_PER_SERVER;  // successor slots per parent (sparse stride)
-    static constexpr int CW4 = CW / 4;                         // core words as uint4
+    // staging of one successor (uint4s): its acting server's row -- the only part of the state an
+    // action changes (see stage_succ) -- plus slot key, |added| and the added message ids
+    static constexpr int SW4 = NADD > 2 ? 3 : 2;
 };
 
 // per-lane successor candidate
@@ -127,6 +150,24 @@ __device__ __forceinline__ uint32_t median_row(uint32_t row, uint32_t k) {
     return best;
 }
 
+// ---- frontier ring access ---------------------------------------------------------------------
+// First word of parent p's record: a level-relative offset into the ring, or a fixed stride.
+template <int RECW_MAX>
+__device__ __forceinline__ uint64_t rec_start(const KParams &P, uint64_t p) {
+    return P.foff ? ring_wrap(P.fbase + P.foff[p], P.rcap) : p * (uint64_t)RECW_MAX;
+}
+__device__ __forceinline__ uint32_t ring_word(const uint32_t *ring, uint64_t start, uint32_t k, uint64_t rcap) {
+    return ring[ring_wrap(start + k, rcap)];
+}
+// message id k of a record whose ids begin at word `start`
+__device__ __forceinline__ uint32_t ring_id(const uint32_t *ring, uint64_t start, uint32_t k, uint64_t rcap) {
+    return (ring_word(ring, start, k >> 1, rcap) >> ((k & 1u) * 16u)) & 0xFFFFu;
+}
+__device__ __forceinline__ void ring_put_id(uint32_t *ring, uint64_t start, uint32_t k, uint64_t rcap, uint32_t id) {
+    const uint64_t w = ring_wrap(start + (k >> 1), rcap);
+    reinterpret_cast<uint16_t *>(ring)[2 * w + (k & 1u)] = (uint16_t)id;
+}
+
 // ---- invariants (on a concrete state; TLC's left-to-right short-circuit) ---------------
 // returns 1 TRUE, 0 FALSE, -1 evaluation error
 template <int N, int V>
@@ -158,18 +199,19 @@ __device__ __forceinline__ int inv_lhace(const uint32_t *c) {  // LeaderHasAllCo
     return 0;
 }
 
-// The message set of the state an invariant is checked on: msgs only grow (SendMsg, tla:77-78),
+// The message set of the state an invariant is checked on: msgs only grow (SendMsg, tla:43-45),
 // so a successor's set is its parent's sorted id list plus the ids its action added.
 struct MsgView {
-    const uint16_t *ids;  // parent's ids in HBM (record word CW on)
+    const uint32_t *ring;  // parent's ids: ring words from `start` on
+    uint64_t start, rcap;
     uint32_t nm;
-    uint32_t add0, add1;  // added ids, two u16 each (saux layout)
+    uint32_t add0, add1;   // added ids, two u16 each (staging layout)
     uint32_t nadd;
-    const uint32_t *info; // message info word by id
+    const uint32_t *info;  // message info word by id
 };
 
 __device__ __forceinline__ uint32_t mv_id(const MsgView &mv, uint32_t k) {
-    if (k < mv.nm) return mv.ids[k];
+    if (k < mv.nm) return ring_id(mv.ring, mv.start, k, mv.rcap);
     k -= mv.nm;
     const uint32_t w = k < 2 ? mv.add0 : mv.add1;
     return (k & 1u) ? (w >> 16) : (w & 0xFFFFu);
@@ -252,12 +294,14 @@ __device__ __forceinline__ int inv_eval(const uint32_t *c, int id, const MsgView
     }
 }
 
-// all selected invariants in bit order; returns 1 ok, 0 violated, -1 eval error; *which = bit
+// The selected invariants in the order the cfg lists them (TLC checks them in that order,
+// Raft.cfg:33-34): P.inv_order holds id + 1 per nibble, first invariant in the low nibble.
+// Returns 1 ok, 0 violated, -1 eval error; *which = the invariant's id (bit).
 template <int N, int V>
-__device__ __forceinline__ int check_invs(const uint32_t *c, uint32_t mask, int *which, const MsgView &mv) {
-    for (int i = 0; i < 7; i++) {
-        if (!(mask & (1u << i))) continue;
-        int r = inv_eval<N, V>(c, i, mv);
+__device__ __forceinline__ int check_invs(const uint32_t *c, uint32_t order, int *which, const MsgView &mv) {
+    for (; order; order >>= 4) {
+        const int i = (int)(order & 15u) - 1;
+        const int r = inv_eval<N, V>(c, i, mv);
         if (r != 1) { *which = i; return r; }
     }
     return 1;
@@ -340,6 +384,7 @@ struct Wave {
     uint32_t c[S::NW];   // parent core (wave-uniform), constant-index reads
     const uint32_t *lds; // same core in LDS [NW] + vpcnt [N]: runtime-indexed reads
     uint32_t nm;
+    uint64_t idw;        // ring position of the parent's first message-id word
     uint32_t id[MR];     // message id owned by this lane per round (0xFFFF = none)
     uint32_t inf[MR];
 };
@@ -587,27 +632,41 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
     }
 }
 
+// Read a packed core (wave-uniform) at ring position `start` and decode it to the nibble layout.
+template <int N, int V>
+__device__ __forceinline__ void load_core(const uint32_t *ring, uint64_t start, uint64_t rcap, int lane, uint32_t *c,
+                                          uint32_t *packed) {
+    constexpr int CCW = Codec<N, V>::CCW;
+    const uint32_t mine = lane < CCW ? ring_word(ring, start, (uint32_t)lane, rcap) : 0u;
+#pragma unroll
+    for (int k = 0; k < CCW; k++) packed[k] = rdlane(mine, k);
+    decode_core<N, V>(packed, c);
+}
+
 // Load a state record into the wave: uniform core, per-lane message ids, LDS copy of
 // the sorted ids and the per-(src,dst) message hash sums.
 template <int N, int V, int MR, bool SUMS>
-__device__ __forceinline__ void load_parent(const KParams &P, const uint32_t *rec, int lane, Wave<N, V, MR> &W, uint16_t *ids,
+__device__ __forceinline__ void load_parent(const KParams &P, uint64_t start, int lane, Wave<N, V, MR> &W, uint16_t *ids,
                             uint64_t *M0, uint64_t *M1, uint32_t *pcore) {
     using Lo = Layout<N, V>;
     using S = Spec<N, V, MR>;
+    uint32_t packed[S::CCW];
+    load_core<N, V>(P.front, start, P.rcap, lane, W.c, packed);
+    if (lane == 0) {  // uniform values: one lane writes the LDS copy (no runtime-indexed register array)
 #pragma unroll
-    for (int w = 0; w < Lo::NW; w++) W.c[w] = rec[w];
-    if (lane < Lo::NW) pcore[lane] = rec[lane];
+        for (int w = 0; w < Lo::NW; w++) pcore[w] = W.c[w];
+    }
     W.lds = pcore;
     W.nm = (W.c[Lo::W_MISC] >> 16) & 0xFFu;
+    W.idw = ring_wrap(start + S::CCW, P.rcap);
     if (SUMS && lane < N * N) { M0[lane] = 0; M1[lane] = 0; }
     __syncthreads();
-    const uint16_t *rid = reinterpret_cast<const uint16_t *>(rec + S::CW);
 #pragma unroll
     for (int r = 0; r < MR; r++) {
         const uint32_t k = (uint32_t)(r * 64 + lane);
         uint32_t id = 0xFFFFu, inf = 0;
         if (k < W.nm) {
-            id = rid[k];
+            id = ring_id(P.front, W.idw, k, P.rcap);
             inf = P.t.info[id];
             if (SUMS) {
                 const ulonglong2 g = P.t.gmsg[id];
@@ -658,33 +717,20 @@ __device__ __forceinline__ void succ_row(const Succ<N, V, MR> &o, const uint64_t
     }
 }
 
-// Write the successor held by lane t (round r) as a record at rec_out (whole wave).
+// Merge the parent's sorted ids (per lane: id[r] = id r*64+lane, 0xFFFF past nm) with a
+// successor's added ids into a record's id list at ring position `idw` (whole wave).
 template <int N, int V, int MR>
-__device__ __forceinline__ void write_record(const Wave<N, V, MR> &W, const Succ<N, V, MR> &o, int t, int lane, uint32_t *rec_out) {
-    using Lo = Layout<N, V>;
+__device__ __forceinline__ void write_ids(uint32_t *ring, uint64_t idw, uint64_t rcap, const uint32_t *id, uint32_t nm,
+                                          const uint32_t *add, uint32_t nadd, int lane) {
     using S = Spec<N, V, MR>;
-    const uint32_t nadd = rdlane(o.nadd, t);
-    uint32_t add[S::NADD];
-#pragma unroll
-    for (int a = 0; a < S::NADD; a++) add[a] = rdlane(o.add[a], t);
-    uint32_t v = 0;
-#pragma unroll
-    for (int w = 0; w < Lo::NW; w++) {
-        uint32_t x = rdlane(o.c[w], t);
-        if (w == Lo::W_MISC) x = (x & ~0xFF0000u) | ((W.nm + nadd) << 16);
-        v = (lane == w) ? x : v;
-    }
-    if (lane < S::CW) rec_out[lane] = v;
-    uint16_t *oid = reinterpret_cast<uint16_t *>(rec_out + S::CW);
 #pragma unroll
     for (int r = 0; r < MR; r++) {
         const uint32_t k = (uint32_t)(r * 64 + lane);
-        if (k < W.nm) {
-            const uint32_t id = W.id[r];
+        if (k < nm) {
             uint32_t pos = k;
 #pragma unroll
-            for (int a = 0; a < S::NADD; a++) pos += ((uint32_t)a < nadd && add[a] < id) ? 1u : 0u;
-            oid[pos] = (uint16_t)id;
+            for (int a = 0; a < S::NADD; a++) pos += ((uint32_t)a < nadd && add[a] < id[r]) ? 1u : 0u;
+            ring_put_id(ring, idw, pos, rcap, id[r]);
         }
     }
 #pragma unroll
@@ -693,24 +739,68 @@ __device__ __forceinline__ void write_record(const Wave<N, V, MR> &W, const Succ
         uint32_t less = 0;
 #pragma unroll
         for (int r = 0; r < MR; r++)
-            less += (uint32_t)__popcll(__ballot((uint32_t)(r * 64 + lane) < W.nm && W.id[r] < add[a]));
+            less += (uint32_t)__popcll(__ballot((uint32_t)(r * 64 + lane) < nm && id[r] < add[a]));
 #pragma unroll
         for (int b = 0; b < S::NADD; b++) less += ((uint32_t)b < nadd && add[b] < add[a]) ? 1u : 0u;
-        if (lane == 0) oid[less] = (uint16_t)add[a];
+        if (lane == 0) ring_put_id(ring, idw, less, rcap, add[a]);
     }
+    if (lane == 0 && ((nm + nadd) & 1u)) ring_put_id(ring, idw, nm + nadd, rcap, 0u);  // pad half-word
 }
 
+// Write the successor held by lane t (round r) as a fixed-stride record at rec_out (whole wave).
+template <int N, int V, int MR>
+__device__ __forceinline__ void write_record(const Wave<N, V, MR> &W, const Succ<N, V, MR> &o, int t, int lane, uint32_t *rec_out) {
+    using Lo = Layout<N, V>;
+    using S = Spec<N, V, MR>;
+    const uint32_t nadd = rdlane(o.nadd, t);
+    uint32_t add[S::NADD];
+#pragma unroll
+    for (int a = 0; a < S::NADD; a++) add[a] = rdlane(o.add[a], t);
+    uint32_t c[Lo::NW], packed[S::CCW];
+#pragma unroll
+    for (int w = 0; w < Lo::NW; w++) c[w] = rdlane(o.c[w], t);
+    c[Lo::W_MISC] = (c[Lo::W_MISC] & ~0xFF0000u) | ((W.nm + nadd) << 16);
+    encode_core<N, V>(c, packed);
+    if (lane < S::CCW) rec_out[lane] = sel<S::CCW>(packed, lane);
+    write_ids<N, V, MR>(rec_out, S::CCW, ~0ull, W.id, W.nm, add, nadd, lane);
+}
+
+// ---- seen set -----------------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t t_index(const ulonglong2 f, uint64_t mask) {
     return (f.y ^ (f.y >> 29) ^ (f.x >> 23)) & mask;
 }
 
-__device__ __forceinline__ bool t_contains(const ulonglong2 *T, uint64_t mask, ulonglong2 f) {
-    uint64_t h = t_index(f, mask);
+__device__ __forceinline__ bool seen_contains(const Seen &S, ulonglong2 f) {
+    uint64_t h = t_index(f, S.mask);
+    if (S.Tc) {
+        for (;;) {
+            const unsigned long long e = S.Tc[h];
+            if (e == 0ull) return false;
+            if (e == f.x) return true;
+            h = (h + 1) & S.mask;
+        }
+    }
     for (;;) {
-        const ulonglong2 e = T[h];
+        const ulonglong2 e = S.T[h];
         if (e.x == 0ull) return false;
         if (e.x == f.x && e.y == f.y) return true;
-        h = (h + 1) & mask;
+        h = (h + 1) & S.mask;
+    }
+}
+
+// keys inserted are never already present (winners are new, rehash moves distinct keys)
+__device__ __forceinline__ void seen_insert(const Seen &S, ulonglong2 f) {
+    uint64_t h = t_index(f, S.mask);
+    if (S.Tc) {
+        for (;;) {
+            if (atomicCAS(&S.Tc[h], 0ull, (unsigned long long)f.x) == 0ull) return;
+            h = (h + 1) & S.mask;
+        }
+    }
+    for (;;) {
+        unsigned long long prev = atomicCAS((unsigned long long *)&S.T[h].x, 0ull, (unsigned long long)f.x);
+        if (prev == 0ull) { S.T[h].y = f.y; return; }
+        h = (h + 1) & S.mask;
     }
 }
 
@@ -722,23 +812,26 @@ __device__ __forceinline__ uint64_t l_index(const ulonglong2 f, uint64_t mask) {
 // The first successor in TLC order (smallest slot q) per new fingerprint wins.  Election slot g
 // holds the fingerprint in LXY[g] -- both words carry the chunk's 16-bit tag in their low bits,
 // so slots of earlier chunks read as free and the table is never cleared (the host clears it
-// once every 65535 epochs) -- and the election word L[g] = elect_key(epoch, smallest q).  The
-// word of a newer epoch is smaller than any older one (and than the all-ones initial value), so
-// every candidate just takes the minimum.  All accesses are agent-scope atomics on the slot's
+// once every 65535 epochs) -- and the election word L[g] = elect_key(epoch, smallest q, its e).
+// The word of a newer epoch is smaller than any older one (and than the all-ones initial value),
+// so every candidate just takes the minimum.  All accesses are agent-scope atomics on the slot's
 // own words: a claimer CASes x then stores y; a candidate that finds x equal but y not yet
 // tagged retries the same slot on its next iteration (never spinning in place, so a claimer
 // in the same wave always gets to its store).
 __device__ __forceinline__ uint32_t elect_tag(uint32_t epoch) { return epoch % 0xFFFFu + 1u; }
-__device__ __forceinline__ unsigned long long elect_key(uint32_t epoch, uint64_t q) {
-    return ((unsigned long long)(0xFFFFFFFFu - epoch) << 32) | (unsigned long long)(uint32_t)q;
+// e = the record words a winner adds beyond CCW + floor(|parent msgs| / 2): ceil((nadd + (nm & 1)) / 2)
+__device__ __forceinline__ unsigned long long elect_key(uint32_t epoch, uint64_t q, uint32_t e) {
+    return ((unsigned long long)(0xFFFFFFFFu - epoch) << 32) | ((unsigned long long)(uint32_t)q << 2) | e;
 }
+__device__ __forceinline__ uint32_t elect_q(unsigned long long w) { return (uint32_t)w >> 2; }
 
-// The candidate that becomes a slot's minimum adds one to its parent's winner count (wacc) and
-// takes one off the parent of the candidate it displaced (the old minimum the atomic returns), so
-// once the launch is done wacc holds winners per parent.
+// The candidate that becomes a slot's minimum adds one winner (and its e extra words) to its
+// parent's packed count wacc = winners | extra << 12, and takes the displaced candidate's (the old
+// minimum the atomic returns) off its parent: once the launch is done, wacc per parent is exact
+// (the packed sum of adds and subtracts is exact mod 2^32 whatever their order).
 template <int MAXS>
 __device__ __forceinline__ uint32_t elect_slot(ulonglong2 *LXY, unsigned long long *L, uint32_t *wacc, uint64_t mask,
-                                               uint32_t epoch, const ulonglong2 f, uint64_t q, uint64_t g,
+                                               uint32_t epoch, const ulonglong2 f, uint64_t q, uint32_t e, uint64_t g,
                                                unsigned long long v) {
     // g = l_index(f, mask) and v = its x word, loaded by the caller together with the seen-set probe
     const unsigned long long tag = elect_tag(epoch);
@@ -765,22 +858,56 @@ __device__ __forceinline__ uint32_t elect_slot(ulonglong2 *LXY, unsigned long lo
         g = (g + 1) & mask;
         v = __hip_atomic_load(&LXY[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const unsigned long long mine = elect_key(epoch, q);
+    const unsigned long long mine = elect_key(epoch, q, e);
     const unsigned long long old = atomicMin(&L[g], mine);
     if (old > mine) {
-        atomicAdd(&wacc[q / MAXS], 1u);
-        if ((old >> 32) == (mine >> 32)) atomicSub(&wacc[(uint32_t)old / MAXS], 1u);
+        atomicAdd(&wacc[q / MAXS], 1u + (e << 12));
+        if ((old >> 32) == (mine >> 32)) atomicSub(&wacc[elect_q(old) / MAXS], 1u + ((uint32_t)(old & 3u) << 12));
     }
     return (uint32_t)g;
 }
 
-__device__ __forceinline__ void t_insert(ulonglong2 *T, uint64_t mask, ulonglong2 f) {
-    uint64_t h = t_index(f, mask);
-    for (;;) {
-        unsigned long long prev = atomicCAS((unsigned long long *)&T[h].x, 0ull, (unsigned long long)f.x);
-        if (prev == 0ull) { T[h].y = f.y; return; }
-        h = (h + 1) & mask;
+// Staging of one successor: the acting server's row and the words an action may change
+// (tla:107-414: every action assigns only votedFor[s], currentTerm[s], role[s], commitIndex[s],
+// logs[s], matchIndex[s], nextIndex[s], pendingResponse, the aux counters and msgs):
+//   w0 = votedFor[s] | currentTerm[s] << 4 | role[s] << 8 | commitIndex[s] << 12 | Len(logs[s]) << 16 | s << 20
+//   w1 = logs[s] word  w2 = matchIndex[s] row  w3 = nextIndex[s] row  w4 = pendingResponse  w5 = misc (|msgs| set)
+//   w6 = key | nadd << 16  w7 = add0 | add1 << 16  [w8 = add2 | add3 << 16]
+template <int N, int V, int MR>
+__device__ __forceinline__ void stage_succ(const Succ<N, V, MR> &o, uint32_t nm, uint4 *dst) {
+    using Lo = Layout<N, V>;
+    using S = Spec<N, V, MR>;
+    const uint32_t s = o.s;
+    const uint32_t w0 = nib(o.c[Lo::W_VF], s) | (nib(o.c[Lo::W_CT], s) << 4) | (nib(o.c[Lo::W_ROLE], s) << 8) |
+                        (nib(o.c[Lo::W_CI], s) << 12) | (nib(o.c[Lo::W_LL], s) << 16) | (s << 20);
+    const uint32_t w5 = (o.c[Lo::W_MISC] & ~0xFF0000u) | ((nm + o.nadd) << 16);
+    uint32_t a01, a23;
+    succ_adds(o, &a01, &a23);
+    dst[0] = make_uint4(w0, o.lw, o.mirow, o.nirow);
+    dst[1] = make_uint4(o.c[Lo::W_PEND], w5, o.key | (o.nadd << 16), a01);
+    if (S::SW4 > 2) dst[2] = make_uint4(a23, 0u, 0u, 0u);
+}
+
+// parent nibble core pc + staged row -> the successor's nibble core c
+template <int N, int V>
+__device__ __forceinline__ void unstage_core(const uint32_t *pc, const uint4 a, const uint4 b, uint32_t *c) {
+    using Lo = Layout<N, V>;
+#pragma unroll
+    for (int w = 0; w < Lo::NW; w++) c[w] = pc[w];
+    const uint32_t s = a.x >> 20;
+    c[Lo::W_VF] = setnib(c[Lo::W_VF], s, a.x & 15u);
+    c[Lo::W_CT] = setnib(c[Lo::W_CT], s, (a.x >> 4) & 15u);
+    c[Lo::W_ROLE] = setnib(c[Lo::W_ROLE], s, (a.x >> 8) & 15u);
+    c[Lo::W_CI] = setnib(c[Lo::W_CI], s, (a.x >> 12) & 15u);
+    c[Lo::W_LL] = setnib(c[Lo::W_LL], s, (a.x >> 16) & 15u);
+#pragma unroll
+    for (int q = 0; q < N; q++) {
+        c[Lo::W_LOG + q] = ((uint32_t)q == s) ? a.y : c[Lo::W_LOG + q];
+        c[Lo::W_MI + q] = ((uint32_t)q == s) ? a.z : c[Lo::W_MI + q];
+        c[Lo::W_NI + q] = ((uint32_t)q == s) ? a.w : c[Lo::W_NI + q];
     }
+    c[Lo::W_PEND] = b.x;
+    c[Lo::W_MISC] = b.y;
 }
 
 template <int N, int V, int MR, int MODE>
@@ -798,7 +925,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
     __shared__ uint64_t sdS[2][N], sdP[2][N * N];       // position seeds
     __shared__ uint8_t pimg[NPM * N];                   // permutation images
     __shared__ uint64_t sU[MAXS], sX[2][MAXS * N];      // compacted successor rows
-    __shared__ uint32_t sS[MAXS];
+    __shared__ uint8_t sS[MAXS], sNa[MAXS];             // acting server, |added ids| per successor
     __shared__ uint32_t sAinf[(MR + 1) * 64 * S::NADD];  // info words of the messages each candidate adds
     if (MODE == M_FUSED && !level_args(P)) return;
     // device-loop grids are sized on a bound of the level: blocks past it leave before the LDS setup
@@ -817,9 +944,8 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
         }
     }
     for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
-        const uint32_t *rec = P.front + p * (uint64_t)S::RECW;
         Wave<N, V, MR> W;
-        load_parent<N, V, MR, SUMS>(P, rec, lane, W, ids, M0, M1, pcore);
+        load_parent<N, V, MR, SUMS>(P, rec_start<S::RECW_MAX>(P, p), lane, W, ids, M0, M1, pcore);
         Succ<N, V, MR> cand[MR + 1];
         uint32_t akey = KEY_NONE;
 #pragma unroll
@@ -866,31 +992,19 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
         if (MODE == M_COUNT || MODE == M_FUSED) {
             if (lane == 0) {
                 P.cnt[pl] = total;
+                if (MODE == M_FUSED) P.pnm[pl] = W.nm;
                 if (total == 0 && !am && P.check_deadlock) atomicMin(&P.err[ERR_DEADLOCK], ((unsigned long long)p << 16) << 8);
             }
             if (MODE == M_COUNT) continue;
         }
         if (MODE == M_FUSED) {
-            // stage every enabled successor at its slot q: core words (|msgs| already updated)
-            // and the message ids it adds -- commit merges them into the parent's id list
+            // stage every enabled successor at its slot q: the acting row and the added message ids
+            // -- commit rebuilds the state from the parent's core and merges the ids
 #pragma unroll
             for (int r = 0; r <= MR; r++) {
                 if (cand[r].key == KEY_NONE) continue;
-                const Succ<N, V, MR> &o = cand[r];
                 const uint64_t q = pl * (uint64_t)S::MAXS + rank[r];
-                uint32_t cw[S::CW];
-#pragma unroll
-                for (int w = 0; w < S::CW; w++) {
-                    if (w < Lo::NW) cw[w] = o.c[w]; else cw[w] = 0u;
-                }
-                cw[Lo::W_MISC] = (cw[Lo::W_MISC] & ~0xFF0000u) | ((W.nm + o.nadd) << 16);
-                uint4 *dst = P.score + q * (uint64_t)S::CW4;
-#pragma unroll
-                for (int k = 0; k < S::CW4; k++) dst[k] = make_uint4(cw[4 * k], cw[4 * k + 1], cw[4 * k + 2], cw[4 * k + 3]);
-                uint32_t a[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-                for (int k = 0; k < S::NADD; k++) a[k] = o.add[k];
-                P.saux[q] = make_uint4(o.key | (o.nadd << 16), a[0] | (a[1] << 16), a[2] | (a[3] << 16), 0u);
+                stage_succ<N, V, MR>(cand[r], W.nm, P.score + q * (uint64_t)S::SW4);
             }
         }
         if (SUMS) {
@@ -934,7 +1048,8 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
                     sX[0][sl * N + j] = row0[j] ^ (sm * PAIR_K0);
                     sX[1][sl * N + j] = row1[j] ^ (sm * PAIR_K1);
                 }
-                sS[sl] = o.s;
+                sS[sl] = (uint8_t)o.s;
+                sNa[sl] = (uint8_t)o.nadd;
             }
             __syncthreads();
             for (int pp = lane; pp < np; pp += 64) {
@@ -1062,9 +1177,10 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
                         const uint64_t g0 = l_index(f, P.Lmask);
                         const unsigned long long v0 =
                             __hip_atomic_load(&P.LXY[g0].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        P.lslot[q] = t_contains(P.T, P.Tmask, f)
+                        const uint32_t e = ((uint32_t)sNa[lo] + (W.nm & 1u) + 1u) >> 1;
+                        P.lslot[q] = seen_contains(P.seen, f)
                                          ? LS_SEEN
-                                         : elect_slot<S::MAXS>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, g0, v0);
+                                         : elect_slot<S::MAXS>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g0, v0);
                     } else {
                         P.fp[((MODE == M_HASH) ? (uint64_t)P.off[pl] : 0ull) + lo] = f;
                     }
@@ -1083,14 +1199,14 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
                     win = true;
                     out = rank[r];
                     P.out_keys[out] = cand[r].key;
-                } else if (P.xrec) {
+                } else {
                     // sharded: the winner goes to its owner's exchange slot with a sidecar
                     // (parent reference, slot key); the owner inserts it into its seen set
                     const uint64_t j = P.off[pl] + rank[r];
                     win = P.wflag[j] != 0;
                     if (win) {
                         out = P.wpos[j];
-                        uint32_t *side = P.xrec + out * (uint64_t)(S::RECW + 4) + S::RECW;
+                        uint32_t *side = P.xrec + out * (uint64_t)(S::RECW_MAX + 4) + S::RECW_MAX;
                         {
                             const uint64_t pref = P.gid_parent_base + p;
                             side[0] = (uint32_t)pref;
@@ -1099,28 +1215,12 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
                             side[3] = 0;
                         }
                         int which = 0;
-                        MsgView mv{reinterpret_cast<const uint16_t *>(rec + S::CW), W.nm, 0u, 0u, cand[r].nadd, P.t.info};
+                        MsgView mv{P.front, W.idw, P.rcap, W.nm, 0u, 0u, cand[r].nadd, P.t.info};
                         succ_adds(cand[r], &mv.add0, &mv.add1);
-                        const int iv = check_invs<N, V>(cand[r].c, P.inv_mask, &which, mv);
-                        if (iv != 1) {
-                            const unsigned long long ek =
-                                ((((unsigned long long)p << 16) | cand[r].key) << 8) | (unsigned long long)which;
-                            atomicMin(&P.err[iv == 0 ? ERR_INV : ERR_EVAL], ek);
-                        }
-                    }
-                } else {
-                    const uint64_t j = P.off[pl] + rank[r];
-                    win = P.wflag[j] != 0;
-                    if (win) {
-                        out = P.next_base + P.wpos[j];
-                        const uint64_t gid = P.gid_next_base + out;
-                        t_insert(P.T, P.Tmask, P.fp[j]);
-                        P.par[gid] = P.gid_parent_base + p;
-                        P.pslot[gid] = (uint16_t)cand[r].key;
-                        int which = 0;
-                        MsgView mv{reinterpret_cast<const uint16_t *>(rec + S::CW), W.nm, 0u, 0u, cand[r].nadd, P.t.info};
-                        succ_adds(cand[r], &mv.add0, &mv.add1);
-                        const int iv = check_invs<N, V>(cand[r].c, P.inv_mask, &which, mv);
+                        uint32_t cc[Lo::NW];
+#pragma unroll
+                        for (int w = 0; w < Lo::NW; w++) cc[w] = cand[r].c[w];
+                        const int iv = check_invs<N, V>(cc, P.inv_order, &which, mv);
                         if (iv != 1) {
                             const unsigned long long ek =
                                 ((((unsigned long long)p << 16) | cand[r].key) << 8) | (unsigned long long)which;
@@ -1129,8 +1229,8 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
                     }
                 }
             }
-            const uint64_t stride = P.xrec ? (uint64_t)(S::RECW + 4) : (uint64_t)S::RECW;
-            uint32_t *dst = P.xrec ? P.xrec : P.next;
+            const uint64_t stride = (MODE == M_MAT) ? (uint64_t)(S::RECW_MAX + 4) : (uint64_t)S::RECW_MAX;
+            uint32_t *dst = (MODE == M_MAT) ? P.xrec : P.next;
             for (uint64_t m = __ballot(win); m; m &= m - 1) {
                 const int t = __ffsll((unsigned long long)m) - 1;
                 const uint64_t ot = rdlane64(out, t);
@@ -1151,7 +1251,7 @@ __global__ __launch_bounds__(64) void k_fp_states(KParams P, uint64_t n) {
     const int lane = threadIdx.x;
     for (uint64_t p = blockIdx.x; p < n; p += gridDim.x) {
         Wave<N, V, MR> W;
-        load_parent<N, V, MR, true>(P, P.front + p * (uint64_t)S::RECW, lane, W, ids, M0, M1, pcore);
+        load_parent<N, V, MR, true>(P, rec_start<S::RECW_MAX>(P, p), lane, W, ids, M0, M1, pcore);
         uint64_t row0[N], row1[N];
 #pragma unroll
         for (int j = 0; j < N; j++) { row0[j] = 0; row1[j] = 0; }
@@ -1166,11 +1266,12 @@ __global__ __launch_bounds__(64) void k_inv_states(KParams P, uint64_t n, int32_
     using Lo = Layout<N, V>;
     const uint64_t i = (uint64_t)blockIdx.x * 64 + threadIdx.x;
     if (i >= n) return;
-    const uint32_t *rec = P.front + i * (uint64_t)S::RECW;
-    uint32_t c[Lo::NW];
+    const uint64_t start = rec_start<S::RECW_MAX>(P, i);
+    uint32_t packed[S::CCW], c[Lo::NW];
 #pragma unroll
-    for (int w = 0; w < Lo::NW; w++) c[w] = rec[w];
-    const MsgView mv{reinterpret_cast<const uint16_t *>(rec + S::CW), (c[Lo::W_MISC] >> 16) & 0xFFu, 0u, 0u, 0u,
+    for (int k = 0; k < S::CCW; k++) packed[k] = ring_word(P.front, start, (uint32_t)k, P.rcap);
+    decode_core<N, V>(packed, c);
+    const MsgView mv{P.front, ring_wrap(start + S::CCW, P.rcap), P.rcap, (c[Lo::W_MISC] >> 16) & 0xFFu, 0u, 0u, 0u,
                      P.t.info};
     for (int b = 0; b < 7; b++) out[i * 7 + b] = inv_eval<N, V>(c, b, mv);
 }
@@ -1201,11 +1302,13 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *ws, ui
 }
 
 // One 1024-thread block per WTILE-parent tile, thread per parent: winners per parent (wcnt, as the
-// election counted them in wacc), their exclusive scan inside the tile (wpos), and per tile the
-// winners (bw) and successors generated (bg).  The last block to finish scans the tile totals into boff and writes
-// {generated, winners} to sum[0..1] -- the only values the host needs before commit.
+// election counted them in wacc) and their record words, the exclusive scans of both inside the
+// tile (wpos, wposw), and per tile the winners (bw), words (bww) and successors generated (bg).
+// The last block to finish scans the tile totals into boff / boffw and writes {generated, winners,
+// words} to the chunk summary -- the only values the host needs before commit.
 template <int N, int V, int MR>
 __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
+    constexpr uint32_t CCW = (uint32_t)Spec<N, V, MR>::CCW;
     __shared__ uint32_t ws[16];
     __shared__ uint32_t flag;
     if (!level_args(P)) return;
@@ -1213,25 +1316,30 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
     const uint32_t ntiles = (uint32_t)((np + WTILE - 1) / WTILE);
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const uint64_t pl = (uint64_t)tile * WTILE + threadIdx.x;
-        uint32_t w = 0, t = 0;
+        uint32_t w = 0, t = 0, wd = 0;
         if (pl < np) {
             // winners per parent were counted by the election itself; the accumulator is
             // re-armed for the next chunk here
             t = P.cnt[pl];
-            w = P.wacc[pl];
+            const uint32_t wa = P.wacc[pl], nm = P.pnm[pl];
             P.wacc[pl] = 0u;
+            w = wa & 0xFFFu;
+            wd = w * (CCW + (nm >> 1)) + (wa >> 12);
         }
-        uint32_t wt, gt;
+        uint32_t wt, gt, dt;
         const uint32_t x = block_excl_scan(w, ws, &wt);
         (void)block_excl_scan(t, ws, &gt);
+        const uint32_t xd = block_excl_scan(wd, ws, &dt);
         if (pl < np) {
             P.wcnt[pl] = w;
             P.wpos[pl] = x;
+            P.wposw[pl] = xd;
         }
         if (threadIdx.x == 0) {
             // write-through (sc1) stores: the last block reads them with sc1 loads, no fences
             __hip_atomic_store(&P.bw[tile], wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&P.bg[tile], gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&P.bww[tile], dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     // arrivals: only the nb blocks that had a tile (MI355X guide: sc1 payload, drained, then an
@@ -1248,25 +1356,31 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
     __syncthreads();
     if (!flag) return;
     // tile offsets (ntiles <= 1024 = blockDim.x) and the chunk totals
-    uint32_t wsum = 0, gsum = 0, wtot, gtot;
+    uint32_t wsum = 0, gsum = 0, dsum = 0, wtot, gtot, dtot;
     const uint32_t i = threadIdx.x;
     if (i < ntiles) {
         wsum = __hip_atomic_load(&P.bw[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         gsum = __hip_atomic_load(&P.bg[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dsum = __hip_atomic_load(&P.bww[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const uint32_t o = block_excl_scan(wsum, ws, &wtot);
     (void)block_excl_scan(gsum, ws, &gtot);
-    if (i < ntiles) P.boff[i] = o;
+    const uint32_t od = block_excl_scan(dsum, ws, &dtot);
+    if (i < ntiles) {
+        P.boff[i] = o;
+        P.boffw[i] = od;
+    }
     if (i == 0) {
         P.sum[0] = gtot;
         P.sum[1] = wtot;
+        P.sum[SUM_WORDS] = dtot;
     }
 }
 
-// Chunk summary, by the last block of the commit pass (one wave): {generated, winners} (from the winner
-// count pass), the error keys and flags (then re-armed).  In device-loop mode it also
+// Chunk summary, by the last block of the commit pass (one wave): {generated, winners, words} (from the
+// winner count pass), the error keys and flags (then re-armed).  In device-loop mode it also
 // records the level and advances the control block to the next one -- or stops the loop.
-template <int MAXS>
+template <int MAXS, int RECW_MAX>
 __device__ void finish_level(const KParams &P) {
     // one wave, everything it reads in flight at once: lanes 0..3 take the error slots, lane 4
     // the flags, lane 0 the summary and the control block
@@ -1280,7 +1394,7 @@ __device__ void finish_level(const KParams &P) {
     unsigned long long *sm = P.sum;
     if (lane <= ERR_NSLOTS) sm[2 + lane] = e;
     if (lane != 0) return;
-    const unsigned long long G = sm[0], Wn = sm[1];
+    const unsigned long long G = sm[0], Wn = sm[1], Ww = sm[SUM_WORDS];
     if (!P.ctl) return;
     LevelCtl c = *P.ctl;
     if (bad) {  // the host reports the error from this level's buffers
@@ -1292,10 +1406,13 @@ __device__ void finish_level(const KParams &P) {
         r.expanded = c.cur_n;
         r.generated = G;
         r.new_states = Wn;
+        r.words = Ww;
     }
     c.done_levels++;
     c.gid_cur += c.cur_n;
     c.cur_n = Wn;
+    c.cur_wbase = ring_wrap(c.cur_wbase + c.cur_words, c.rcap);
+    c.cur_words = Ww;
     c.T_count += Wn;
     c.level++;
     c.epoch++;
@@ -1306,7 +1423,8 @@ __device__ void finish_level(const KParams &P) {
     if (Wn == 0)
         c.stop = CTL_DONE;
     else if (c.done_levels >= c.batch || c.done_levels >= (uint32_t)LREC_CAP || Wn > c.chunk_parents ||
-             Gub > c.nxt_cap || c.gid_cur + Wn + Gub > c.trace_cap || 2 * (c.T_count + Gub) > c.T_cap)
+             Gub > c.off_cap || Ww + Gub * RECW_MAX > c.rcap || c.gid_cur + Wn + Gub - c.trace_base > c.trace_cap ||
+             2 * (c.T_count + Gub) > c.T_cap)
         c.stop = CTL_HOST;  // the next level is not known to fit the buffers: the host grows them
     *P.ctl = c;
 }
@@ -1338,49 +1456,10 @@ __device__ __forceinline__ bool last_commit_block(uint32_t *tick, uint32_t nb) {
     return __builtin_amdgcn_readfirstlane(last) != 0;
 }
 
-// Write the staged successor held by lane t as a record at rec_out (whole wave): core words
-// from lane t's registers, message ids = parent ids (per lane) merged with the added ids.
-template <int N, int V, int MR>
-__device__ __forceinline__ void write_staged(const uint32_t *id, uint32_t nm, const uint32_t *c, const uint4 ax, int t,
-                                             int lane, uint32_t *rec_out) {
-    using S = Spec<N, V, MR>;
-    const uint32_t nadd = rdlane(ax.x, t) >> 16;
-    const uint32_t ay = rdlane(ax.y, t), az = rdlane(ax.z, t);
-    const uint32_t add[4] = {ay & 0xFFFFu, ay >> 16, az & 0xFFFFu, az >> 16};
-    uint32_t v = 0;
-#pragma unroll
-    for (int w = 0; w < S::CW; w++) {
-        const uint32_t x = rdlane(c[w], t);
-        v = (lane == w) ? x : v;
-    }
-    if (lane < S::CW) rec_out[lane] = v;
-    uint16_t *oid = reinterpret_cast<uint16_t *>(rec_out + S::CW);
-#pragma unroll
-    for (int r = 0; r < MR; r++) {
-        const uint32_t k = (uint32_t)(r * 64 + lane);
-        if (k < nm) {
-            uint32_t pos = k;
-#pragma unroll
-            for (int a = 0; a < S::NADD; a++) pos += ((uint32_t)a < nadd && add[a] < id[r]) ? 1u : 0u;
-            oid[pos] = (uint16_t)id[r];
-        }
-    }
-#pragma unroll
-    for (int a = 0; a < S::NADD; a++) {
-        if ((uint32_t)a >= nadd) break;
-        uint32_t less = 0;
-#pragma unroll
-        for (int r = 0; r < MR; r++)
-            less += (uint32_t)__popcll(__ballot((uint32_t)(r * 64 + lane) < nm && id[r] < add[a]));
-#pragma unroll
-        for (int b = 0; b < S::NADD; b++) less += ((uint32_t)b < nadd && add[b] < add[a]) ? 1u : 0u;
-        if (lane == 0) oid[less] = (uint16_t)add[a];
-    }
-}
-
-// One wave per parent with winners: copy each winner (in TLC order) from staging into the next
-// level at next_base + wpos[pl] + i, insert its fingerprint, record its parent pointer and slot
-// key, and check the INVARIANTs (Raft.cfg:33) on it.
+// One wave per parent with winners: rebuild each winner (in TLC order) from the parent's core and
+// its staged row, check the INVARIANTs (Raft.cfg:33) on it, append it to the next level (record
+// at the scanned word offset, its offset in noff), insert its fingerprint, record its parent
+// pointer and slot key.
 template <int N, int V, int MR>
 __global__ __launch_bounds__(64) void k_commit(KParams P) {
     using S = Spec<N, V, MR>;
@@ -1391,73 +1470,96 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
     for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
         const uint64_t pl = p - P.p_begin;
         // every load of the parent that depends on no other load goes out at once: its winner
-        // count, offsets, successor count, record word, message ids and first 64 election
-        // slots (read ahead of knowing whether they are needed; all in bounds)
+        // count, offsets, successor count and first 64 election slots (read ahead of knowing
+        // whether they are needed; all in bounds)
         const uint32_t wc = P.wcnt[pl];
         const uint32_t bo = P.boff[pl / WTILE], wp = P.wpos[pl], t = P.cnt[pl];
-        const uint32_t *rec = P.front + p * (uint64_t)S::RECW;
-        const uint32_t misc = rec[Lo::W_MISC];
-        const uint16_t *rid = reinterpret_cast<const uint16_t *>(rec + S::CW);
-        uint32_t idr[MR];
-#pragma unroll
-        for (int r = 0; r < MR; r++) idr[r] = rid[r * 64 + lane];
+        const uint32_t bow = P.boffw[pl / WTILE], wpw = P.wposw[pl];
         const uint32_t g0 = lane < S::MAXS ? P.lslot[pl * (uint64_t)S::MAXS + lane] : LS_SEEN;
         if (!wc) continue;
-        const uint32_t w0 = bo + wp;
-        const uint32_t nm = (misc >> 16) & 0xFFu;
+        const uint64_t start = rec_start<S::RECW_MAX>(P, p);
+        uint32_t pc[Lo::NW], ppk[S::CCW];
+        load_core<N, V>(P.front, start, P.rcap, lane, pc, ppk);
+        const uint32_t nm = (pc[Lo::W_MISC] >> 16) & 0xFFu;
+        const uint64_t idw = ring_wrap(start + S::CCW, P.rcap);
         uint32_t id[MR];
 #pragma unroll
-        for (int r = 0; r < MR; r++) id[r] = (uint32_t)(r * 64 + lane) < nm ? idr[r] : 0xFFFFu;
+        for (int r = 0; r < MR; r++) {
+            const uint32_t k = (uint32_t)(r * 64 + lane);
+            id[r] = k < nm ? ring_id(P.front, idw, k, P.rcap) : 0xFFFFu;
+        }
+        const uint32_t w0 = bo + wp;
+        const uint64_t wd0 = P.next_wbase + bow + wpw;
         uint32_t done = 0;
+        uint64_t done_w = 0;
         for (uint32_t r0 = 0; r0 < t; r0 += 64) {
             const uint32_t r = r0 + (uint32_t)lane;
             const uint64_t q = pl * (uint64_t)S::MAXS + r;
             bool win = false;
             if (r < t) {
                 const uint32_t g = r0 == 0 ? g0 : P.lslot[q];
-                win = g < LS_ELECT && (uint32_t)P.L[g] == (uint32_t)q;
+                win = g < LS_ELECT && elect_q(P.L[g]) == (uint32_t)q;
             }
             const uint64_t m = __ballot(win);
             if (!m) continue;
-            uint32_t c[S::CW];
-            uint4 ax = make_uint4(0u, 0u, 0u, 0u);
+            uint32_t pk[S::CCW];
+            uint4 sa = make_uint4(0u, 0u, 0u, 0u), sb = sa, sc = sa;
+            uint32_t size = 0;
 #pragma unroll
-            for (int w = 0; w < S::CW; w++) c[w] = 0u;
+            for (int w = 0; w < S::CCW; w++) pk[w] = 0u;
             if (win) {
-                const uint4 *src = P.score + q * (uint64_t)S::CW4;
-#pragma unroll
-                for (int k = 0; k < S::CW4; k++) {
-                    const uint4 x = src[k];
-                    c[4 * k] = x.x; c[4 * k + 1] = x.y; c[4 * k + 2] = x.z; c[4 * k + 3] = x.w;
-                }
-                ax = P.saux[q];
-                const uint32_t key = ax.x & 0xFFFFu;
+                const uint4 *src = P.score + q * (uint64_t)S::SW4;
+                sa = src[0];
+                sb = src[1];
+                if (S::SW4 > 2) sc = src[2];
+                uint32_t c[Lo::NW];
+                unstage_core<N, V>(pc, sa, sb, c);
+                encode_core<N, V>(c, pk);
+                const uint32_t key = sb.z & 0xFFFFu, nadd = sb.z >> 16;
+                size = (uint32_t)S::CCW + ((nm + nadd + 1u) >> 1);
                 const uint64_t out = P.next_base + w0 + done + (uint32_t)__popcll(m & lt_mask);
                 const uint64_t gid = P.gid_next_base + out;
-                t_insert(P.T, P.Tmask, P.fp[q]);
-                P.par[gid] = P.gid_parent_base + p;
-                P.pslot[gid] = (uint16_t)key;
+                seen_insert(P.seen, P.fp[q]);
+                P.par[gid - P.trace_base] = P.gid_parent_base + p;
+                P.pslot[gid - P.trace_base] = (uint16_t)key;
                 int which = 0;
-                const MsgView mv{rid, nm, ax.y, ax.z, ax.x >> 16, P.t.info};
-                const int iv = check_invs<N, V>(c, P.inv_mask, &which, mv);
+                const MsgView mv{P.front, idw, P.rcap, nm, sb.w, sc.x, nadd, P.t.info};
+                const int iv = check_invs<N, V>(c, P.inv_order, &which, mv);
                 if (iv != 1) {
                     const unsigned long long ek = ((((unsigned long long)p << 16) | key) << 8) | (unsigned long long)which;
                     atomicMin(&P.err[iv == 0 ? ERR_INV : ERR_EVAL], ek);
                 }
             }
+            uint32_t wtot;
+            const uint32_t wpre = wave_excl_scan(size, lane, &wtot);
+            if (win) {
+                const uint64_t out = P.next_base + w0 + done + (uint32_t)__popcll(m & lt_mask);
+                P.noff[out] = wd0 + done_w + wpre;
+            }
+            // each winner's record (whole wave per record): packed core words + merged ids
             uint32_t i = 0;
             for (uint64_t mm = m; mm; mm &= mm - 1, i++) {
                 const int tt = __ffsll((unsigned long long)mm) - 1;
-                write_staged<N, V, MR>(id, nm, c, ax, tt, lane,
-                                       P.next + (P.next_base + w0 + done + i) * (uint64_t)S::RECW);
+                const uint64_t rstart = ring_wrap(P.nbase + wd0 + done_w + rdlane(wpre, tt), P.rcap);
+                uint32_t v = 0;
+#pragma unroll
+                for (int w = 0; w < S::CCW; w++) {
+                    const uint32_t x = rdlane(pk[w], tt);
+                    v = (lane == w) ? x : v;
+                }
+                if (lane < S::CCW) P.next[ring_wrap(rstart + lane, P.rcap)] = v;
+                const uint32_t nadd = rdlane(sb.z, tt) >> 16, ay = rdlane(sb.w, tt), az = rdlane(sc.x, tt);
+                const uint32_t add[4] = {ay & 0xFFFFu, ay >> 16, az & 0xFFFFu, az >> 16};
+                write_ids<N, V, MR>(P.next, ring_wrap(rstart + S::CCW, P.rcap), P.rcap, id, nm, add, nadd, lane);
             }
             done += (uint32_t)__popcll(m);
+            done_w += wtot;
         }
     }
     // the last block to leave finishes the level (finish_level)
     const uint64_t np = P.p_end - P.p_begin;
     const uint32_t nb = np < gridDim.x ? (np ? (uint32_t)np : 1u) : gridDim.x;
-    if (last_commit_block(P.ctick, nb)) finish_level<S::MAXS>(P);
+    if (last_commit_block(P.ctick, nb)) finish_level<S::MAXS, S::RECW_MAX>(P);
 }
 
 static inline unsigned grid_for(uint64_t n) {
@@ -1495,13 +1597,15 @@ struct Launch {
     static void invs(const KParams &P, uint64_t n, int32_t *out, hipStream_t s) {
         hipLaunchKernelGGL((k_inv_states<N, V, MR>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, P, n, out);
     }
+    static void enc(const uint32_t *c, uint32_t *o) { encode_core<N, V>(c, o); }
+    static void dec(const uint32_t *w, uint32_t *c) { decode_core<N, V>(w, c); }
 };
 
 template <int N, int V, int MR>
 static void fill(KernelSet *ks) {
     using S = Spec<N, V, MR>;
-    ks->N = N; ks->V = V; ks->MR = MR; ks->MCAP = S::MCAP; ks->CW = S::CW; ks->RECW = S::RECW;
-    ks->maxsucc = S::MCAP + N * S::SLOTS_PER_SERVER;
+    ks->N = N; ks->V = V; ks->MR = MR; ks->MCAP = S::MCAP; ks->CCW = S::CCW; ks->RECW_MAX = S::RECW_MAX;
+    ks->maxsucc = S::MAXS;
     ks->count = &Launch<N, V, MR>::count;
     ks->hash = &Launch<N, V, MR>::hash;
     ks->materialize = &Launch<N, V, MR>::mat;
@@ -1511,6 +1615,8 @@ static void fill(KernelSet *ks) {
     ks->commit = &Launch<N, V, MR>::commit;
     ks->fp_states = &Launch<N, V, MR>::fps;
     ks->inv_states = &Launch<N, V, MR>::invs;
+    ks->encode = &Launch<N, V, MR>::enc;
+    ks->decode = &Launch<N, V, MR>::dec;
 }
 
 bool get_kernels(int N, int V, int msg_cap, KernelSet *ks) {
@@ -1527,12 +1633,11 @@ bool get_kernels(int N, int V, int msg_cap, KernelSet *ks) {
 }
 
 // ---- seen-set / chunk dedup (thread per successor) -------------------------------------
-// Probe the global seen set T (read-only in this launch) and, for fingerprints not in
-// it, elect the first successor in TLC order per fingerprint in the chunk table L
-// (slots hold chunk-local successor indices; index order == TLC order).
+// Probe the global seen set (read-only in this launch) and, for fingerprints not in it, elect
+// the first successor in TLC order per fingerprint in the chunk table L (slots hold
+// chunk-local successor indices; index order == TLC order).
 __global__ __launch_bounds__(256) void k_dedup(const ulonglong2 *__restrict__ fp, const uint32_t *__restrict__ Gp,
-                                               const ulonglong2 *__restrict__ T, uint64_t Tmask,
-                                               unsigned long long *L, uint64_t Lmask, uint32_t epoch,
+                                               Seen seen, unsigned long long *L, uint64_t Lmask, uint32_t epoch,
                                                uint32_t *lslot) {
     // L slots hold (epoch << 32) | j; a slot whose epoch is not this chunk's is empty, so
     // the table never needs clearing.  atomicMin on the packed word keeps the smallest j
@@ -1541,15 +1646,7 @@ __global__ __launch_bounds__(256) void k_dedup(const ulonglong2 *__restrict__ fp
     const unsigned long long tag = (unsigned long long)epoch << 32;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < G; j += (uint64_t)gridDim.x * blockDim.x) {
         const ulonglong2 f = fp[j];
-        uint64_t h = t_index(f, Tmask);
-        bool old = false;
-        for (;;) {
-            const ulonglong2 e = T[h];
-            if (e.x == 0ull) break;
-            if (e.x == f.x && e.y == f.y) { old = true; break; }
-            h = (h + 1) & Tmask;
-        }
-        if (old) { lslot[j] = 0xFFFFFFFFu; continue; }
+        if (seen_contains(seen, f)) { lslot[j] = 0xFFFFFFFFu; continue; }
         uint64_t g = (f.x ^ (f.x >> 31) ^ (f.y >> 7)) & Lmask;
         const unsigned long long mine = tag | (unsigned long long)j;
         for (;;) {
@@ -1569,98 +1666,23 @@ __global__ __launch_bounds__(256) void k_dedup(const ulonglong2 *__restrict__ fp
     }
 }
 
-__global__ __launch_bounds__(256) void k_winflag(const uint32_t *__restrict__ lslot,
-                                                 const unsigned long long *__restrict__ L,
-                                                 const uint32_t *__restrict__ Gp, uint64_t Gub,
-                                                 uint32_t *__restrict__ w) {
-    const uint64_t G = *Gp;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < Gub;
-         j += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t win = 0;
-        if (j < G) {
-            const uint32_t g = lslot[j];
-            win = (g != 0xFFFFFFFFu && (uint32_t)L[g] == (uint32_t)j) ? 1u : 0u;
-        }
-        w[j] = win;
-    }
-}
-
-// one copy-back per chunk: G, W, error keys, flags
-__global__ void k_summary(const uint32_t *Gp, const uint32_t *wpos, unsigned long long *err, uint32_t *flags,
-                          unsigned long long *out) {
-    if (threadIdx.x == 0) {
-        const uint32_t G = *Gp;
-        out[0] = G;
-        out[1] = wpos[G];
-        for (int i = 0; i < ERR_NSLOTS; i++) {
-            out[2 + i] = err[i];
-            err[i] = ~0ull;  // reset for the next chunk
-        }
-        out[2 + ERR_NSLOTS] = flags[0];
-        flags[0] = 0;
-    }
-}
-
-// One-workgroup exclusive scan for small chunks (n <= 64K): out[i] = sum in[0..i), out[n] = total.
-// WIN = true computes the winner flags inline (flag_j = L[lslot[j]] == j, k_winflag) and
-// also stores them, replacing the flag kernel + a two-kernel library scan.
-template <bool WIN>
-__global__ __launch_bounds__(1024) void k_scan_small(const uint32_t *__restrict__ in, const uint32_t *__restrict__ Gp,
-                                                     uint64_t nmax, const uint32_t *__restrict__ lslot,
-                                                     const unsigned long long *__restrict__ L,
-                                                     uint32_t *__restrict__ flags_out, uint32_t *__restrict__ out) {
-    __shared__ uint32_t wsum[16];
-    const uint32_t n = WIN ? *Gp : (uint32_t)nmax;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint32_t per = (n + 1023) / 1024;
-    const uint32_t b = tid * per, e = min(n, b + per);
-    uint32_t local = 0;
-    for (uint32_t i = b; i < e; i++) {
-        uint32_t v;
-        if (WIN) {
-            const uint32_t g = lslot[i];
-            v = (g != 0xFFFFFFFFu && (uint32_t)L[g] == i) ? 1u : 0u;
-            flags_out[i] = v;
-        } else {
-            v = in[i];
-        }
-        local += v;
-    }
-    // exclusive scan of the 1024 thread sums: in-wave shuffles, then across the 16 waves
-    uint32_t x = local;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= (uint32_t)d) x += y;
-    }
-    if (lane == 63) wsum[wv] = x;
-    __syncthreads();
-    uint32_t wbase = 0;
-    for (uint32_t k = 0; k < wv; k++) wbase += wsum[k];
-    uint32_t run = wbase + x - local;
-    for (uint32_t i = b; i < e; i++) {
-        out[i] = run;
-        run += WIN ? flags_out[i] : in[i];
-    }
-    if (tid == 1023) out[n] = wbase + x;
-    if (WIN) {  // flags past the chunk's G stay zero for scans sized on an upper bound
-        for (uint64_t i = n + tid; i < nmax; i += 1024) flags_out[i] = 0;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_rehash(const ulonglong2 *__restrict__ Told, uint64_t old_cap, ulonglong2 *Tn,
-                                                uint64_t mask) {
+__global__ __launch_bounds__(256) void k_rehash(const ulonglong2 *__restrict__ Told, uint64_t old_cap, Seen dst) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < old_cap;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const ulonglong2 e = Told[i];
-        if (e.x) t_insert(Tn, mask, e);
+        if (e.x) seen_insert(dst, e);
     }
 }
 
-__global__ __launch_bounds__(256) void k_insert(const ulonglong2 *__restrict__ fp, uint64_t n, ulonglong2 *T,
-                                                uint64_t mask) {
+__global__ __launch_bounds__(256) void k_insert(const ulonglong2 *__restrict__ fp, uint64_t n, Seen seen) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        t_insert(T, mask, fp[i]);
+        seen_insert(seen, fp[i]);
+}
+
+__global__ __launch_bounds__(256) void k_rebase(const uint64_t *__restrict__ in, uint64_t n, uint64_t sub,
+                                                uint64_t *__restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = in[i] - sub;
 }
 
 static inline unsigned grid256(uint64_t n) {
@@ -1668,33 +1690,18 @@ static inline unsigned grid256(uint64_t n) {
     return (unsigned)(b < cap ? (b ? b : 1) : cap);
 }
 
-void launch_dedup(const ulonglong2 *fp, const uint32_t *Gp, uint64_t Gub, const ulonglong2 *T, uint64_t Tmask,
-                  unsigned long long *L, uint64_t Lmask, uint32_t epoch, uint32_t *lslot, hipStream_t s) {
-    hipLaunchKernelGGL(k_dedup, dim3(grid256(Gub)), dim3(256), 0, s, fp, Gp, T, Tmask, L, Lmask, epoch, lslot);
+void launch_dedup(const ulonglong2 *fp, const uint32_t *Gp, uint64_t Gub, Seen seen, unsigned long long *L,
+                  uint64_t Lmask, uint32_t epoch, uint32_t *lslot, hipStream_t s) {
+    hipLaunchKernelGGL(k_dedup, dim3(grid256(Gub)), dim3(256), 0, s, fp, Gp, seen, L, Lmask, epoch, lslot);
 }
-void launch_winflag(const uint32_t *lslot, const unsigned long long *L, const uint32_t *Gp, uint64_t Gub,
-                    uint32_t *wflag, hipStream_t s) {
-    hipLaunchKernelGGL(k_winflag, dim3(grid256(Gub)), dim3(256), 0, s, lslot, L, Gp, Gub, wflag);
+void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, Seen dst, hipStream_t s) {
+    hipLaunchKernelGGL(k_rehash, dim3(grid256(old_cap)), dim3(256), 0, s, Told, old_cap, dst);
 }
-void launch_summary(const uint32_t *Gp, const uint32_t *wpos, const unsigned long long *err, const uint32_t *flags,
-                    unsigned long long *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_summary, dim3(1), dim3(64), 0, s, Gp, wpos, const_cast<unsigned long long *>(err),
-                       const_cast<uint32_t *>(flags), out);
+void launch_insert_fps(const ulonglong2 *fp, uint64_t n, Seen seen, hipStream_t s) {
+    hipLaunchKernelGGL(k_insert, dim3(grid256(n)), dim3(256), 0, s, fp, n, seen);
 }
-void launch_scan_small(const uint32_t *in, uint64_t n, uint32_t *out, hipStream_t s) {
-    hipLaunchKernelGGL((k_scan_small<false>), dim3(1), dim3(1024), 0, s, in, (const uint32_t *)nullptr, n,
-                       (const uint32_t *)nullptr, (const unsigned long long *)nullptr, (uint32_t *)nullptr, out);
-}
-void launch_winscan_small(const uint32_t *lslot, const unsigned long long *L, const uint32_t *Gp, uint64_t Gub,
-                          uint32_t *wflag, uint32_t *wpos, hipStream_t s) {
-    hipLaunchKernelGGL((k_scan_small<true>), dim3(1), dim3(1024), 0, s, (const uint32_t *)nullptr, Gp, Gub, lslot, L,
-                       wflag, wpos);
-}
-void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, ulonglong2 *Tnew, uint64_t new_mask, hipStream_t s) {
-    hipLaunchKernelGGL(k_rehash, dim3(grid256(old_cap)), dim3(256), 0, s, Told, old_cap, Tnew, new_mask);
-}
-void launch_insert_fps(const ulonglong2 *fp, uint64_t n, ulonglong2 *T, uint64_t Tmask, hipStream_t s) {
-    hipLaunchKernelGGL(k_insert, dim3(grid256(n)), dim3(256), 0, s, fp, n, T, Tmask);
+void launch_rebase(const uint64_t *in, uint64_t n, uint64_t sub, uint64_t *out, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_rebase, dim3(grid256(n)), dim3(256), 0, s, in, n, sub, out);
 }
 
 // ---- sharded exchange helpers (one GPU per owner shard) -------------------------------------
@@ -1743,17 +1750,19 @@ __global__ __launch_bounds__(256) void k_scatter_flags(const uint32_t *__restric
     }
 }
 
-// owner: append received winner records (record + 4-word sidecar) to the next level,
-// parent pointers to the trace arrays, fingerprints to the seen set
+// owner: append received winner records (record + 4-word sidecar) to the next level (fixed
+// stride recw inside the frontier ring), parent pointers to the trace arrays
 __global__ __launch_bounds__(256) void k_accept(const uint32_t *__restrict__ xrec, uint64_t n, uint32_t recw,
-                                                uint32_t *__restrict__ next, uint64_t *__restrict__ par,
+                                                uint32_t *__restrict__ ring, uint64_t rcap, uint64_t nbase,
+                                                uint64_t rel0, uint64_t *__restrict__ noff, uint64_t *__restrict__ par,
                                                 uint16_t *__restrict__ pslot, uint64_t src_tag) {
     const uint64_t total = n * recw;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t q = i / recw, w = i - q * recw;
-        next[i] = xrec[q * (recw + 4) + w];
+        ring[ring_wrap(nbase + ring_wrap(rel0 + i, rcap), rcap)] = xrec[q * (recw + 4) + w];
         if (w == 0) {
             const uint32_t *side = xrec + q * (recw + 4) + recw;
+            noff[q] = rel0 + q * recw;
             par[q] = src_tag | ((uint64_t)side[0] | ((uint64_t)side[1] << 32));
             pslot[q] = (uint16_t)side[2];
         }
@@ -1761,10 +1770,9 @@ __global__ __launch_bounds__(256) void k_accept(const uint32_t *__restrict__ xre
 }
 
 __global__ __launch_bounds__(256) void k_insert_flagged(const ulonglong2 *__restrict__ fp,
-                                                        const uint32_t *__restrict__ flag, uint64_t n, ulonglong2 *T,
-                                                        uint64_t mask) {
+                                                        const uint32_t *__restrict__ flag, uint64_t n, Seen seen) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        if (flag[i]) t_insert(T, mask, fp[i]);
+        if (flag[i]) seen_insert(seen, fp[i]);
 }
 
 // values at a list of indices (segment boundaries of scans) -> out
@@ -1791,13 +1799,13 @@ void launch_scatter_flags(const uint32_t *perm, const uint32_t *sflag, const uin
                           uint32_t *wflag, uint32_t *wpos, hipStream_t s) {
     hipLaunchKernelGGL(k_scatter_flags, dim3(grid256(G)), dim3(256), 0, s, perm, sflag, spos, G, wflag, wpos);
 }
-void launch_accept(const uint32_t *xrec, uint64_t n, uint32_t recw, uint32_t *next, uint64_t *par, uint16_t *pslot,
-                   uint64_t src_tag, hipStream_t s) {
-    hipLaunchKernelGGL(k_accept, dim3(grid256(n * recw)), dim3(256), 0, s, xrec, n, recw, next, par, pslot, src_tag);
+void launch_accept(const uint32_t *xrec, uint64_t n, uint32_t recw, uint32_t *ring, uint64_t rcap, uint64_t nbase,
+                   uint64_t rel0, uint64_t *noff, uint64_t *par, uint16_t *pslot, uint64_t src_tag, hipStream_t s) {
+    hipLaunchKernelGGL(k_accept, dim3(grid256(n * recw)), dim3(256), 0, s, xrec, n, recw, ring, rcap, nbase, rel0, noff,
+                       par, pslot, src_tag);
 }
-void launch_insert_flagged(const ulonglong2 *fp, const uint32_t *flag, uint64_t n, ulonglong2 *T, uint64_t mask,
-                           hipStream_t s) {
-    hipLaunchKernelGGL(k_insert_flagged, dim3(grid256(n)), dim3(256), 0, s, fp, flag, n, T, mask);
+void launch_insert_flagged(const ulonglong2 *fp, const uint32_t *flag, uint64_t n, Seen seen, hipStream_t s) {
+    hipLaunchKernelGGL(k_insert_flagged, dim3(grid256(n)), dim3(256), 0, s, fp, flag, n, seen);
 }
 void launch_pick(const uint32_t *a, const uint64_t *idx, int n, unsigned long long *out, hipStream_t s) {
     hipLaunchKernelGGL(k_pick, dim3(1), dim3(256), 0, s, a, idx, n, out);

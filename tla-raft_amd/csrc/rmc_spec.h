@@ -52,6 +52,124 @@ struct Layout {
 RMC_HD uint32_t nib(uint32_t w, int i) { return (w >> (4 * i)) & 15u; }
 RMC_HD uint32_t setnib(uint32_t w, int i, uint32_t v) { return (w & ~(15u << (4 * i))) | ((v & 15u) << (4 * i)); }
 
+// ---- storage codec: the nibble core above, bit-packed for HBM ------------------------------
+// The kernels compute on the nibble layout (constant-position fields in registers); frontier
+// records and the successor staging store the same fields with the widths the spec's domains
+// need (tla:8-16, cfg:3-4: terms <= MaxElection <= 7, indices <= |Vals| + 2, restarts <= 15,
+// |msgs| <= 255).  Raft.cfg's core (3 servers, 2 values) is exactly 128 bits -- 16 B instead
+// of the nibble layout's 64 B.  A record in HBM is CCW packed core words followed by |msgs|
+// u16 message ids (TLC order), padded to a whole word: CCW + ceil(|msgs| / 2) words.
+constexpr int bits_for(int maxval) { return maxval <= 0 ? 0 : 1 + bits_for(maxval >> 1); }
+
+template <int N, int V>
+struct Codec {
+    static constexpr int B_VF = bits_for(N);                  // 0 = None, k + 1 = server k
+    static constexpr int B_CT = 3;                            // currentTerm 0..MaxElection (<= 7)
+    static constexpr int B_RO = 2;                            // Follower / Candidate / Leader
+    static constexpr int B_IX = bits_for(V + 1);              // commitIndex, Len(logs), matchIndex: 1..V+1
+    static constexpr int B_NI = bits_for(V + 2);              // nextIndex 2..V+2
+    static constexpr int B_VAL = bits_for(V - 1);             // a log entry's value 0..V-1
+    static constexpr int B_ENT = 3 + B_VAL;                   // log entry: term | val
+    static constexpr int BITS = N * (B_VF + B_CT + B_RO + 2 * B_IX) + N * V * B_ENT + N * N * (B_IX + B_NI) +
+                                N * N + 3 + 4 + V + 8;
+    static constexpr int CCW = (BITS + 31) / 32;              // packed core words
+};
+
+RMC_HD void bits_put(uint32_t *w, int pos, uint32_t v, int b) {
+    if (b == 0) return;
+    const int i = pos >> 5, o = pos & 31;
+    w[i] |= v << o;
+    if (o + b > 32) w[i + 1] |= v >> (32 - o);
+}
+RMC_HD uint32_t bits_get(const uint32_t *w, int pos, int b) {
+    if (b == 0) return 0u;
+    const int i = pos >> 5, o = pos & 31;
+    uint32_t v = w[i] >> o;
+    if (o + b > 32) v |= w[i + 1] << (32 - o);
+    return b >= 32 ? v : (v & ((1u << b) - 1u));
+}
+
+// nibble core c[Layout::NW] -> packed words o[Codec::CCW] (every position is a compile-time
+// constant once the loops unroll)
+template <int N, int V>
+RMC_HD void encode_core(const uint32_t *c, uint32_t *o) {
+    using L = Layout<N, V>;
+    using C = Codec<N, V>;
+#pragma unroll
+    for (int k = 0; k < C::CCW; k++) o[k] = 0u;
+    int pos = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint32_t vf = nib(c[L::W_VF], i);
+        bits_put(o, pos, vf == VF_NONE ? 0u : vf + 1u, C::B_VF); pos += C::B_VF;
+        bits_put(o, pos, nib(c[L::W_CT], i), C::B_CT); pos += C::B_CT;
+        bits_put(o, pos, nib(c[L::W_ROLE], i), C::B_RO); pos += C::B_RO;
+        bits_put(o, pos, nib(c[L::W_CI], i), C::B_IX); pos += C::B_IX;
+        bits_put(o, pos, nib(c[L::W_LL], i), C::B_IX); pos += C::B_IX;
+#pragma unroll
+        for (int x = 0; x < V; x++) {
+            const uint32_t b = (c[L::W_LOG + i] >> (8 * x)) & 0xFFu;
+            bits_put(o, pos, (b & 7u) | ((b >> 4) << 3), C::B_ENT); pos += C::B_ENT;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++)
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            bits_put(o, pos, nib(c[L::W_MI + i], j), C::B_IX); pos += C::B_IX;
+            bits_put(o, pos, nib(c[L::W_NI + i], j), C::B_NI); pos += C::B_NI;
+        }
+    bits_put(o, pos, c[L::W_PEND] & ((1u << (N * N)) - 1u), N * N); pos += N * N;
+    const uint32_t misc = c[L::W_MISC];
+    bits_put(o, pos, misc & 7u, 3); pos += 3;
+    bits_put(o, pos, (misc >> 4) & 15u, 4); pos += 4;
+    bits_put(o, pos, (misc >> 8) & ((1u << V) - 1u), V); pos += V;
+    bits_put(o, pos, (misc >> 16) & 0xFFu, 8);
+}
+
+template <int N, int V>
+RMC_HD void decode_core(const uint32_t *w, uint32_t *c) {
+    using L = Layout<N, V>;
+    using C = Codec<N, V>;
+#pragma unroll
+    for (int k = 0; k < L::NW; k++) c[k] = 0u;
+    int pos = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const uint32_t vf = bits_get(w, pos, C::B_VF); pos += C::B_VF;
+        c[L::W_VF] |= (vf == 0u ? VF_NONE : vf - 1u) << (4 * i);
+        c[L::W_CT] |= bits_get(w, pos, C::B_CT) << (4 * i); pos += C::B_CT;
+        c[L::W_ROLE] |= bits_get(w, pos, C::B_RO) << (4 * i); pos += C::B_RO;
+        c[L::W_CI] |= bits_get(w, pos, C::B_IX) << (4 * i); pos += C::B_IX;
+        c[L::W_LL] |= bits_get(w, pos, C::B_IX) << (4 * i); pos += C::B_IX;
+#pragma unroll
+        for (int x = 0; x < V; x++) {
+            const uint32_t e = bits_get(w, pos, C::B_ENT); pos += C::B_ENT;
+            c[L::W_LOG + i] |= ((e & 7u) | ((e >> 3) << 4)) << (8 * x);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++)
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            c[L::W_MI + i] |= bits_get(w, pos, C::B_IX) << (4 * j); pos += C::B_IX;
+            c[L::W_NI + i] |= bits_get(w, pos, C::B_NI) << (4 * j); pos += C::B_NI;
+        }
+    c[L::W_PEND] = bits_get(w, pos, N * N); pos += N * N;
+    uint32_t misc = bits_get(w, pos, 3); pos += 3;
+    misc |= bits_get(w, pos, 4) << 4; pos += 4;
+    misc |= bits_get(w, pos, V) << 8; pos += V;
+    misc |= bits_get(w, pos, 8) << 16;
+    c[L::W_MISC] = misc;
+}
+
+// |msgs| of a packed core (its last 8 bits)
+template <int N, int V>
+RMC_HD uint32_t core_nm(const uint32_t *w) { return bits_get(w, Codec<N, V>::BITS - 8, 8); }
+
+// ring-buffer position: x < 2 * cap
+RMC_HD uint64_t ring_wrap(uint64_t x, uint64_t cap) { return x >= cap ? x - cap : x; }
+
 // ---- message info word ------------------------------------------------------------
 // [1:0] type  [4:2] src  [7:5] dst  [11:8] term  [15:12] x1  [19:16] x2  [23:20] x3
 // [24] entry present  [28:25] entry term  [31:29] entry val

@@ -48,6 +48,8 @@ class _Config(ctypes.Structure):
         ("rank", ctypes.c_int32), ("world_size", ctypes.c_int32), ("comm_unique_id", ctypes.c_void_p),
         ("virtual_shards", ctypes.c_int32), ("timing_phases", ctypes.c_uint32),
         ("device_levels", ctypes.c_uint32), ("shard_min_states", ctypes.c_uint64),
+        ("invariant_order", ctypes.c_uint32), ("compact_log2", ctypes.c_uint32),
+        ("seen_mem_bytes", ctypes.c_uint64), ("frontier_mem_bytes", ctypes.c_uint64),
     ]
 
 
@@ -57,6 +59,7 @@ class _LevelStats(ctypes.Structure):
         ("generated", ctypes.c_uint64), ("new_states", ctypes.c_uint64), ("total_generated", ctypes.c_uint64),
         ("total_distinct", ctypes.c_uint64), ("queue", ctypes.c_uint64), ("seconds", ctypes.c_double),
         ("kernel_ms", ctypes.c_double * 6), ("kernel_launches", ctypes.c_uint64 * 6),
+        ("new_bytes", ctypes.c_uint64),
     ]
 
 
@@ -65,6 +68,8 @@ class _Result(ctypes.Structure):
         ("status", ctypes.c_int32), ("depth", ctypes.c_int32), ("generated", ctypes.c_uint64),
         ("distinct", ctypes.c_uint64), ("queue", ctypes.c_uint64), ("violated", ctypes.c_int32),
         ("trace_len", ctypes.c_uint32), ("seconds", ctypes.c_double),
+        ("seen_slots", ctypes.c_uint64), ("seen_slot_bytes", ctypes.c_int32), ("pad_", ctypes.c_int32),
+        ("frontier_ring_bytes", ctypes.c_uint64), ("frontier_peak_bytes", ctypes.c_uint64),
     ]
 
 
@@ -132,15 +137,23 @@ class ModelConfig:
     timing_phases: int = 0           # bit i: time phase i with HIP events (0 = all phases)
     device_levels: int = 0           # levels per host round trip in run() (0 = auto, 1 = host-driven)
     shard_min_states: int = 0        # >1 shards: replicate levels below this size (0 = auto 2^20, 1 = always shard)
+    compact_log2: int = 0            # seen set: 16-B slots up to 2^compact_log2 slots, then 8-B slots (0 = auto 27)
+    seen_mem_bytes: int = 0          # compact seen-set budget (0 = auto: half the free device memory)
+    frontier_mem_bytes: int = 0      # frontier ring budget once the seen set is compact (0 = auto)
 
     def to_c(self) -> _Config:
         c = _Config()
         c.n_servers, c.n_vals = self.n_servers, self.n_vals
         c.max_election, c.max_restart = self.max_election, self.max_restart
-        mask = 0
-        for name in self.invariants:
-            mask |= INVARIANT_BITS[name]
+        mask, order, k = 0, 0, 0
+        for name in self.invariants:  # cfg order: TLC checks the invariants in that order
+            bit = INVARIANT_BITS[name]
+            if not mask & bit:
+                order |= (bit.bit_length()) << (4 * k)
+                k += 1
+            mask |= bit
         c.invariants = mask
+        c.invariant_order = order
         c.check_deadlock = int(self.check_deadlock)
         c.spec_variant = self.spec_variant
         c.device = self.device
@@ -153,6 +166,9 @@ class ModelConfig:
         c.timing_phases = self.timing_phases
         c.device_levels = self.device_levels
         c.shard_min_states = self.shard_min_states
+        c.compact_log2 = self.compact_log2
+        c.seen_mem_bytes = self.seen_mem_bytes
+        c.frontier_mem_bytes = self.frontier_mem_bytes
         if self.comm_unique_id is not None:
             self._idbuf = ctypes.create_string_buffer(bytes(self.comm_unique_id), 128)
             c.comm_unique_id = ctypes.cast(self._idbuf, ctypes.c_void_p)
@@ -178,7 +194,11 @@ def parse_config(cfg_text: str, tla_text: Optional[str] = None) -> ModelConfig:
                               ctypes.byref(c), err, 512)
     if rc != RMC_OK:
         raise RmcError(err.value.decode())
-    invs = tuple(name for bit, name in enumerate(INVARIANT_BY_BIT) if c.invariants & (1 << bit))
+    invs, o = [], c.invariant_order
+    while o:
+        invs.append(INVARIANT_BY_BIT[(o & 15) - 1])
+        o >>= 4
+    invs = tuple(invs) or tuple(name for bit, name in enumerate(INVARIANT_BY_BIT) if c.invariants & (1 << bit))
     return ModelConfig(n_servers=c.n_servers, n_vals=c.n_vals, max_election=c.max_election,
                        max_restart=c.max_restart, invariants=invs, check_deadlock=bool(c.check_deadlock),
                        spec_variant=c.spec_variant, symmetry=not c.no_symmetry)
@@ -289,6 +309,7 @@ class LevelStats:
     seconds: float
     kernel_ms: List[float] = field(default_factory=list)
     kernel_launches: List[int] = field(default_factory=list)
+    new_bytes: int = 0
 
 
 @dataclass
@@ -302,6 +323,10 @@ class Result:
     trace_len: int
     seconds: float
     levels: List[LevelStats] = field(default_factory=list)
+    seen_slots: int = 0
+    seen_slot_bytes: int = 0
+    frontier_ring_bytes: int = 0
+    frontier_peak_bytes: int = 0
 
 
 class ModelChecker:
@@ -345,7 +370,7 @@ class ModelChecker:
     def _stats(s: _LevelStats) -> LevelStats:
         return LevelStats(s.level, STATUS_NAMES.get(s.status, str(s.status)), s.expanded, s.generated,
                           s.new_states, s.total_generated, s.total_distinct, s.queue, s.seconds,
-                          list(s.kernel_ms), list(s.kernel_launches))
+                          list(s.kernel_ms), list(s.kernel_launches), s.new_bytes)
 
     def init(self) -> LevelStats:
         st = _LevelStats()
@@ -405,7 +430,8 @@ class ModelChecker:
         self._check(self.lib.rmc_get_result(self.h, ctypes.byref(r)))
         return Result(STATUS_NAMES.get(r.status, str(r.status)), r.depth, r.generated, r.distinct, r.queue,
                       INVARIANT_BY_BIT[r.violated] if r.violated >= 0 else None, r.trace_len, r.seconds,
-                      list(self.levels))
+                      list(self.levels), r.seen_slots, r.seen_slot_bytes, r.frontier_ring_bytes,
+                      r.frontier_peak_bytes)
 
     def trace(self) -> List[Tuple[Optional[Tuple[int, int, int]], dict]]:
         n = ctypes.c_uint32()
