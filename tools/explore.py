@@ -22,10 +22,14 @@ ap.add_argument("--seeded", action="store_true")
 ap.add_argument("--chunk", type=int, default=0)
 ap.add_argument("--seenlog2", type=int, default=0)
 ap.add_argument("--json", default="")
+ap.add_argument("--compact-log2", type=int, default=0)
+ap.add_argument("--seen-mem-gb", type=float, default=0)
+ap.add_argument("--frontier-mem-gb", type=float, default=0)
 a = ap.parse_args()
 cfg = raftmc.ModelConfig(n_servers=a.n, n_vals=a.V, max_election=a.E, max_restart=a.R,
                          spec_variant=raftmc.SPEC_SEEDED if a.seeded else raftmc.SPEC_RAFT,
-                         chunk_successors=a.chunk, seen_log2=a.seenlog2)
+                         chunk_successors=a.chunk, seen_log2=a.seenlog2, compact_log2=a.compact_log2,
+                         seen_mem_bytes=int(a.seen_mem_gb * 2**30), frontier_mem_bytes=int(a.frontier_mem_gb * 2**30))
 t0 = time.time()
 mc = raftmc.ModelChecker(cfg)
 print(f"create {time.time() - t0:.2f}s", flush=True)
@@ -38,11 +42,12 @@ while ls.status == "ok" and time.time() - t1 < a.budget:
     ms = " ".join(f"{x:.1f}" for x in ls.kernel_ms)
     print(f"L{ls.level:3d} F={ls.expanded:>11d} G={ls.generated:>12d} N={ls.new_states:>11d} "
           f"tot={ls.total_distinct:>12d} {ls.seconds * 1e3:9.1f}ms [{ms}] el={el:.1f}s "
-          f"{ls.total_distinct / el:.3e} ds/s", flush=True)
+          f"{ls.total_distinct / el:.3e} ds/s rec={ls.new_bytes / max(1, ls.new_states):.1f}B", flush=True)
     rows.append(ls.__dict__)
 r = mc.result()
 print("RESULT", r.status, "generated", r.generated, "distinct", r.distinct, "depth", r.depth,
-      "seconds", round(r.seconds, 3), flush=True)
+      "seconds", round(r.seconds, 3), "seen_slots", r.seen_slots, "x", r.seen_slot_bytes, "B; ring",
+      r.frontier_ring_bytes, "B; frontier peak", r.frontier_peak_bytes, "B", flush=True)
 if a.json:
     with open(a.json, "w") as f:
         json.dump(dict(result=r.__dict__ | {"levels": None}, levels=rows), f)
