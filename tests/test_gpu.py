@@ -133,6 +133,20 @@ def test_no_all_commit_run_matches_oracle():
     mc.close()
 
 
+@pytest.mark.parametrize("order", [("NoAllCommit", "RaftCanCommt"), ("RaftCanCommt", "NoAllCommit"),
+                                   ("Inv", "CommitAll", "RaftCanCommt")])
+def test_invariants_checked_in_cfg_order(order):
+    """Both invariants are FALSE at Init: TLC reports the one the cfg lists first (Raft.cfg:33-34),
+    as the oracle does -- not the lower invariant bit."""
+    cfg = R.Config(n=3, V=1, max_election=1, max_restart=3, invariants=order)
+    p = R.bfs(cfg)
+    with raftmc.ModelChecker(raftmc.ModelConfig(n_servers=3, n_vals=1, max_election=1, max_restart=3,
+                                                invariants=order)) as mc:
+        res = mc.run()
+    assert res.status == p.verdict == "invariant"
+    assert res.violated == p.violated == [i for i in order if i != "Inv"][0]
+
+
 def test_eval_error_state():
     mc = checker(3, 2, 3, 3)
     s = R.state_to_json(R.State((-1, -1, -1), (1, 1, 1), (((0, -1), (1, 0), (1, 1)), ((0, -1), (1, 0)), ((0, -1),)),
@@ -239,6 +253,46 @@ def test_steps_api_batches_levels():
            [(x.level, x.expanded, x.generated, x.new_states, x.queue) for x in lb]
     assert a.result().distinct == g["distinct"]
     a.close(); b.close()
+
+
+# ---- large-run storage: compact seen set, frontier ring at a fixed budget --------------------
+LARGE_MODE = ["n3_v1_e2_r3", "n3_v2_e1_r3", "n4_v1_e1_r3", "n5_v1_e1_r3", "n3_v3_e1_r3", "seeded_n3_v2_e2_r3",
+              "deadlock_n3_v1_e1_r3", "nosplit_n3_v1_e2_r3", "seeded_n3_v1_e2_r3"]
+
+
+@pytest.mark.parametrize("device_levels", [0, 1])
+@pytest.mark.parametrize("name", LARGE_MODE)
+def test_compact_seen_set_and_fixed_ring_match_golden(name, device_levels):
+    """The storage a large run switches to -- 8-B seen-set slots (migrated from the 16-B table after
+    2^10 slots, sized to the run) and a frontier ring pinned at ~60 % of the live frontier's peak,
+    so that the next level reuses the space of chunks already expanded and wraps around the ring --
+    gives TLC's results: per-level counts, depth, verdict, queue and the counterexample."""
+    g = LEVELS[name]
+    probe, res0 = run_cfg(g, chunk_successors=6000, device_levels=1)
+    peak = res0.frontier_peak_bytes
+    probe.close()
+    slots = 1 << max(12, (int(g["distinct"] / 0.6)).bit_length())
+    ring = int(0.6 * peak) + 4 * 6000 * 36 + 4096
+    mc, res = run_cfg(g, chunk_successors=6000, device_levels=device_levels, compact_log2=10, seen_log2=8,
+                      seen_mem_bytes=8 * slots, frontier_mem_bytes=ring)
+    check_levels(g, res)
+    if g["distinct"] > 2048:  # the run outgrew the 2^10-slot full table
+        assert res.seen_slot_bytes == 8 and res.seen_slots == slots
+        assert res.frontier_ring_bytes <= max(ring, 4 * 6000 * 36 * 2)
+    if name in TRACES:
+        tr = mc.trace()
+        assert [st for _, st in tr] == [e["state"] for e in TRACES[name]["steps"]]
+    mc.close()
+
+
+def test_compact_seen_set_at_scale():
+    """bench's at-scale configuration (18.5M states) on the compact seen set and a ring at ~60 % of
+    its peak frontier: the C oracle's per-level counts."""
+    g = LEVELS_BIG["n3_v2_e2_r3"]
+    mc, res = run_cfg(g, compact_log2=20, seen_log2=12, seen_mem_bytes=8 << 25, frontier_mem_bytes=600 << 20)
+    check_levels(g, res)
+    assert res.seen_slot_bytes == 8
+    mc.close()
 
 
 def test_seeded_trace_independent_of_chunking():

@@ -30,6 +30,8 @@ CFG = """CONSTANTS
     s1 = s1
     s2 = s2
     s3 = s3
+    s4 = s4
+    s5 = s5
     Servers = {{{servers}}}
     v1 = v1
     v2 = v2
@@ -63,10 +65,29 @@ def test_parse_shipped_config_equivalent():
     assert c.invariants == ("Inv",) and c.symmetry
 
 
+def test_parse_verbatim_reference_pair():
+    """The reference's own Raft.cfg + Raft.tla (myrun.sh:3 inputs), read in place."""
+    cfg_path, tla_path = "/root/reference/Raft.cfg", REF_TLA
+    if not (os.path.exists(cfg_path) and os.path.exists(REF_TLA)):
+        pytest.skip("reference files not present on this machine")
+    c = raftmc.parse_config(open(cfg_path).read(), open(tla_path).read())
+    assert (c.n_servers, c.n_vals, c.max_election, c.max_restart) == (3, 2, 3, 3)
+    assert c.invariants == ("Inv",) and c.symmetry and c.spec_variant == raftmc.SPEC_RAFT
+
+
+def test_parse_keeps_invariant_order():
+    """TLC checks INVARIANTs in the order the cfg lists them (Raft.cfg:33-34)."""
+    c = raftmc.parse_config(cfg_text(inv="NoAllCommit\nRaftCanCommt\nInv"))
+    assert c.invariants == ("NoAllCommit", "RaftCanCommt", "Inv")
+    assert c.to_c().invariant_order == (6 | 3 << 4 | 1 << 8)
+    c = raftmc.parse_config(cfg_text(inv="Inv\nNoAllCommit\nInv"))  # listed twice: checked once
+    assert c.invariants == ("Inv", "NoAllCommit")
+
+
 def test_parse_variants():
     c = raftmc.parse_config(cfg_text(E=2, servers="s1, s2, s3, s4, s5", vals="v1", inv="Inv\nNoSplitVote"))
     assert (c.n_servers, c.n_vals, c.max_election) == (5, 1, 2)
-    assert set(c.invariants) == {"Inv", "NoSplitVote"}
+    assert c.invariants == ("Inv", "NoSplitVote")
     c = raftmc.parse_config(cfg_text().replace("SYMMETRY symmServers", ""))
     assert not c.symmetry
 

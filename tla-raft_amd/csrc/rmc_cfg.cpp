@@ -258,6 +258,10 @@ bool parse_model(const std::string &cfg_text, const char *tla_text, ParsedModel 
                                       "None", "VoteReq", "VoteResp", "AppendReq", "AppendResp"};
         bool k = false;
         for (const char *n : known) k |= kv.first == n;
+        // s1 = s1, v1 = v1 (Raft.cfg:7-20): the model values Servers / Vals are built from
+        k |= kv.second.kind == Value::MODEL &&
+             (std::count(pm->servers.begin(), pm->servers.end(), kv.first) ||
+              std::count(pm->vals.begin(), pm->vals.end(), kv.first));
         if (!k) pm->ignored_constants.push_back(kv.first);
     }
     if (tla_text) {

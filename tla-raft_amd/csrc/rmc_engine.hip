@@ -764,7 +764,7 @@ struct rmc_ctx {
         HIPCHK(hipMemsetAsync(s.flags, 0, 16, stream));
         s.sum = dmalloc<unsigned long long>(160);
         HIPCHK(hipHostMalloc((void **)&s.hsum, 160 * 8, hipHostMallocDefault));
-        s.rcap = 1ull << 18;
+        s.rcap = 1ull << 14;
         s.R = dmalloc<uint32_t>(s.rcap);
         s.cur_off_cap = s.nxt_off_cap = 1 << 16;
         s.cur_off = dmalloc<uint64_t>(s.cur_off_cap);
@@ -900,8 +900,11 @@ struct rmc_ctx {
         if (need * 2 <= s.T_cap) return;
         uint64_t nc = s.T_cap;
         while (need * 2 > nc) nc *= 4;
-        const uint32_t full_max = cfg.compact_log2 ? cfg.compact_log2 : 27;
-        if (nc > (1ull << full_max)) { migrate_compact(s, need); return; }
+        if (nc > (1ull << full_max_log2())) {
+            migrate_compact(s, s.T_count);
+            grow_seen(s, need);
+            return;
+        }
         ulonglong2 *nT = dmalloc<ulonglong2>(nc);
         HIPCHK(hipMemsetAsync(nT, 0, nc * 16, stream));
         launch_rehash(s.T, s.T_cap, Seen{nT, nullptr, nc - 1}, stream);
@@ -909,6 +912,17 @@ struct rmc_ctx {
         dfree(s.T);
         s.T = nT;
         s.T_cap = nc;
+    }
+
+    uint32_t full_max_log2() const { return cfg.compact_log2 ? cfg.compact_log2 : 27; }
+
+    // Switch to the compact seen set now if the full one would have to grow past its limit to take
+    // `need` (a bound): callers then size their chunk on the compact table's room.
+    void maybe_migrate(Shard &s, uint64_t need) {
+        if (s.Tc || need * 2 <= s.T_cap) return;
+        uint64_t nc = s.T_cap;
+        while (need * 2 > nc) nc *= 4;
+        if (nc > (1ull << full_max_log2())) migrate_compact(s, s.T_count);
     }
 
     void migrate_compact(Shard &s, uint64_t need) {
@@ -928,12 +942,29 @@ struct rmc_ctx {
         s.Tc = Tc;
         s.T_cap = slots;
         // the run is large: the frontier ring goes to its budget and stops growing
-        const uint64_t fb = cfg.frontier_mem_bytes ? cfg.frontier_mem_bytes
-                                                   : (uint64_t)((double)free_device_bytes() * 0.7) / local;
-        const uint64_t words = std::max<uint64_t>(fb / 4, s.rcap);
-        if (words > s.rcap && !ring_realloc(s, words))
+        fix_ring(s, local);
+    }
+
+    // The frontier ring at its budget: rmc_config.frontier_mem_bytes (which may be smaller than the
+    // ring so far, down to the live frontier), else 70 % of the free device memory.
+    void fix_ring(Shard &s, uint64_t local) {
+        const uint64_t live = s.cur_words + s.nxt_words;
+        uint64_t words;
+        if (cfg.frontier_mem_bytes) {
+            words = std::max<uint64_t>(cfg.frontier_mem_bytes / 4, live + 1);
+        } else {
+            HIPCHK(hipStreamSynchronize(stream));
+            words = std::max<uint64_t>((uint64_t)((double)free_device_bytes() * 0.7) / local / 4, s.rcap);
+        }
+        if (words != s.rcap && !ring_realloc(s, words))
             throw Fail(RMC_E_MEMORY, "frontier ring of " + std::to_string(words * 4) + " B");
         s.ring_fixed = true;
+    }
+
+    // would a chunk bounded by `gub` successors fit without growing a fixed ring or a compact seen set?
+    bool seen_room(const Shard &s, uint64_t need) const { return !s.Tc || (double)need <= 0.9 * (double)s.T_cap; }
+    bool ring_room(const Shard &s, uint64_t extra, uint64_t consumed) const {
+        return !s.ring_fixed || s.cur_words + s.nxt_words - consumed + extra <= s.rcap;
     }
 
     template <class T>
@@ -1321,8 +1352,10 @@ struct rmc_ctx {
             // Small chunks size the next level, trace and seen set on the successor upper bound
             // without a host round trip; large ones read the winner count back before commit.
             const uint64_t Gub = np_ * (uint64_t)ks.maxsucc;
-            const bool small = Gub <= (1ull << 20);
+            maybe_migrate(s, s.T_count + Gub);
             const uint64_t consumed = (s.ring_fixed && p0) ? d2h(s.cur_off + p0) : 0;
+            // bounds that a fixed ring or a compact seen set cannot take go the exact way
+            const bool small = Gub <= (1ull << 20) && seen_room(s, s.T_count + Gub) && ring_room(s, np_ * MSW, consumed);
             if (small) {
                 ensure_ring(s, np_ * MSW, consumed);
                 ensure_off(s.nxt_off, s.nxt_off_cap, s.nxt_n, s.nxt_n + Gub);
@@ -1408,8 +1441,11 @@ struct rmc_ctx {
     int batch_levels() const { return cfg.device_levels ? (int)cfg.device_levels : LREC_CAP; }
     uint64_t dev_parents() const { return std::min<uint64_t>(chunk_parents, 1ull << 15); }
     bool batch_ok() const {
-        return (W == 1 || (replicated && sh[0].cur_n < shard_min)) && inited && !finished && cfg.device_levels != 1 &&
-               sh[0].cur_n > 0 && sh[0].cur_n <= dev_parents();
+        const Shard &s = sh[0];
+        const uint64_t first = s.cur_n * (uint64_t)ks.maxsucc;
+        return (W == 1 || (replicated && s.cur_n < shard_min)) && inited && !finished && cfg.device_levels != 1 &&
+               s.cur_n > 0 && s.cur_n <= dev_parents() && ring_room(s, first * (uint64_t)ks.RECW_MAX, 0) &&
+               seen_room(s, s.T_count + 2 * first);
     }
 
     // Returns the number of level stats written to out[0..maxl] (the error level included).
@@ -1419,7 +1455,13 @@ struct rmc_ctx {
         const uint64_t DP = dev_parents(), MS = (uint64_t)ks.maxsucc;
         const int K = std::max(1, std::min(maxl, LREC_CAP));
         // capacities with headroom for several levels; the first level always fits
-        const uint64_t target = std::min(std::max<uint64_t>(s.cur_n * MS * 32, 1ull << 16), DP * MS);
+        uint64_t target = std::min(std::max<uint64_t>(s.cur_n * MS * 32, 1ull << 16), DP * MS);
+        maybe_migrate(s, s.T_count + 2 * target);
+        if (!ring_room(s, s.cur_n * MS * (uint64_t)ks.RECW_MAX, 0) || !seen_room(s, s.T_count + 2 * s.cur_n * MS))
+            return 0;  // the first level no longer fits (the seen set just became compact): host-driven level
+        if (s.ring_fixed) target = std::min<uint64_t>(target, (s.rcap - s.cur_words) / (uint64_t)ks.RECW_MAX);
+        if (s.Tc) target = std::min<uint64_t>(target, ((uint64_t)(0.9 * (double)s.T_cap) - s.T_count) / 2);
+        target = std::max<uint64_t>(target, s.cur_n * MS);  // batch_ok: the first level fits
         s.nxt_words = 0;
         ensure_ring(s, target * (uint64_t)ks.RECW_MAX, 0);
         ensure_off(s.cur_off, s.cur_off_cap, s.cur_n, target);
@@ -1441,7 +1483,7 @@ struct rmc_ctx {
         h.rcap = s.rcap;
         h.trace_base = s.tdev;
         h.trace_cap = s.trace_cap;
-        h.T_cap = s.Tc ? (uint64_t)((double)s.T_cap * 0.9) * 2 / 2 : s.T_cap;
+        h.T_cap = s.Tc ? (uint64_t)((double)s.T_cap * 1.8) : s.T_cap;  // compact: load <= 0.9
         h.chunk_parents = replicated ? std::min<uint64_t>(DP, shard_min - 1) : DP;  // stop before sharding starts
         h.Lcap_max = Lcap_max;
         h.level = (uint32_t)L0;
@@ -2110,13 +2152,7 @@ struct rmc_ctx {
         s.cur_words = h.cur_words;
         s.T_count = h.T_count;
         s.epoch = std::max(s.epoch, h.epoch);
-        if (s.Tc) {  // a compact seen set means a large run: the ring goes to its budget
-            const uint64_t fb = cfg.frontier_mem_bytes ? cfg.frontier_mem_bytes
-                                                       : (uint64_t)((double)free_device_bytes() * 0.7);
-            const uint64_t words = std::max<uint64_t>(fb / 4, s.rcap);
-            if (words > s.rcap && !ring_realloc(s, words)) throw Fail(RMC_E_MEMORY, "frontier ring");
-            s.ring_fixed = true;
-        }
+        if (s.Tc) fix_ring(s, 1);  // a compact seen set means a large run: the ring goes to its budget
         total_generated = h.total_generated;
         total_distinct = h.total_distinct;
         depth = h.depth;
@@ -2248,10 +2284,7 @@ int rmc_run(void *ctx, rmc_result *res) {
         if (!c->inited) c->init(nullptr);
         std::vector<rmc_level_stats> tmp(LREC_CAP + 1);
         while (!c->finished) {
-            if (c->batch_ok())
-                c->step_batch(tmp.data(), c->batch_levels());
-            else
-                c->step(nullptr);
+            if (!c->batch_ok() || c->step_batch(tmp.data(), c->batch_levels()) == 0) c->step(nullptr);
         }
         if (res) c->result(res);
         return c->status;
@@ -2267,8 +2300,10 @@ int rmc_steps(void *ctx, rmc_level_stats *levels, uint32_t cap, uint32_t *n) {
         if (c->finished) return c->status == RMC_OK ? RMC_DONE : c->status;
         if (c->batch_ok() && cap > 1) {
             const int k = c->step_batch(levels, std::min<int>(c->batch_levels(), (int)cap - 1));
-            *n = (uint32_t)k;
-            return levels[k - 1].status;
+            if (k > 0) {
+                *n = (uint32_t)k;
+                return levels[k - 1].status;
+            }
         }
         const int rc = c->step(levels);
         *n = 1;
@@ -2322,8 +2357,8 @@ int rmc_run_levels(void *ctx, rmc_level_stats *levels, uint32_t cap, uint32_t *n
         }
         std::vector<rmc_level_stats> bt(LREC_CAP + 1);
         while (!c->finished) {
-            if (c->batch_ok()) {
-                const int k = c->step_batch(bt.data(), c->batch_levels());
+            const int k = c->batch_ok() ? c->step_batch(bt.data(), c->batch_levels()) : 0;
+            if (k > 0) {
                 for (int i = 0; i < k; i++, n++)
                     if (n < cap && levels) levels[n] = bt[i];
             } else {

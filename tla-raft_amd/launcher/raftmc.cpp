@@ -323,9 +323,12 @@ int main(int argc, char **argv) {
         std::printf("Model checking completed. No error has been found.\n");
     } else {
         if (res.status == RMC_VIOLATION) {
-            std::printf("Error: Invariant %s is violated.\n",
-                        res.violated == 0 && !pm.invariant_names.empty() ? pm.invariant_names[0].c_str()
-                                                                          : kInvNames[res.violated]);
+            // the name the cfg used for the violated invariant (Inv and LeaderHasAllCommittedEntries share bit 0)
+            std::string name = kInvNames[res.violated];
+            for (const std::string &n : pm.invariant_names)
+                if ((res.violated == 0 && (n == "Inv" || n == "LeaderHasAllCommittedEntries")) || n == kInvNames[res.violated])
+                    name = n;
+            std::printf("Error: Invariant %s is violated.\n", name.c_str());
             exit_code = 12;
         } else if (res.status == RMC_ASSERT) {
             std::printf("Error: The first argument of Assert evaluated to FALSE; the second argument was:\n\"split brain\"\n");
