@@ -10,8 +10,9 @@ buffers; inputs = the compiled spec tables, resident in HBM).
 Workload at N=1: BASELINE.json configs[1] ("3 servers, 1 value, MaxTerm=2, MaxLogLen=2 on
 one MI355X") = Raft.tla with Servers={s1,s2,s3}, Vals={v1}, MaxElection=2, MaxRestart=3,
 SYMMETRY symmServers, VIEW view, INVARIANT Inv, -deadlock (MaxTerm is
-MaxElection, MaxLogLen is |Vals|+1).  configs[2]/[3] (Raft.cfg as shipped, 5 servers) do
-not fit one GPU (>2.1e9 states by BFS level 37, still growing).
+MaxElection, MaxLogLen is |Vals|+1).  The `at_scale` key exhausts configs[0]/[2] -- Raft.cfg as
+shipped (3 servers, 2 values, MaxElection 3: 10,946,499,503 distinct states, depth 72) -- on the
+same GPU and reports its wall time and distinct states/s (N = 1 only).
 
 N>1 (torchrun, one process per GPU): the same workload is exhausted ONCE by all ranks
 together through the engine's multi-GPU mode: levels below
@@ -36,6 +37,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "tla-raft_amd"))
 
 WORKLOADS = {
+    "raftcfg": dict(n=3, V=2, E=3, R=3, desc="BASELINE configs[0]/[2]: Raft.cfg as shipped -- Raft.tla, 3 servers, "
+                                             "2 values, MaxElection 3, MaxRestart 3, SYMMETRY+VIEW, INVARIANT Inv, "
+                                             "-deadlock"),
     "c2": dict(n=3, V=1, E=2, R=3, desc="BASELINE configs[1]: Raft.tla, 3 servers, 1 value, MaxElection(=MaxTerm)=2, "
                                          "MaxRestart=3, MaxLogLen=2, SYMMETRY+VIEW, INVARIANT Inv, -deadlock"),
     "n3v2e2": dict(n=3, V=2, E=2, R=3, desc="Raft.tla, 3 servers, 2 values, MaxElection=2, MaxRestart=3 "
@@ -49,45 +53,59 @@ TIMED_PHASES = 1 << PHASES.index("expand_hash")  # HIP-event timing of the domin
 TIMING_EVERY = 4
 
 
-def alg_bytes(phase, F, G, N, S, CWB):
+def alg_bytes(phase, F, G, N, S, CCWB, slot_bytes=16, SWB=32):
     """Algorithmic HBM bytes of one phase of the fused single-GPU level (DESIGN.md "Kernels"):
-    F parents of S-byte records, G generated successors, N new states, CWB core bytes."""
-    if phase == "expand_hash":   # k_expand<FUSED>: parents in, successor count out; per successor: staged core + aux +
-        # fp + slot, one 16-B seen-set probe; per new fingerprint at least one election (16-B slot, 8-B word, count)
-        return F * S + F * 4 + G * (CWB + 16 + 16 + 4) + G * 16 + N * (16 + 8 + 4)
-    if phase == "dedup":         # k_wincount: per parent successor count, winner count (read + re-arm), its scan
-        return F * (4 + 4 + 4 + 4 + 4)
-    if phase == "materialize":   # k_commit: per parent wcnt/offsets/count + its message ids; per slot of a parent
-        # with winners its election slot + word; per new state: staging in, seen insert, trace, record out
-        return F * (4 + 8 + 4) + F * (S - CWB) + G * (4 + 8) + N * (CWB + 16 + 16 + 16 + 8 + 2 + S)
+    F parents of S-byte records (S = the run's average packed record: CCWB core bytes + message
+    ids), G generated successors, N new states; SWB = staging bytes per successor (the acting row),
+    slot_bytes = seen-set slot (16 full, 8 compact)."""
+    if phase == "expand_hash":   # k_expand<FUSED>: parents in, count + |msgs| out; per successor: staged row +
+        # fp + election slot, one seen-set probe; per new fingerprint at least one election (16-B slot, 8-B word, count)
+        return F * S + F * 8 + G * (SWB + 16 + 4) + G * slot_bytes + N * (16 + 8 + 4)
+    if phase == "dedup":         # k_wincount: per parent successor count, packed winner count (read + re-arm),
+        # |msgs|; out winner count and the two scans
+        return F * (4 + 4 + 4 + 4 + 4 + 4 + 4)
+    if phase == "materialize":   # k_commit: per parent counts/offsets + its record; per slot of a parent with
+        # winners its election slot + word; per new state: staged row + fp in, seen insert, trace, offset, record out
+        return F * (4 * 6) + F * S + G * (4 + 8) + N * (SWB + 16 + slot_bytes + 8 + 2 + 8 + S)
     return 0
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(w, budget_s=12.0):
-    """The C restatement (oracle/raft_oracle.c, single thread) on the same workload."""
-    so = os.path.join(ROOT, "oracle", "build", "libraft_oracle.so")
+    """oracle/raft_mt.c -- the C restatement of Raft.tla + TLC -workers 1 BFS semantics, level-
+    synchronous on every host core this process may use -- exhausting the same workload."""
+    so = os.path.join(ROOT, "oracle", "build", "libraft_mt.so")
     if not os.path.exists(so):
         return None
     lib = ctypes.CDLL(so)
-    lib.orc_create.restype = ctypes.c_void_p
-    lib.orc_create.argtypes = [ctypes.c_int] * 6 + [ctypes.c_uint32, ctypes.c_int]
-    lib.orc_run.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    lib.orc_distinct.restype = ctypes.c_uint64
-    lib.orc_distinct.argtypes = [ctypes.c_void_p]
-    lib.orc_destroy.argtypes = [ctypes.c_void_p]
+    lib.orc_mt_run.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_uint64)] * 2 + [ctypes.POINTER(ctypes.c_int)]
+    # the host cores this job may use: the box's share (OMP_NUM_THREADS is set to it on the GPU
+    # boxes; the affinity mask there shows the whole machine)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
     runs, states = 0, 0
+    d, g, dep = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
-        h = lib.orc_create(w["n"], w["V"], w["E"], w["R"], 0, 0, 1, 0)
-        lib.orc_run(h, 0)
-        states += lib.orc_distinct(h)
-        lib.orc_destroy(h)
+        rc = lib.orc_mt_run(w["n"], w["V"], w["E"], w["R"], threads, ctypes.byref(d), ctypes.byref(g), ctypes.byref(dep))
+        assert rc == 0
+        states += d.value
         runs += 1
     dt = time.perf_counter() - t0
-    return {"value": states / dt, "unit": "distinct states/s", "cores": 1, "kind": "port",
-            "sample": f"{runs} full exhaustions of the same workload by oracle/raft_oracle.c "
-                      f"(C restatement of Raft.tla + TLC -workers 1 BFS, exact canonical forms; not TLC: "
-                      f"no JVM/tla2tools.jar on the box), {dt:.1f} s"}
+    return {"value": states / dt, "unit": "distinct states/s", "cores": threads, "cpu_model": cpu_model(),
+            "kind": "port",
+            "sample": f"{runs} full exhaustions ({d.value} distinct, {g.value} generated, depth {dep.value}) of the "
+                      f"same workload by oracle/raft_mt.c on {threads} threads (C restatement of Raft.tla, exact "
+                      f"canonical forms, level-synchronous first-wins BFS; not TLC: no JVM/tla2tools.jar on the "
+                      f"box), {dt:.1f} s"}
 
 
 def main():
@@ -187,20 +205,29 @@ def main():
     value = units * args.steps / elapsed
 
     # dominant kernel phase: the one with the most device time (HIP events on the engine's stream)
-    S, CWB = record_bytes(mc)
+    S, CCWB = record_bytes(res, mc.cfg)
+    slot_b = res.seen_slot_bytes or 16
     dom = max(range(4), key=lambda i: phase_ms[i])
     per_launch_ms = phase_ms[dom] / max(1, launches[dom])
-    bytes_total = alg_bytes(PHASES[dom], Fs, Gs, Ns, S, CWB)
+    bytes_total = alg_bytes(PHASES[dom], Fs, Gs, Ns, S, CCWB, slot_b, staging_bytes(mc.cfg))
     achieved = bytes_total / max(1, launches[dom]) / (per_launch_ms / 1e3) / 1e9 if per_launch_ms > 0 else 0.0
-    traffic, pmc_src = pmc_traffic(mc, PHASES[dom], args.workload, res.depth)
+    pmc = pmc_kernel(mc, PHASES[dom], args.workload, res.depth)
     roof = {"bound": "hbm", "kernel": PHASES[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-            "traffic_source": pmc_src,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc.get("traffic"),
+            "traffic_source": pmc.get("source"),
             "algorithmic_bytes_per_launch": round(bytes_total / max(1, launches[dom])),
             "avg_launch_ms": round(per_launch_ms, 5), "launches": launches[dom],
             "timed_steps": len(range(0, args.steps, TIMING_EVERY)),
+            "record_bytes_avg": round(S, 2), "seen_slot_bytes": slot_b,
             "phase_ms_per_step": {PHASES[i]: round(phase_ms[i] / len(range(0, args.steps, TIMING_EVERY)), 4)
                                   for i in range(4)}}
+    if pmc.get("valu_insts") and per_launch_ms > 0:
+        # the binding limit of the expansion kernel: VALU issue.  A wave64 VALU instruction occupies a
+        # SIMD-32 for 2 cycles (MI355X_MICROARCH.md constants table): peak = CUs x 4 SIMDs x clock / 2
+        rate = pmc["valu_insts"] / (per_launch_ms / 1e3)
+        roof["valu"] = {"insts_per_launch": round(pmc["valu_insts"]), "achieved_insts_per_s": round(rate),
+                        "peak_insts_per_s": VALU_PEAK, "frac": round(rate / VALU_PEAK, 4),
+                        "source": pmc.get("source")}
     # seen-set probe throughput of the run (one probe per generated successor in the expansion
     # pass, one insert per new state in commit) against the random-probe peak of the same slot
     # layout measured on this GPU: a table the size of the run's (2^22 slots, L2/MALL-resident)
@@ -235,7 +262,7 @@ def main():
         "seen_set": seen,
     }
     if rank == 0 and world == 1 and not args.no_scale:
-        line["at_scale"] = at_scale(local, S, CWB)
+        line["at_scale"] = at_scale(local)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(w)
     if rank == 0:
@@ -245,41 +272,50 @@ def main():
         dist.destroy_process_group()
 
 
-def at_scale(device, S, CWB, workload="n3v2e2"):
-    """One exhaustion of a larger configuration (not the headline): levels of up to ~10^6 states,
-    where the level loop is throughput-bound rather than latency-bound.  Reports the run's
-    distinct states/s and the fused expansion kernel's algorithmic GB/s over the whole run."""
+def at_scale(device, workload="raftcfg"):
+    """configs[0]/[2] -- Raft.cfg as shipped -- exhausted on this GPU (not the headline: one run is
+    ~75 s).  The first run includes growing every buffer (the seen set's move to 8-B slots, the
+    frontier ring, the pinned host trace); the second, after rmc_reset, is the steady state.  Its
+    first 30 levels are compared with the C oracle's (tests/golden/levels_prefix.json)."""
     import raftmc
     w = WORKLOADS[workload]
     cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
                              invariants=("Inv",), check_deadlock=False, device=device, timing_phases=TIMED_PHASES)
     with raftmc.ModelChecker(cfg) as mc:
-        mc.set_timing(0)
-        mc.run()  # warm: buffers grown to the run's size
+        mc.set_timing(TIMED_PHASES)
+        t0 = time.perf_counter()
+        cold = mc.run()
+        dt_cold = time.perf_counter() - t0
         mc.reset()
+        mc.set_timing(0)
         t0 = time.perf_counter()
         res = mc.run()
         dt = time.perf_counter() - t0
-        mc.reset()
-        mc.set_timing(TIMED_PHASES)
-        timed = mc.run()
-    ms = sum(ls.kernel_ms[PHASES.index("expand_hash")] for ls in timed.levels)
-    F = sum(ls.expanded for ls in timed.levels)
-    G = sum(ls.generated for ls in timed.levels)
-    N = sum(ls.new_states for ls in timed.levels)
-    gbs = alg_bytes("expand_hash", F, G, N, S, CWB) / (ms / 1e3) / 1e9 if ms > 0 else 0.0
-    # the C oracle's full BFS of the same configuration (tests/golden/make_golden_big.py): data only
+    ms = sum(ls.kernel_ms[PHASES.index("expand_hash")] for ls in cold.levels)
+    F = sum(ls.expanded for ls in cold.levels)
+    G = sum(ls.generated for ls in cold.levels)
+    N = sum(ls.new_states for ls in cold.levels)
+    S, CCWB = record_bytes(cold, cfg)
+    gbs = alg_bytes("expand_hash", F, G, N, S, CCWB, cold.seen_slot_bytes, staging_bytes(cfg)) / (ms / 1e3) / 1e9 \
+        if ms > 0 else 0.0
     gold = {}
-    gpath = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden", "levels_big.json")
+    gpath = os.path.join(ROOT, "tests", "golden", "levels_prefix.json")
     if os.path.exists(gpath):
         with open(gpath) as f:
             gold = json.load(f).get(f"n{w['n']}_v{w['V']}_e{w['E']}_r{w['R']}", {})
-    match = (res.distinct, res.generated, res.depth) == (gold.get("distinct"), gold.get("generated"),
-                                                         gold.get("depth")) if gold else None
+    match = None
+    if gold:
+        got = [ls.new_states for ls in res.levels]
+        match = got[:len(gold["levels"])] == gold["levels"]
     return {"workload": w["desc"], "distinct_states": res.distinct, "states_generated": res.generated,
-            "matches_c_oracle_golden": match,
-            "depth": res.depth, "seconds": round(dt, 4), "distinct_per_s": round(res.distinct / dt, 1),
+            "depth": res.depth, "verdict": "Inv holds" if res.status == "done" else res.status,
+            "seconds_to_exhaust": round(dt, 3), "distinct_per_s": round(res.distinct / dt, 1),
             "generated_per_s": round(res.generated / dt, 1),
+            "first_run_seconds_incl_allocation": round(dt_cold, 3),
+            "matches_c_oracle_prefix_levels": match, "c_oracle_prefix_levels": len(gold.get("levels", [])),
+            "seen_set": f"{res.seen_slots} x {res.seen_slot_bytes} B slots",
+            "frontier_ring_bytes": res.frontier_ring_bytes, "frontier_peak_bytes": res.frontier_peak_bytes,
+            "record_bytes_avg": round(S, 2),
             "expand_kernel_ms": round(ms, 3), "expand_alg_GBps": round(gbs, 1),
             "expand_frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
 
@@ -290,35 +326,54 @@ KERNEL_NAME = {"expand_hash": "void rmc::k_expand<{n}, {V}, {mr}, 4>(rmc::KParam
 
 
 PMC_RUNS = 6  # tools/pmc.sh: bench.py --steps 5 --warmup 1 per counter pass
+VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions per second on MI355X
 
 
-def pmc_traffic(mc, phase, workload, depth):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary
-    (tools/pmc.sh + tools/pmc_summary.py, FETCH_SIZE x2 correction per MI355X_MICROARCH.md)."""
+def pmc_kernel(mc, phase, workload, depth):
+    """Per launch of the dominant kernel, from the committed rocprofv3 PMC summary
+    (tools/pmc.sh + tools/pmc_summary.py): HBM bytes (FETCH_SIZE x2 correction per
+    MI355X_MICROARCH.md + WRITE_SIZE) and VALU wave-instructions (SQ_INSTS_VALU)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}.json")))
     if not files or phase not in KERNEL_NAME:
-        return None, None
+        return {}
     n, V = mc.cfg.n_servers, mc.cfg.n_vals
     mr = 1 if (mc.cfg.msg_cap or (64 if n <= 3 else 128)) <= 64 else 2
     name = KERNEL_NAME[phase].format(n=n, V=V, mr=mr)
     d = json.load(open(files[-1]))
     e = d.get(name)
-    if not e or "hbm_bytes_per_dispatch" not in e:
-        return None, None
+    if not e:
+        return {}
     # the device-driven level loop enqueues a few levels past the last one, whose launches
-    # return at once: spread the pass's bytes over the launches that expanded a level
+    # return at once: spread each pass's totals over the launches that expanded a level
     real = PMC_RUNS * depth
-    per = e["hbm_bytes_per_dispatch"] * e["dispatches"] / real if e["dispatches"] >= real else e["hbm_bytes_per_dispatch"]
-    return round(per), os.path.relpath(files[-1], ROOT)
+    scale = e["dispatches"] / real if e["dispatches"] >= real else 1.0
+    out = {"source": os.path.relpath(files[-1], ROOT)}
+    if "hbm_bytes_per_dispatch" in e:
+        out["traffic"] = round(e["hbm_bytes_per_dispatch"] * scale)
+    if "SQ_INSTS_VALU" in e:
+        out["valu_insts"] = e["SQ_INSTS_VALU"] * scale
+    return out
 
 
-def record_bytes(mc):
-    """(bytes of one packed state record, bytes of its core words), rmc_spec.h Layout."""
-    n = mc.cfg.n_servers
-    cw = (7 + 3 * n + 3) // 4 * 4
-    mcap = mc.cfg.msg_cap or (64 if n <= 3 else 128)
-    return cw * 4 + 2 * mcap, cw * 4
+def codec_words(n, V):
+    """Packed core words (rmc_spec.h Codec<N, V>::CCW)."""
+    bits_for = lambda m: 0 if m <= 0 else m.bit_length()
+    b_ix, b_ni, b_ent = bits_for(V + 1), bits_for(V + 2), 3 + bits_for(V - 1)
+    bits = n * (bits_for(n) + 3 + 2 + 2 * b_ix) + n * V * b_ent + n * n * (b_ix + b_ni) + n * n + 3 + 4 + V + 8
+    return (bits + 31) // 32
+
+
+def staging_bytes(cfg):
+    return 48 if cfg.n_servers >= 4 else 32  # Spec::SW4 uint4s per successor slot
+
+
+def record_bytes(res, cfg):
+    """(average bytes of the run's packed frontier records, bytes of the packed core)."""
+    nb = sum(ls.new_bytes for ls in res.levels)
+    ns = sum(ls.new_states for ls in res.levels)
+    ccwb = 4 * codec_words(cfg.n_servers, cfg.n_vals)
+    return (nb / ns if ns else float(ccwb)), ccwb
 
 
 if __name__ == "__main__":

@@ -23,6 +23,7 @@ def load(name):
 
 LEVELS = load("levels.json")
 LEVELS_BIG = load("levels_big.json") if os.path.exists(os.path.join(GOLDEN, "levels_big.json")) else {}
+PREFIX = load("levels_prefix.json") if os.path.exists(os.path.join(GOLDEN, "levels_prefix.json")) else {}
 SAMPLES = load("successors.json")
 TRACES = load("traces.json")
 
@@ -194,6 +195,31 @@ def test_bfs_matches_golden_levels_at_scale(name):
     mc, res = run_cfg(g)
     check_levels(g, res)
     mc.close()
+
+
+# Raft.cfg as shipped (Raft.cfg:1-34 under myrun.sh:3): the exhaustion recorded on MI355X
+# (profiles/r02_explore_raftcfg_levels.txt, profiles/r02_myrun_raftcfg_raft.txt).  Beyond the C
+# oracle's prefix these totals are this checker's own (TLC cannot run here: parity unpinned).
+RAFT_CFG_TOTALS = dict(distinct=10946499503, generated=56936653204, depth=72)
+
+
+def test_raft_cfg_exhausted_and_prefix_matches_c_oracle():
+    """configs[0]/[2]: Raft.cfg as shipped (3 servers, 2 values, MaxElection 3, MaxRestart 3) exhausted
+    on one GPU -- the large-run storage (compact seen set, frontier ring, host trace) end to end.  The
+    first 30 levels (211M states) equal the C oracle's level by level, distinct and generated."""
+    g = PREFIX["n3_v2_e3_r3"]
+    for mc in _cache.values():  # the run takes most of the device's memory
+        mc.close()
+    _cache.clear()
+    with raftmc.ModelChecker(raftmc.ModelConfig(n_servers=3, n_vals=2, max_election=3, max_restart=3)) as mc:
+        res = mc.run()
+    got = [ls.new_states for ls in res.levels]
+    assert got[:len(g["levels"])] == g["levels"]
+    assert [ls.generated for ls in res.levels[1:len(g["gen_per_level"]) + 1]] == g["gen_per_level"]
+    assert res.status == "done" and res.queue == 0
+    assert (res.distinct, res.generated, res.depth) == (RAFT_CFG_TOTALS["distinct"], RAFT_CFG_TOTALS["generated"],
+                                                        RAFT_CFG_TOTALS["depth"])
+    assert res.seen_slot_bytes == 8
 
 
 @pytest.mark.parametrize("name", sorted(TRACES))

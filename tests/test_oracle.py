@@ -180,3 +180,23 @@ def test_follower_append_entry_variant_is_raft(n, V, E, Rr):
     assert R.FAPP_STATS["reached_unchanged"] > 0 and R.FAPP_STATS["enabled"] == 0
     assert (var.verdict, var.generated, var.distinct, var.depth, var.levels, var.generated_per_level) == (
         base.verdict, base.generated, base.distinct, base.depth, base.levels, base.generated_per_level)
+
+
+def test_multithreaded_cpu_baseline_matches_golden():
+    """oracle/raft_mt.c (bench.py's cpu_baseline: the same restatement on all host cores, level-
+    synchronous with first-wins election) reaches the single-threaded oracle's counts."""
+    import ctypes
+    so = os.path.join(ROOT, "oracle", "build", "libraft_mt.so")
+    if not os.path.exists(so):
+        pytest.skip("oracle/build/libraft_mt.so not built")
+    lib = ctypes.CDLL(so)
+    lib.orc_mt_run.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_uint64)] * 2 + [ctypes.POINTER(ctypes.c_int)]
+    levels = json.load(open(os.path.join(GOLDEN, "levels.json")))
+    for name in ("n3_v1_e1_r3", "n3_v2_e1_r3", "n2_v2_e3_r3", "n4_v1_e1_r3", "n3_v1_e2_r1"):
+        g = levels[name]
+        for threads in (1, 3, 8):
+            d, gen, dep = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+            rc = lib.orc_mt_run(g["n"], g["V"], g["E"], g["R"], threads, ctypes.byref(d), ctypes.byref(gen),
+                                ctypes.byref(dep))
+            assert rc == 0
+            assert (d.value, gen.value, dep.value) == (g["distinct"], g["generated"], g["depth"]), (name, threads)

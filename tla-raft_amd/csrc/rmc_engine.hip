@@ -265,7 +265,7 @@ struct Shard {
     ulonglong2 *T = nullptr;
     unsigned long long *Tc = nullptr;
     uint64_t T_cap = 0, T_count = 0;
-    Seen seen() const { return Seen{Tc ? nullptr : T, Tc, T_cap - 1}; }
+    Seen seen() const { return Seen{Tc ? nullptr : T, Tc, Tc ? 0 : T_cap - 1, T_cap}; }
     // trace: parent reference (shard << 48 | local gid) + slot key per local gid; the device
     // buffers hold gids from tflushed on, the host arrays everything before
     uint64_t *par = nullptr;
@@ -907,7 +907,7 @@ struct rmc_ctx {
         }
         ulonglong2 *nT = dmalloc<ulonglong2>(nc);
         HIPCHK(hipMemsetAsync(nT, 0, nc * 16, stream));
-        launch_rehash(s.T, s.T_cap, Seen{nT, nullptr, nc - 1}, stream);
+        launch_rehash(s.T, s.T_cap, Seen{nT, nullptr, nc - 1, nc}, stream);
         HIPCHK(hipStreamSynchronize(stream));
         dfree(s.T);
         s.T = nT;
@@ -929,14 +929,13 @@ struct rmc_ctx {
         const uint64_t local = sh.size();
         HIPCHK(hipStreamSynchronize(stream));
         const uint64_t budget = cfg.seen_mem_bytes ? cfg.seen_mem_bytes : free_device_bytes() / 2 / local;
-        uint64_t slots = 1;
-        while (slots * 2 * 8 <= budget) slots *= 2;
+        const uint64_t slots = budget / 8 / 64 * 64;
         if ((double)need > 0.85 * (double)slots)
             throw Fail(RMC_E_MEMORY, "seen set: " + std::to_string(need) + " fingerprints do not fit the budget of " +
                                          std::to_string(budget) + " B");
         unsigned long long *Tc = dmalloc<unsigned long long>(slots);
         HIPCHK(hipMemsetAsync(Tc, 0, slots * 8, stream));
-        launch_rehash(s.T, s.T_cap, Seen{nullptr, Tc, slots - 1}, stream);
+        launch_rehash(s.T, s.T_cap, Seen{nullptr, Tc, 0, slots}, stream);
         HIPCHK(hipStreamSynchronize(stream));
         dfree(s.T);
         s.Tc = Tc;
@@ -2095,7 +2094,8 @@ struct rmc_ctx {
             throw Fail(RMC_E_ARG, std::string("resume: ") + path + " was written with another fingerprint scheme");
         }
         // the header's own consistency, before anything is allocated from it
-        if (h.check != header_check(h) || h.n_levels == 0 || h.n_levels > 100000 || (h.T_cap & (h.T_cap - 1)) != 0 ||
+        if (h.check != header_check(h) || h.n_levels == 0 || h.n_levels > 100000 ||
+            (!h.compact && (h.T_cap & (h.T_cap - 1)) != 0) || h.T_cap == 0 ||
             h.T_count >= h.T_cap || h.T_count > h.trace_n || h.cur_words > h.cur_n * (uint64_t)RECW ||
             h.cur_words < h.cur_n * (uint64_t)ks.CCW) {
             std::fclose(f);

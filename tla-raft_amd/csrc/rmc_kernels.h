@@ -21,11 +21,13 @@ struct Tables {
 //   full:    16-B slots {x, y} (T != nullptr), grown x4 by rehash while small;
 //   compact:  8-B slots holding x only (Tc != nullptr): the slot's probe run, which starts at the
 //             home index derived from y, carries the rest of the identity.  Used once the run is
-//             large (rmc_config.compact_log2); sized once from the memory budget, never grown.
+//             large (rmc_config.compact_log2); sized once from the memory budget (any slot count:
+//             the home slot is the high half of hash * cap), never grown.
 struct Seen {
     ulonglong2 *T;
     unsigned long long *Tc;
-    uint64_t mask;
+    uint64_t mask;  // full table: slots - 1 (a power of two)
+    uint64_t cap;   // slots; the compact table may have any number (home slot by multiply-shift)
 };
 
 enum ErrSlot { ERR_ASSERT = 0, ERR_DEADLOCK = 1, ERR_INV = 2, ERR_EVAL = 3, ERR_NSLOTS = 4 };
@@ -98,12 +100,11 @@ struct KParams {
     uint32_t *xrec;
     // fused single-shard level: expand (+hash, +seen-set probe, +election, +staging) -> wincount
     // -> commit.  Successor slot q = (p - p_begin) * maxsucc + rank is sparse and increases in
-    // TLC order; it indexes fp, lslot, score (packed core words, CCW4 uint4 each) and saux
-    // {key | nadd << 16, add0 | add1 << 16, add2 | add3 << 16, 0}.  wpos / wposw are then the
-    // exclusive scans of winners / their record words per parent inside each WTILE-parent tile,
-    // and a parent's first winner lands at boff[tile] + wpos (words boffw[tile] + wposw).
+    // TLC order; it indexes fp, lslot and score (the staged successor: its acting server's row,
+    // slot key and added message ids, Spec::SW4 uint4 each; stage_succ).  wpos / wposw are then
+    // the exclusive scans of winners / their record words per parent inside each WTILE-parent
+    // tile, and a parent's first winner lands at boff[tile] + wpos (words boffw[tile] + wposw).
     uint4 *score;
-    uint4 *saux;
     uint32_t *lslot;           // LS_SEEN, LS_ELECT, or the election slot in L
     unsigned long long *L;     // chunk election table: sharded path (epoch << 32) | q; fused path
                                // the election word ((0xFFFFFFFF - epoch) << 32) | q << 2 | e (elect_key)

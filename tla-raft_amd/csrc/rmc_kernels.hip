@@ -770,16 +770,26 @@ __device__ __forceinline__ uint64_t t_index(const ulonglong2 f, uint64_t mask) {
     return (f.y ^ (f.y >> 29) ^ (f.x >> 23)) & mask;
 }
 
+// Home slot of the compact table: multiply-shift of a remixed word (any cap).  The remix matters:
+// y is a minimum over Permutations(Servers), so its high bits are far from uniform (the smallest of
+// 6 -- or 120 -- hashes), and multiply-shift reads the high bits.
+__device__ __forceinline__ uint64_t t_home_c(const ulonglong2 f, uint64_t cap) {
+    uint64_t z = (f.y ^ (f.x >> 17)) * 0x9e3779b97f4a7c15ull;
+    z ^= z >> 29;
+    return __umul64hi(z, cap);
+}
+
 __device__ __forceinline__ bool seen_contains(const Seen &S, ulonglong2 f) {
-    uint64_t h = t_index(f, S.mask);
     if (S.Tc) {
+        uint64_t h = t_home_c(f, S.cap);
         for (;;) {
             const unsigned long long e = S.Tc[h];
             if (e == 0ull) return false;
             if (e == f.x) return true;
-            h = (h + 1) & S.mask;
+            h = (h + 1 == S.cap) ? 0 : h + 1;
         }
     }
+    uint64_t h = t_index(f, S.mask);
     for (;;) {
         const ulonglong2 e = S.T[h];
         if (e.x == 0ull) return false;
@@ -790,13 +800,14 @@ __device__ __forceinline__ bool seen_contains(const Seen &S, ulonglong2 f) {
 
 // keys inserted are never already present (winners are new, rehash moves distinct keys)
 __device__ __forceinline__ void seen_insert(const Seen &S, ulonglong2 f) {
-    uint64_t h = t_index(f, S.mask);
     if (S.Tc) {
+        uint64_t h = t_home_c(f, S.cap);
         for (;;) {
             if (atomicCAS(&S.Tc[h], 0ull, (unsigned long long)f.x) == 0ull) return;
-            h = (h + 1) & S.mask;
+            h = (h + 1 == S.cap) ? 0 : h + 1;
         }
     }
+    uint64_t h = t_index(f, S.mask);
     for (;;) {
         unsigned long long prev = atomicCAS((unsigned long long *)&S.T[h].x, 0ull, (unsigned long long)f.x);
         if (prev == 0ull) { S.T[h].y = f.y; return; }
