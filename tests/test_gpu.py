@@ -432,3 +432,87 @@ def test_launcher_checkpoint_and_recover(tmp_path):
     assert r2.returncode == 0, r2.stdout + r2.stderr
     assert "Recovery completed" in r2.stdout and want in r2.stdout
     assert f"The depth of the complete state graph search is {g['depth']}." in r2.stdout
+
+
+# ---- error paths and the TLC-style output ----------------------------------------------------
+def _leader_with_same_term_append_req():
+    """s1 leads at term 1 while s2 (also at term 1) has sent it an AppendReq: UpdateTerm(s1)'s
+    second disjunct evaluates Assert(role[s1] # Leader, "split brain") (Raft.tla:183-185)."""
+    req = R.append_req(1, 0, 1, 1, 0, (), 1)
+    return R.State(votedFor=(0, 1, -1), currentTerm=(1, 1, 1), logs=(((0, -1),),) * 3,
+                   matchIndex=((1, 1, 1),) * 3, nextIndex=((2, 2, 2),) * 3, commitIndex=(1, 1, 1),
+                   msgs=frozenset([req]), role=(R.LEADER, R.LEADER, R.FOLLOWER), electionCount=2, restartCount=0,
+                   pendingResponse=((False,) * 3,) * 3, valSent=(-1,))
+
+
+def test_assert_split_brain_through_the_kernels():
+    """The HIP expansion reports the Assert of Raft.tla:185 exactly where the oracle raises it."""
+    cfg = R.Config(n=3, V=1, max_election=2, max_restart=3)
+    st = _leader_with_same_term_append_req()
+    with pytest.raises(R.AssertionFailure):
+        R.successors(cfg, st)
+    mc = checker(3, 1, 2, 3)
+    with pytest.raises(AssertionError, match="split brain"):
+        mc.successors(R.state_to_json(st))
+    # the same message at a higher term takes UpdateTerm's first disjunct: no Assert, same successors
+    st2 = dataclasses.replace(st, msgs=frozenset([R.append_req(1, 0, 2, 1, 0, (), 1)]), currentTerm=(1, 2, 1))
+    exp = R.successors(cfg, st2)
+    got = mc.successors(R.state_to_json(st2))
+    assert [list(k) for k, _, _ in got] == [list(k) for k, _ in exp]
+    assert [g[1] for g in got] == [R.state_to_json(t) for _, t in exp]
+
+
+def test_eval_error_through_successor_invariants():
+    """A state whose Inv evaluation leaves logs[p]'s domain (Raft.tla:499) gives the TLC evaluation
+    error through the kernels' invariant code, and a leader-free state does not."""
+    mc = checker(3, 2, 3, 3)
+    bad = R.State((-1, -1, -1), (1, 1, 1), (((0, -1), (1, 0), (1, 1)), ((0, -1), (1, 0)), ((0, -1),)),
+                  ((1, 1, 1),) * 3, ((2, 2, 2),) * 3, (1, 3, 1), frozenset(), (2, 0, 0), 0, 0,
+                  ((False,) * 3,) * 3, (0, 0))
+    cfg = R.Config(n=3, V=2, max_election=3, max_restart=3)
+    with pytest.raises(R.EvalError):
+        R.INV_FUNCS["Inv"](cfg, bad)
+    assert mc.eval_invariant(R.state_to_json(bad), "Inv") is None
+    ok = dataclasses.replace(bad, role=(0, 0, 0))
+    assert mc.eval_invariant(R.state_to_json(ok), "Inv") is True
+
+
+def test_launcher_prints_tlc_counterexample(tmp_path):
+    """raftmc on the seeded spec: TLC's error line, then every State k block -- the action and all 12
+    variables in TLA+ syntax -- equal to the oracle's counterexample rendered the same way."""
+    import subprocess
+    from test_host import LAUNCHER, cfg_text
+    from tla_render import render_state
+    g, t = LEVELS["seeded_n3_v1_e2_r3"], TRACES["seeded_n3_v1_e2_r3"]
+    (tmp_path / "RaftSeeded.cfg").write_text(cfg_text(E=2, R=3, vals="v1"))
+    env = dict(os.environ, RMC_SKIP_SPEC_CHECK="1")
+    r = subprocess.run([LAUNCHER, "-deadlock", "-workers", "4", "-config", str(tmp_path / "RaftSeeded.cfg"),
+                        str(tmp_path / "RaftSeeded.tla")], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 12, r.stdout + r.stderr
+    out = r.stdout.splitlines()
+    assert "Error: Invariant Inv is violated." in out
+    assert "Error: The behavior up to this point is:" in out
+    # State blocks; msgs continuation lines ("   [..]") belong to the msgs line
+    blocks, cur = [], None
+    for line in out:
+        if line.startswith("State "):
+            cur = [line]
+            blocks.append(cur)
+        elif cur is not None and line.startswith("/\\ "):
+            cur.append(line)
+        elif cur is not None and line.startswith("   ["):
+            cur[-1] += " " + line.strip()
+        elif cur is not None and not line.strip():
+            cur = None
+    assert len(blocks) == len(t["steps"]) == g["trace_len"]
+    actions = raftmc.ACTIONS
+    for k, (blk, step) in enumerate(zip(blocks, t["steps"])):
+        if step["key"] is None:
+            assert blk[0] == f"State {k + 1}: <Initial predicate>"
+        else:
+            srv, act, _ = step["key"]
+            assert blk[0] == f"State {k + 1}: <{actions[act]}(s{srv + 1})>", blk[0]
+        want = render_state(step["state"], ["s1", "s2", "s3"], ["v1"])
+        assert [l.replace(",  [", ", [") for l in blk[1:]] == want, (k, blk[1:], want)
+    assert f"{g['generated']} states generated, {g['distinct']} distinct states found, " \
+           f"{g['queue_left']} states left on queue." in out
