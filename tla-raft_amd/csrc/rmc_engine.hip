@@ -663,7 +663,7 @@ struct rmc_ctx {
         d_seeds = dmalloc<uint64_t>(seeds.size());
         HIPCHK(hipMemcpy(d_seeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
         // fingerprint scheme identity (checkpoints): seeds, message hashes, record codec, slot hash
-        scheme_hash = 0x5eed5c4e3e000003ull;
+        scheme_hash = 0x5eed5c4e3e000004ull;  // 4: signature-coset minimum for n >= 4
         auto mixin = [&](uint64_t v) { scheme_hash = mix64(scheme_hash ^ (v + 0x9e3779b97f4a7c15ull)); };
         for (uint64_t s : seeds) mixin(s);
         for (const ulonglong2 &g : U.gmsg) { mixin(g.x); mixin(g.y); }

@@ -26,6 +26,32 @@
 
 #include "rmc_kernels.h"
 
+// waves per SIMD the n >= 4 / two-round expansion kernel is compiled for (register budget)
+// phase profile (tools/phase_prof.py): a build with -DRMC_PHASE_PROF adds up, per phase of
+// k_expand, the shader clock its waves spend there (lane 0 of each wave, flushed once per wave)
+#ifdef RMC_PHASE_PROF
+__device__ unsigned long long g_phase[8];
+#define PHASE_DECL unsigned long long _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; long long _tp = clock64();
+#define PHASE(k) do { const long long _t = clock64(); _acc[k] += (unsigned long long)(_t - _tp); _tp = _t; } while (0)
+#define PHASE_FLUSH do { if (threadIdx.x == 0) for (int _k = 0; _k < 8; _k++) atomicAdd(&g_phase[_k], _acc[_k]); } while (0)
+extern "C" int rmc_debug_phases(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 8;
+}
+#else
+#define PHASE_DECL
+#define PHASE(k) do {} while (0)
+#define PHASE_FLUSH do {} while (0)
+#endif
+
+#ifndef RMC_WIDE_WAVES
+#define RMC_WIDE_WAVES 2
+#endif
+
 namespace rmc {
 
 enum Mode { M_COUNT = 0, M_HASH = 1, M_MAT = 2, M_SINGLE = 3, M_FUSED = 4 };
@@ -307,6 +333,105 @@ __device__ __forceinline__ int check_invs(const uint32_t *c, uint32_t order, int
     return 1;
 }
 
+// ---- signature pre-sort (n >= 4) ----------------------------------------------------------
+// The fingerprint is min over permutations pi of H(pi), H = sum_s Z(pi(s), U[s]) +
+// sum_{s != j} Z(pi(s), pi(j), X[s][j]).  Any permutation-equivariant signature of a server
+// (a function of its data that does not name other servers) orders the servers; taking the
+// minimum only over the permutations that send the servers to their signature-sorted
+// positions (the coset fixed by the signature ties) is still constant on every symmetry class
+// (Raft.tla:21 SYMMETRY): for y = sigma(x) the allowed set of y is that of x composed with
+// sigma^-1.  The signature is the server's own word plus the sum of its outgoing pair inputs
+// (its message hashes to each peer, matchIndex / nextIndex / vote for that peer), mixed.
+constexpr uint64_t SIG_KU = 0x2545f4914f6cdd1dull, SIG_KX = 0x9fb21c651e98df25ull;
+__device__ __forceinline__ uint64_t sig_part_u(uint64_t u) { return mix64(u ^ SIG_KU); }
+__device__ __forceinline__ uint64_t sig_part_x(uint64_t x) { return mix64(x ^ SIG_KX); }
+
+// per server t, 6 bits: lo_t (servers with a smaller signature) | (ties_t - 1) << 3
+template <int N>
+__device__ __forceinline__ uint32_t coset_ranks(const uint64_t *sig) {
+    uint32_t rk = 0;
+#pragma unroll
+    for (int t = 0; t < N; t++) {
+        uint32_t lo = 0, eq = 0;
+#pragma unroll
+        for (int u = 0; u < N; u++) {
+            lo += sig[u] < sig[t] ? 1u : 0u;
+            eq += (u != t && sig[u] == sig[t]) ? 1u : 0u;
+        }
+        rk |= (lo | (eq << 3)) << (6 * t);
+    }
+    return rk;
+}
+__device__ __forceinline__ uint32_t small_fact(uint32_t g) {
+    return g <= 1 ? 1u : g == 2 ? 2u : g == 3 ? 6u : g == 4 ? 24u : 120u;
+}
+// number of allowed permutations: product over tie groups of |group|!
+template <int N>
+__device__ __forceinline__ uint32_t coset_size(uint32_t rk) {
+    uint32_t K = 1;
+#pragma unroll
+    for (int t = 0; t < N; t++) {
+        const uint32_t lo = (rk >> (6 * t)) & 7u, g = ((rk >> (6 * t + 3)) & 7u) + 1u;
+        bool head = true;
+#pragma unroll
+        for (int u = 0; u < t; u++) head &= ((rk >> (6 * u)) & 7u) != lo;
+        if (head) K *= small_fact(g);
+    }
+    return K;
+}
+// the k-th allowed permutation (k < coset_size): tie groups in server order, each group's
+// members (in server order) take the positions [lo, lo + g) in the k-th arrangement
+// (factorial number system, group by group)
+template <int N>
+__device__ __forceinline__ void coset_img(uint32_t rk, uint32_t k, uint32_t *img) {
+#pragma unroll
+    for (int t = 0; t < N; t++) {
+        const uint32_t lo = (rk >> (6 * t)) & 7u, g = ((rk >> (6 * t + 3)) & 7u) + 1u;
+        bool head = true;
+#pragma unroll
+        for (int u = 0; u < t; u++) head &= ((rk >> (6 * u)) & 7u) != lo;
+        if (!head) continue;
+        const uint32_t gf = small_fact(g);
+        uint32_t kg = k % gf;
+        k /= gf;
+        uint32_t avail = (1u << g) - 1u, i = 0;
+#pragma unroll
+        for (int u = t; u < N; u++) {
+            if (((rk >> (6 * u)) & 7u) != lo) continue;
+            const uint32_t f = small_fact(g - 1u - i);
+            uint32_t d = kg / f;
+            kg -= d * f;
+            uint32_t m = avail;
+            for (; d; d--) m &= m - 1u;
+            const uint32_t pos = (uint32_t)__builtin_ctz(m);
+            avail &= ~(1u << pos);
+            img[u] = lo + pos;
+            i++;
+        }
+    }
+}
+// H_f at one permutation from per-server inputs: u(t), x(f, t, j), seeds sS(f, a), sP(f, a, b)
+template <int N, class FU, class FX, class FS, class FP>
+__device__ __forceinline__ ulonglong2 hash_at(const uint32_t *img, FU u, FX x, FS sS, FP sP) {
+    uint64_t h0 = 0, h1 = 0;
+#pragma unroll
+    for (int t = 0; t < N; t++) {
+        const uint64_t ut = u(t);
+        h0 += mix64(ut ^ sS(0, img[t]));
+        h1 += mix64(ut ^ sS(1, img[t]));
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            if (j == t) continue;
+            h0 += mix64(x(0, t, j) ^ sP(0, img[t], img[j]));
+            h1 += mix64(x(1, t, j) ^ sP(1, img[t], img[j]));
+        }
+    }
+    return make_ulonglong2(h0, h1);
+}
+__device__ __forceinline__ bool lex_less(ulonglong2 a, ulonglong2 b) {  // (h1, h0) order
+    return a.y < b.y || (a.y == b.y && a.x < b.x);
+}
+
 // ---- structured symmetry fingerprint --------------------------------------------------
 // seeds layout: [f][0..MAXN) server position seeds, [f][MAXN + k*MAXN + l] pair seeds
 template <int N, int V>
@@ -336,6 +461,29 @@ __device__ __forceinline__ ulonglong2 fingerprint(const uint32_t *c, int srow, c
     }
     uint64_t b0 = ~0ull, b1 = ~0ull;
     const uint64_t *S0 = t.seeds, *S1 = t.seeds + (MAXN + MAXN * MAXN);
+    if (N >= 4) {
+        uint64_t sig[N];
+#pragma unroll
+        for (int i = 0; i < N; i++) {
+            sig[i] = sig_part_u(U[i]);
+#pragma unroll
+            for (int j = 0; j < N; j++)
+                if (j != i) sig[i] += sig_part_x(X0[i * N + j]);
+        }
+        const uint32_t rk = coset_ranks<N>(sig), K = coset_size<N>(rk);
+        ulonglong2 best = make_ulonglong2(~0ull, ~0ull);
+        for (uint32_t k = 0; k < K; k++) {
+            uint32_t img[N];
+            coset_img<N>(rk, k, img);
+            const ulonglong2 h = hash_at<N>(
+                img, [&](int i) { return U[i]; },
+                [&](int f, int i, int j) { return f ? X1[i * N + j] : X0[i * N + j]; },
+                [&](int f, uint32_t a) { return (f ? S1 : S0)[a]; },
+                [&](int f, uint32_t a, uint32_t b) { return (f ? S1 : S0)[MAXN + a * MAXN + b]; });
+            if (lex_less(h, best)) best = h;
+        }
+        return make_ulonglong2(best.x | 1ull, best.y);
+    }
     for (int p = 0; p < t.np; p++) {
         const uint8_t *pi = t.perms + p * MAXN;
         uint32_t img[N];
@@ -922,7 +1070,7 @@ __device__ __forceinline__ void unstage_core(const uint32_t *pc, const uint4 a, 
 }
 
 template <int N, int V, int MR, int MODE>
-__global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KParams P) {
+__global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void k_expand(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
     constexpr bool SUMS = (MODE == M_HASH || MODE == M_SINGLE || MODE == M_FUSED);
@@ -930,20 +1078,28 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
     __shared__ ulonglong2 sPart[SUMS ? 64 : 1];         // partial minima per (successor, permutation block)
     __shared__ uint64_t M0[N * N], M1[N * N];
     __shared__ uint32_t pcore[Lo::NW + N];
-    constexpr int NPM = SUMS ? factorial(N) : 1;        // |Permutations(Servers)| (tla:21)
+    constexpr bool SIG = SUMS && N >= 4;                // signature pre-sort (coset minimum)
+    constexpr int NPM = (SUMS && !SIG) ? factorial(N) : 1;  // |Permutations(Servers)| (tla:21)
     constexpr int MAXS = SUMS ? S::MCAP + N * S::SLOTS_PER_SERVER : 1;
+    constexpr int MAXG = SIG ? MAXS : 1;
     __shared__ uint64_t Rt[2][NPM * N], Tt[2][NPM];     // parent row terms / totals per permutation
     __shared__ uint64_t sdS[2][N], sdP[2][N * N];       // position seeds
     __shared__ uint8_t pimg[NPM * N];                   // permutation images
     __shared__ uint64_t sU[MAXS], sX[2][MAXS * N];      // compacted successor rows
     __shared__ uint8_t sS[MAXS], sNa[MAXS];             // acting server, |added ids| per successor
+    // signature pre-sort: parent rows / signatures, per successor the tie ranks, the first task
+    // of its coset (exclusive scan of coset sizes) and its running minimum; per task its successor
+    __shared__ uint64_t pU[SIG ? N : 1], pX[2][SIG ? N * N : 1], psig[SIG ? N : 1];
+    __shared__ uint32_t sRk[MAXG], sKoff[MAXG], sTl[SIG ? 64 : 1];
+    __shared__ ulonglong2 sBest[MAXG];
     __shared__ uint32_t sAinf[(MR + 1) * 64 * S::NADD];  // info words of the messages each candidate adds
     if (MODE == M_FUSED && !level_args(P)) return;
     // device-loop grids are sized on a bound of the level: blocks past it leave before the LDS setup
     if (MODE == M_FUSED && P.p_begin + blockIdx.x >= P.p_end) return;
     const int lane = threadIdx.x;
     if (SUMS) {
-        for (int i = lane; i < P.t.np * N; i += 64) pimg[i] = P.t.perms[(i / N) * MAXN + (i % N)];
+        if (!SIG)
+            for (int i = lane; i < P.t.np * N; i += 64) pimg[i] = P.t.perms[(i / N) * MAXN + (i % N)];
         if (lane < N) {
             sdS[0][lane] = P.t.seeds[lane];
             sdS[1][lane] = P.t.seeds[MAXN + MAXN * MAXN + lane];
@@ -954,15 +1110,18 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
             sdP[1][lane] = P.t.seeds[2 * MAXN + MAXN * MAXN + k * MAXN + l];
         }
     }
+    PHASE_DECL
     for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
         Wave<N, V, MR> W;
         load_parent<N, V, MR, SUMS>(P, rec_start<S::RECW_MAX>(P, p), lane, W, ids, M0, M1, pcore);
+        PHASE(0);
         Succ<N, V, MR> cand[MR + 1];
         uint32_t akey = KEY_NONE;
 #pragma unroll
         for (int r = 0; r < MR; r++)
             eval_msg<N, V, MR>(P, W, ids, r, lane, cand[r], akey, &sAinf[(r * 64 + lane) * S::NADD]);
         eval_slot<N, V, MR>(P, W, ids, lane, cand[MR], &sAinf[(MR * 64 + lane) * S::NADD]);
+        PHASE(1);
         // rank of every enabled successor in TLC order
         uint64_t en[MR + 1];
         uint32_t total = 0;
@@ -1008,6 +1167,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
             }
             if (MODE == M_COUNT) continue;
         }
+        PHASE(2);
         if (MODE == M_FUSED) {
             // stage every enabled successor at its slot q: the acting row and the added message ids
             // -- commit rebuilds the state from the parent's core and merges the ids
@@ -1018,29 +1178,53 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
                 stage_succ<N, V, MR>(cand[r], W.nm, P.score + q * (uint64_t)S::SW4);
             }
         }
+        PHASE(3);
         if (SUMS) {
-            // (a) parent row terms Rt[f][p][s] = Z_f(pi(s), U[s]) + sum_j Z_f(pi(s), pi(j), X_f[s][j])
-            //     and their per-permutation totals Tt[f][p]  (structured hash, rmc_spec.h)
             const int np = P.t.np;
-            for (int idx = lane; idx < np * N; idx += 64) {
-                const int pp = idx / N;
-                const uint32_t sv = (uint32_t)(idx - pp * N);
-                const uint32_t imgs = pimg[idx];
-                const uint32_t mirow = pcore[Lo::W_MI + sv], nirow = pcore[Lo::W_NI + sv];
-                const uint64_t u = own_word<N>(W.c[Lo::W_VF], W.c[Lo::W_CT], W.c[Lo::W_ROLE], W.c[Lo::W_CI],
-                                               W.c[Lo::W_LL], pcore[Lo::W_LOG + sv], mirow, nirow, sv);
-                uint64_t r0 = mix64(u ^ sdS[0][imgs]), r1 = mix64(u ^ sdS[1][imgs]);
-                const uint32_t vfs = nib(W.c[Lo::W_VF], sv);
+            if (!SIG) {
+                // (a) parent row terms Rt[f][p][s] = Z_f(pi(s), U[s]) + sum_j Z_f(pi(s), pi(j), X_f[s][j])
+                //     and their per-permutation totals Tt[f][p]  (structured hash, rmc_spec.h)
+                for (int idx = lane; idx < np * N; idx += 64) {
+                    const int pp = idx / N;
+                    const uint32_t sv = (uint32_t)(idx - pp * N);
+                    const uint32_t imgs = pimg[idx];
+                    const uint32_t mirow = pcore[Lo::W_MI + sv], nirow = pcore[Lo::W_NI + sv];
+                    const uint64_t u = own_word<N>(W.c[Lo::W_VF], W.c[Lo::W_CT], W.c[Lo::W_ROLE], W.c[Lo::W_CI],
+                                                   W.c[Lo::W_LL], pcore[Lo::W_LOG + sv], mirow, nirow, sv);
+                    uint64_t r0 = mix64(u ^ sdS[0][imgs]), r1 = mix64(u ^ sdS[1][imgs]);
+                    const uint32_t vfs = nib(W.c[Lo::W_VF], sv);
 #pragma unroll
-                for (int j = 0; j < N; j++) {
-                    if ((uint32_t)j == sv) continue;
-                    const uint64_t sm = pair_small(mirow, nirow, vfs, j);
-                    const uint32_t q = imgs * N + pimg[pp * N + j];
-                    r0 += mix64((M0[sv * N + j] ^ (sm * PAIR_K0)) ^ sdP[0][q]);
-                    r1 += mix64((M1[sv * N + j] ^ (sm * PAIR_K1)) ^ sdP[1][q]);
+                    for (int j = 0; j < N; j++) {
+                        if ((uint32_t)j == sv) continue;
+                        const uint64_t sm = pair_small(mirow, nirow, vfs, j);
+                        const uint32_t q = imgs * N + pimg[pp * N + j];
+                        r0 += mix64((M0[sv * N + j] ^ (sm * PAIR_K0)) ^ sdP[0][q]);
+                        r1 += mix64((M1[sv * N + j] ^ (sm * PAIR_K1)) ^ sdP[1][q]);
+                    }
+                    Rt[0][idx] = r0;
+                    Rt[1][idx] = r1;
                 }
-                Rt[0][idx] = r0;
-                Rt[1][idx] = r1;
+            } else {
+                // (a') the parent's per-server inputs and signatures (lane t = server t)
+                if (lane < N) {
+                    const uint32_t t = (uint32_t)lane;
+                    const uint32_t mirow = pcore[Lo::W_MI + t], nirow = pcore[Lo::W_NI + t];
+                    const uint64_t u = own_word<N>(W.c[Lo::W_VF], W.c[Lo::W_CT], W.c[Lo::W_ROLE], W.c[Lo::W_CI],
+                                                   W.c[Lo::W_LL], pcore[Lo::W_LOG + t], mirow, nirow, t);
+                    const uint32_t vft = nib(W.c[Lo::W_VF], t);
+                    pU[t] = u;
+                    uint64_t sg = sig_part_u(u);
+#pragma unroll
+                    for (int j = 0; j < N; j++) {
+                        const uint64_t sm = pair_small(mirow, nirow, vft, j);
+                        const uint64_t x0 = M0[t * N + j] ^ (sm * PAIR_K0);
+                        pX[0][t * N + j] = x0;
+                        pX[1][t * N + j] = M1[t * N + j] ^ (sm * PAIR_K1);
+                        if ((uint32_t)j != t) sg += sig_part_x(x0);
+                    }
+                    psig[t] = sg;
+                }
+                __syncthreads();
             }
             // (b) every enabled successor writes its acting row to LDS slot rank
 #pragma unroll
@@ -1051,154 +1235,169 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
                 uint64_t row0[N], row1[N];
                 succ_row<N, V, MR>(o, M0, M1, &sAinf[(r * 64 + lane) * S::NADD], row0, row1);
                 const uint32_t vfs = nib(o.c[Lo::W_VF], o.s);
-                sU[sl] = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI], o.c[Lo::W_LL],
-                                     o.lw, o.mirow, o.nirow, o.s);
+                const uint64_t u = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI],
+                                               o.c[Lo::W_LL], o.lw, o.mirow, o.nirow, o.s);
+                sU[sl] = u;
+                uint64_t sg = sig_part_u(u);
 #pragma unroll
                 for (int j = 0; j < N; j++) {
                     const uint64_t sm = pair_small(o.mirow, o.nirow, vfs, j);
-                    sX[0][sl * N + j] = row0[j] ^ (sm * PAIR_K0);
+                    const uint64_t x0 = row0[j] ^ (sm * PAIR_K0);
+                    sX[0][sl * N + j] = x0;
                     sX[1][sl * N + j] = row1[j] ^ (sm * PAIR_K1);
+                    if ((uint32_t)j != o.s) sg += sig_part_x(x0);
                 }
                 sS[sl] = (uint8_t)o.s;
                 sNa[sl] = (uint8_t)o.nadd;
-            }
-            __syncthreads();
-            for (int pp = lane; pp < np; pp += 64) {
-                uint64_t t0 = 0, t1 = 0;
+                if (SIG) {
+                    // only the acting server's row changes (every message it adds is its own)
+                    uint64_t sig[N];
 #pragma unroll
-                for (int q = 0; q < N; q++) { t0 += Rt[0][pp * N + q]; t1 += Rt[1][pp * N + q]; }
-                Tt[0][pp] = t0;
-                Tt[1][pp] = t1;
+                    for (int t = 0; t < N; t++) sig[t] = (uint32_t)t == o.s ? sg : psig[t];
+                    const uint32_t rk = coset_ranks<N>(sig);
+                    sRk[sl] = rk;
+                    sKoff[sl] = coset_size<N>(rk);
+                    sBest[sl] = make_ulonglong2(~0ull, ~0ull);
+                }
             }
             __syncthreads();
-            // (c) one (successor l, permutation block b) task per lane: the lane takes the minimum
-            //     over permutations b, b + PB, ... of (parent total - old row + new row), and the PB
-            //     partial minima of a successor meet in LDS.  PB = 64 / total (at most |perms|)
-            //     keeps all 64 lanes busy when a parent has few successors -- the common case.
-            const uint32_t npu = (uint32_t)np;
-            constexpr bool TWO_PASS = N >= 4;
-            static_assert(!TWO_PASS || factorial(N) <= 128, "two-pass tie mask holds 128 permutations per lane");
-            uint32_t PB = 1;
-            if (total > 0 && total < 64) PB = min(64u / total, npu);
-            const uint32_t SB = 64u / PB;  // successors per round
-            const uint32_t li = (uint32_t)lane / PB, blk = (uint32_t)lane - li * PB;
-            for (uint32_t b0 = 0; b0 < total; b0 += SB) {
-                const uint32_t l = b0 + li;
-                uint64_t m0 = ~0ull, m1 = ~0ull;
-                if (TWO_PASS) {
-                    // n >= 4: family 1 first over every permutation of the block, remembering
-                    // which ones reach the lane's minimum; family 0 then only for the permutations
-                    // that reach the successor's minimum (one, or an automorphism group) -- the
-                    // same lexicographic minimum of (H1, H0) with about half the mixes
-                    const bool act = li < SB && l < total;
-                    uint32_t sv = 0;
-                    uint64_t u = 0, x0[N], x1[N], tm[2] = {0ull, 0ull};
-                    if (act) {
-                        sv = sS[l];
-                        u = sU[l];
+            // the successor's fingerprint: seen-set probe + election (fused), or the hash pass output
+            PHASE(4);
+            auto emit = [&](uint32_t lo, ulonglong2 best) {
+                const ulonglong2 f = make_ulonglong2(best.x | 1ull, best.y);
+                if (MODE == M_FUSED) {
+                    // the seen set is read-only in this launch (commit inserts)
+                    const uint64_t q = pl * (uint64_t)S::MAXS + lo;
+                    P.fp[q] = f;
+                    // the election slot's first word goes out with the seen-set probe: one
+                    // round trip fewer for a new fingerprint
+                    const uint64_t g0 = l_index(f, P.Lmask);
+                    const unsigned long long v0 =
+                        __hip_atomic_load(&P.LXY[g0].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t e = ((uint32_t)sNa[lo] + (W.nm & 1u) + 1u) >> 1;
+                    P.lslot[q] = seen_contains(P.seen, f)
+                                     ? LS_SEEN
+                                     : elect_slot<S::MAXS>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g0, v0);
+                } else {
+                    P.fp[((MODE == M_HASH) ? (uint64_t)P.off[pl] : 0ull) + lo] = f;
+                }
+            };
+            if (SIG) {
+                // (c') one task per (successor, allowed permutation): exclusive scan of the coset
+                //      sizes, then 64 tasks per round; a successor's tasks are consecutive, so the
+                //      first lane of each run folds the run into the successor's minimum
+                uint32_t ntask = 0;
+                for (uint32_t b0 = 0; b0 < total; b0 += 64) {
+                    const uint32_t l = b0 + (uint32_t)lane;
+                    uint32_t rt;
+                    const uint32_t ex = wave_excl_scan(l < total ? sKoff[l] : 0u, lane, &rt);
+                    if (l < total) sKoff[l] = ntask + ex;
+                    ntask += rt;
+                }
+                __syncthreads();
+                for (uint32_t tb = 0; tb < ntask; tb += 64) {
+                    const uint32_t ti = tb + (uint32_t)lane;
+                    uint32_t l = 0xFFFFFFFFu;
+                    ulonglong2 h = make_ulonglong2(~0ull, ~0ull);
+                    if (ti < ntask) {
+                        uint32_t a = 0, b = total;  // sKoff[a] <= ti < sKoff[b]
+                        while (b - a > 1) {
+                            const uint32_t m = (a + b) >> 1;
+                            if (sKoff[m] <= ti) a = m; else b = m;
+                        }
+                        l = a;
+                        uint32_t img[N];
+                        coset_img<N>(sRk[l], ti - sKoff[l], img);
+                        const uint32_t sv = sS[l];
+                        const uint64_t su = sU[l];
+                        h = hash_at<N>(
+                            img, [&](int t) { return (uint32_t)t == sv ? su : pU[t]; },
+                            [&](int f, int t, int j) {
+                                return (uint32_t)t == sv ? sX[f][l * N + j] : pX[f][t * N + j];
+                            },
+                            [&](int f, uint32_t x) { return sdS[f][x]; },
+                            [&](int f, uint32_t x, uint32_t y) { return sdP[f][x * N + y]; });
+                    }
+                    sPart[lane] = h;
+                    sTl[lane] = l;
+                    __syncthreads();
+                    if (ti < ntask && (lane == 0 || sTl[lane - 1] != l)) {
+                        ulonglong2 best = sBest[l];
+                        for (int j = lane; j < 64 && sTl[j] == l; j++)
+                            if (lex_less(sPart[j], best)) best = sPart[j];
+                        sBest[l] = best;
+                    }
+                    __syncthreads();
+                }
+                PHASE(5);
+                for (uint32_t b0 = 0; b0 < total; b0 += 64) {
+                    const uint32_t lo = b0 + (uint32_t)lane;
+                    if (lo < total) emit(lo, sBest[lo]);
+                }
+                __syncthreads();
+                PHASE(6);
+            } else {
+                for (int pp = lane; pp < np; pp += 64) {
+                    uint64_t t0 = 0, t1 = 0;
+#pragma unroll
+                    for (int q = 0; q < N; q++) { t0 += Rt[0][pp * N + q]; t1 += Rt[1][pp * N + q]; }
+                    Tt[0][pp] = t0;
+                    Tt[1][pp] = t1;
+                }
+                __syncthreads();
+                // (c) one (successor l, permutation block b) task per lane: the lane takes the minimum
+                //     over permutations b, b + PB, ... of (parent total - old row + new row), and the PB
+                //     partial minima of a successor meet in LDS.  PB = 64 / total (at most |perms|)
+                //     keeps all 64 lanes busy when a parent has few successors -- the common case.
+                const uint32_t npu = (uint32_t)np;
+                uint32_t PB = 1;
+                if (total > 0 && total < 64) PB = min(64u / total, npu);
+                const uint32_t SB = 64u / PB;  // successors per round
+                const uint32_t li = (uint32_t)lane / PB, blk = (uint32_t)lane - li * PB;
+                for (uint32_t b0 = 0; b0 < total; b0 += SB) {
+                    const uint32_t l = b0 + li;
+                    uint64_t m0 = ~0ull, m1 = ~0ull;
+                    if (li < SB && l < total) {
+                        const uint32_t sv = sS[l];
+                        const uint64_t u = sU[l];
+                        uint64_t x0[N], x1[N];
 #pragma unroll
                         for (int j = 0; j < N; j++) { x0[j] = sX[0][l * N + j]; x1[j] = sX[1][l * N + j]; }
-                        uint32_t it = 0;
-                        for (uint32_t pp = blk; pp < npu; pp += PB, it++) {
+                        for (uint32_t pp = blk; pp < npu; pp += PB) {
                             uint32_t img[N];
 #pragma unroll
                             for (int j = 0; j < N; j++) img[j] = pimg[pp * N + j];
                             uint32_t imgs = img[0];
 #pragma unroll
                             for (int j = 1; j < N; j++) imgs = ((uint32_t)j == sv) ? img[j] : imgs;
+                            uint64_t h0 = Tt[0][pp] - Rt[0][pp * N + sv] + mix64(u ^ sdS[0][imgs]);
                             uint64_t h1 = Tt[1][pp] - Rt[1][pp * N + sv] + mix64(u ^ sdS[1][imgs]);
 #pragma unroll
                             for (int j = 0; j < N; j++) {
                                 if ((uint32_t)j == sv) continue;
-                                h1 += mix64(x1[j] ^ sdP[1][imgs * N + img[j]]);
+                                const uint32_t q = imgs * N + img[j];
+                                h0 += mix64(x0[j] ^ sdP[0][q]);
+                                h1 += mix64(x1[j] ^ sdP[1][q]);
                             }
-                            if (h1 < m1) { m1 = h1; tm[0] = 0ull; tm[1] = 0ull; }
-                            if (h1 == m1) tm[it >> 6] |= 1ull << (it & 63u);
+                            if (h1 < m1 || (h1 == m1 && h0 < m0)) { m1 = h1; m0 = h0; }
                         }
                     }
-                    sPart[lane] = make_ulonglong2(0ull, m1);
+                    sPart[lane] = make_ulonglong2(m0, m1);
                     __syncthreads();
-                    uint64_t M1 = ~0ull;
-                    if (act)
-                        for (uint32_t k = 0; k < PB; k++) M1 = min(M1, (uint64_t)sPart[li * PB + k].y);
+                    const uint32_t lo = b0 + (uint32_t)lane;
+                    if ((uint32_t)lane < SB && lo < total) {
+                        ulonglong2 best = sPart[lane * PB];
+                        for (uint32_t k = 1; k < PB; k++) {
+                            const ulonglong2 v = sPart[lane * PB + k];
+                            if (lex_less(v, best)) best = v;
+                        }
+                        emit(lo, best);
+                    }
                     __syncthreads();
-                    if (act && m1 == M1) {
-#pragma unroll
-                        for (int w = 0; w < 2; w++) {
-                            for (uint64_t bits = tm[w]; bits; bits &= bits - 1) {
-                                const uint32_t it = (uint32_t)(w * 64 + __ffsll((unsigned long long)bits) - 1);
-                                const uint32_t pp = blk + it * PB;
-                                uint32_t img[N];
-#pragma unroll
-                                for (int j = 0; j < N; j++) img[j] = pimg[pp * N + j];
-                                uint32_t imgs = img[0];
-#pragma unroll
-                                for (int j = 1; j < N; j++) imgs = ((uint32_t)j == sv) ? img[j] : imgs;
-                                uint64_t h0 = Tt[0][pp] - Rt[0][pp * N + sv] + mix64(u ^ sdS[0][imgs]);
-#pragma unroll
-                                for (int j = 0; j < N; j++) {
-                                    if ((uint32_t)j == sv) continue;
-                                    h0 += mix64(x0[j] ^ sdP[0][imgs * N + img[j]]);
-                                }
-                                m0 = min(m0, h0);
-                            }
-                        }
-                    }
-                } else if (li < SB && l < total) {
-                    const uint32_t sv = sS[l];
-                    const uint64_t u = sU[l];
-                    uint64_t x0[N], x1[N];
-#pragma unroll
-                    for (int j = 0; j < N; j++) { x0[j] = sX[0][l * N + j]; x1[j] = sX[1][l * N + j]; }
-                    for (uint32_t pp = blk; pp < npu; pp += PB) {
-                        uint32_t img[N];
-#pragma unroll
-                        for (int j = 0; j < N; j++) img[j] = pimg[pp * N + j];
-                        uint32_t imgs = img[0];
-#pragma unroll
-                        for (int j = 1; j < N; j++) imgs = ((uint32_t)j == sv) ? img[j] : imgs;
-                        uint64_t h0 = Tt[0][pp] - Rt[0][pp * N + sv] + mix64(u ^ sdS[0][imgs]);
-                        uint64_t h1 = Tt[1][pp] - Rt[1][pp * N + sv] + mix64(u ^ sdS[1][imgs]);
-#pragma unroll
-                        for (int j = 0; j < N; j++) {
-                            if ((uint32_t)j == sv) continue;
-                            const uint32_t q = imgs * N + img[j];
-                            h0 += mix64(x0[j] ^ sdP[0][q]);
-                            h1 += mix64(x1[j] ^ sdP[1][q]);
-                        }
-                        if (h1 < m1 || (h1 == m1 && h0 < m0)) { m1 = h1; m0 = h0; }
-                    }
                 }
-                sPart[lane] = make_ulonglong2(m0, m1);
-                __syncthreads();
-                const uint32_t lo = b0 + (uint32_t)lane;
-                if ((uint32_t)lane < SB && lo < total) {
-                    ulonglong2 best = sPart[lane * PB];
-                    for (uint32_t k = 1; k < PB; k++) {
-                        const ulonglong2 v = sPart[lane * PB + k];
-                        if (v.y < best.y || (v.y == best.y && v.x < best.x)) best = v;
-                    }
-                    const ulonglong2 f = make_ulonglong2(best.x | 1ull, best.y);
-                    if (MODE == M_FUSED) {
-                        // the seen set is read-only in this launch (commit inserts)
-                        const uint64_t q = pl * (uint64_t)S::MAXS + lo;
-                        P.fp[q] = f;
-                        // the election slot's first word goes out with the seen-set probe: one
-                        // round trip fewer for a new fingerprint
-                        const uint64_t g0 = l_index(f, P.Lmask);
-                        const unsigned long long v0 =
-                            __hip_atomic_load(&P.LXY[g0].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        const uint32_t e = ((uint32_t)sNa[lo] + (W.nm & 1u) + 1u) >> 1;
-                        P.lslot[q] = seen_contains(P.seen, f)
-                                         ? LS_SEEN
-                                         : elect_slot<S::MAXS>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g0, v0);
-                    } else {
-                        P.fp[((MODE == M_HASH) ? (uint64_t)P.off[pl] : 0ull) + lo] = f;
-                    }
-                }
-                __syncthreads();
             }
         }
+        PHASE(5);
         if (MODE == M_HASH || MODE == M_FUSED) continue;
         // MATERIALIZE / SINGLE: write chosen successors
 #pragma unroll
@@ -1250,6 +1449,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : 1) void k_expand(KPar
         }
         if (MODE == M_SINGLE && lane == 0) *P.out_count = total;
     }
+    PHASE_FLUSH;
 }
 
 // fingerprints of whole states (Init, test hooks): one wave per state

@@ -15,7 +15,7 @@ from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "librmc.so")
+LIB_PATH = os.environ.get("RMC_LIBRARY") or os.path.join(os.path.dirname(_HERE), "build", "librmc.so")
 
 RMC_OK, RMC_DONE, RMC_VIOLATION, RMC_ASSERT, RMC_EVAL_ERROR, RMC_DEADLOCK = 0, 1, 2, 3, 4, 5
 STATUS_NAMES = {RMC_OK: "ok", RMC_DONE: "done", RMC_VIOLATION: "invariant", RMC_ASSERT: "assert",

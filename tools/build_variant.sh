@@ -1,0 +1,19 @@
+#!/bin/bash
+# Build an experimental variant of librmc.so next to the default one:
+#   tools/build_variant.sh prof   -> tla-raft_amd/build_prof/librmc.so  (-DRMC_PHASE_PROF, tools/phase_prof.py)
+#   tools/build_variant.sh w1     -> tla-raft_amd/build_w1/librmc.so    (n >= 4 expansion at 1 wave / SIMD)
+# Select it with RMC_LIBRARY=<path> (raftmc.load_library).  Needs the default build (make -C tla-raft_amd).
+set -e
+cd "$(dirname "$0")/../tla-raft_amd"
+case "$1" in
+  prof) FLAGS="-DRMC_PHASE_PROF" ;;
+  w1) FLAGS="-DRMC_WIDE_WAVES=1" ;;
+  *) echo "usage: $0 prof|w1" >&2; exit 2 ;;
+esac
+OUT=build_$1
+mkdir -p "$OUT"
+HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
+$HIPCC --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -DRMC_WITH_RCCL $FLAGS -Iinclude -I../include -Icsrc \
+  -c csrc/rmc_kernels.hip -o "$OUT/rmc_kernels.o"
+$HIPCC --offload-arch=gfx950 -shared -fPIC -o "$OUT/librmc.so" "$OUT/rmc_kernels.o" build/rmc_engine.o build/rmc_cfg.o build/rmc_probe.o -lrccl
+echo "$OUT/librmc.so"
