@@ -266,7 +266,7 @@ struct Shard {
     unsigned long long *Tc = nullptr;
     uint64_t T_cap = 0, T_count = 0;
     Seen seen() const { return Seen{Tc ? nullptr : T, Tc, Tc ? 0 : T_cap - 1, T_cap}; }
-    // trace: parent reference (shard << 48 | local gid) + slot key per local gid; the device
+    // trace: parent's global id + slot key per local gid; the device
     // buffers hold gids from tflushed on, the host arrays everything before
     uint64_t *par = nullptr;
     uint16_t *pslot = nullptr;
@@ -276,7 +276,7 @@ struct Shard {
     HostArr<uint16_t> hslot;
     std::vector<uint64_t> level_start;  // local gid of the first state of each level
     // chunk buffers (source side)
-    uint32_t *cnt = nullptr, *off = nullptr, *lslot = nullptr, *wflag = nullptr, *wpos = nullptr;
+    uint32_t *cnt = nullptr, *lslot = nullptr, *wpos = nullptr;
     ulonglong2 *fp = nullptr;
     unsigned long long *L = nullptr;
     ulonglong2 *LXY = nullptr;  // fused path: fingerprint of each election slot (tagged)
@@ -291,21 +291,28 @@ struct Shard {
     LevelRec *lrec = nullptr, *hlrec = nullptr;
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
-    // exchange buffers (W > 1)
-    uint32_t *okey = nullptr, *okey2 = nullptr, *iota = nullptr, *perm = nullptr, *sflag = nullptr, *spos = nullptr;
-    ulonglong2 *sfp = nullptr;
-    unsigned long long *ocnt = nullptr;
-    ulonglong2 *rfp = nullptr;
-    uint32_t *rlslot = nullptr, *rflag = nullptr, *rpos = nullptr, *rcount = nullptr;
-    uint64_t rcap_x = 0;
-    uint32_t *sx = nullptr, *rx = nullptr;
-    uint64_t sx_cap = 0, rx_cap = 0;
-    uint64_t *pick_idx = nullptr;
+    // sharded round (W > 1): successors to their fingerprint's owner (xs, owner-grouped; perm =
+    // each item's slot, sflag = the owner's verdict), received successors (xr, rslot, rflag), the
+    // owner's election table (OT / OK), the round's winners (outbox: records ob, offsets ooff,
+    // sidecars oside) and the winners received from the sources (ib, iside, isz / ioff)
+    XItem *xs = nullptr, *xr = nullptr;
+    uint64_t xs_cap = 0, xr_cap = 0;
+    uint32_t *perm = nullptr, *sflag = nullptr, *rslot = nullptr, *rflag = nullptr, *ocnt = nullptr;
+    ulonglong2 *OT = nullptr;
+    unsigned long long *OK = nullptr;
+    uint64_t ot_cap = 0;
+    uint32_t *ob = nullptr, *ib = nullptr;
+    uint64_t ob_cap = 0, ib_cap = 0;
+    uint4 *oside = nullptr, *iside = nullptr;
+    uint64_t *ooff = nullptr;
+    uint32_t *isz = nullptr, *ioff = nullptr;
+    uint64_t os_cap = 0, is_cap = 0;
     // errors, summary
     unsigned long long *err = nullptr, *sum = nullptr, *hsum = nullptr;
     uint32_t *flags = nullptr;
-    // per-chunk host bookkeeping (sharded path)
-    uint64_t p0 = 0, np = 0, G = 0;
+    // per-round host bookkeeping (sharded path): first parent, parents, successors, global index
+    // of the round's first parent in the level
+    uint64_t p0 = 0, np = 0, G = 0, gblk = 0;
 };
 
 struct rmc_ctx {
@@ -351,7 +358,8 @@ struct rmc_ctx {
     int32_t *d_inv = nullptr;
     unsigned long long *d_err1 = nullptr;
     uint32_t *d_flags1 = nullptr;
-    unsigned long long *d_red = nullptr, *h_red = nullptr;  // collective scratch
+    unsigned long long *d_red = nullptr, *h_red = nullptr;  // collective scratch (RED_CAP values)
+    static constexpr int RED_CAP = 16 * 64;
 
     // progress
     bool inited = false, finished = false;
@@ -359,8 +367,13 @@ struct rmc_ctx {
     int depth = 0;
     uint64_t total_generated = 0, total_distinct = 0, queue_at_end = 0;
     int violated = -1;
-    uint64_t err_ref = 0;  // state whose trace is reported: shard << 48 | local gid
+    uint64_t err_ref = 0;  // global id of the state whose trace is reported
     uint32_t err_last_slot = KEY_NONE;  // sharded: slot of the violating successor (not stored anywhere)
+    // W > 1, block-cyclic levels: global index g of a level lives on shard (g / B) % W at local
+    // index (g / (B W)) B + g % B, B = chunk_parents; glevel = global id of each level's first
+    // state; levels before L_shard were expanded replicated (global id == local gid everywhere)
+    std::vector<uint64_t> glevel;
+    int L_shard = 0;
     std::vector<TraceStep> trace;
     double seconds = 0;
 
@@ -677,12 +690,11 @@ struct rmc_ctx {
         if (Gcap >= (1ull << 30)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^30");
         chunk_parents = Gcap / ks.maxsucc;
         shard_min = W > 1 ? (cfg.shard_min_states ? cfg.shard_min_states : (1ull << 20)) : 0;
-        const bool fused_ok = W == 1 || shard_min > 1;  // shard 0 runs the fused single-GPU level
-        if (fused_ok) chunk_parents = std::min<uint64_t>(chunk_parents, (uint64_t)WTILE * 1024);  // winner-count tiles
+        chunk_parents = std::min<uint64_t>(chunk_parents, (uint64_t)WTILE * 1024);  // winner-count tiles
         Lcap_max = next_pow2(2 * Gcap);
 
         sh.resize(virt ? W : 1);
-        for (size_t i = 0; i < sh.size(); i++) alloc_shard(sh[i], virt ? (int)i : rank, fused_ok && i == 0);
+        for (size_t i = 0; i < sh.size(); i++) alloc_shard(sh[i], virt ? (int)i : rank);
 
         d_one = dmalloc<uint32_t>(RECW);
         d_out = dmalloc<uint32_t>((size_t)ks.maxsucc * RECW);
@@ -692,69 +704,49 @@ struct rmc_ctx {
         d_inv = dmalloc<int32_t>(7);
         d_err1 = dmalloc<unsigned long long>(ERR_NSLOTS);
         d_flags1 = dmalloc<uint32_t>(4);
-        d_red = dmalloc<unsigned long long>(4 * 64 + 8);
-        HIPCHK(hipHostMalloc((void **)&h_red, (4 * 64 + 8) * 8, hipHostMallocDefault));
+        d_red = dmalloc<unsigned long long>(2 * RED_CAP);
+        HIPCHK(hipHostMalloc((void **)&h_red, RED_CAP * 8, hipHostMallocDefault));
         HIPCHK(hipStreamSynchronize(stream));
     }
 
-    void alloc_shard(Shard &s, int id, bool fused) {
+    void alloc_shard(Shard &s, int id) {
         s.id = id;
         s.cnt = dmalloc<uint32_t>(chunk_parents + 1);
-        s.off = dmalloc<uint32_t>(chunk_parents + 1);
         s.fp = dmalloc<ulonglong2>(Gcap);
         s.lslot = dmalloc<uint32_t>(Gcap);
-        s.wflag = dmalloc<uint32_t>(Gcap + 1);
         s.wpos = dmalloc<uint32_t>(Gcap + 1);
         HIPCHK(hipMemsetAsync(s.cnt, 0, (chunk_parents + 1) * 4, stream));
-        HIPCHK(hipMemsetAsync(s.wflag, 0, (Gcap + 1) * 4, stream));
         s.L = dmalloc<unsigned long long>(Lcap_max);
-        // an all-ones election word is older than every epoch's (elect_key) and, for the sharded
-        // path's (epoch << 32) | j words, of no epoch
+        // an all-ones election word is older than every epoch's (elect_key)
         HIPCHK(hipMemsetAsync(s.L, 0xFF, Lcap_max * 8, stream));
-        if (fused) {
-            s.LXY = dmalloc<ulonglong2>(Lcap_max);
-            HIPCHK(hipMemsetAsync(s.LXY, 0, Lcap_max * 16, stream));
-            int sw4 = ks.N >= 4 ? 3 : 2;
-            s.score = dmalloc<uint4>(Gcap * (uint64_t)sw4);
-            s.wcnt = dmalloc<uint32_t>(chunk_parents + 1);
-            s.wacc = dmalloc<uint32_t>(chunk_parents + 1);
-            s.pnm = dmalloc<uint32_t>(chunk_parents + 1);
-            s.wposw = dmalloc<uint32_t>(chunk_parents + 1);
-            s.ctick = dmalloc<uint32_t>(33 * 32);
-            HIPCHK(hipMemsetAsync(s.ctick, 0, 33 * 32 * 4, stream));
-            HIPCHK(hipMemsetAsync(s.wacc, 0, (chunk_parents + 1) * 4, stream));
-            s.bw = dmalloc<uint32_t>(1024);
-            s.bg = dmalloc<uint32_t>(1024);
-            s.boff = dmalloc<uint32_t>(1024);
-            s.bww = dmalloc<uint32_t>(1024);
-            s.boffw = dmalloc<uint32_t>(1024);
-            s.tickets = dmalloc<uint32_t>(4);
-            HIPCHK(hipMemsetAsync(s.tickets, 0, 16, stream));
-            s.ctl = dmalloc<LevelCtl>(1);
-            s.lrec = dmalloc<LevelRec>(LREC_CAP);
-            HIPCHK(hipHostMalloc((void **)&s.hctl, sizeof(LevelCtl), hipHostMallocDefault));
-            HIPCHK(hipHostMalloc((void **)&s.hsnap, 3 * sizeof(LevelCtl), hipHostMallocDefault));
-            HIPCHK(hipHostMalloc((void **)&s.hlrec, sizeof(LevelRec) * LREC_CAP, hipHostMallocDefault));
-        }
-        size_t t1 = 0, t2 = 0;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, s.cnt, s.off, (int)Gcap + 1, stream));
+        s.LXY = dmalloc<ulonglong2>(Lcap_max);
+        HIPCHK(hipMemsetAsync(s.LXY, 0, Lcap_max * 16, stream));
+        s.score = dmalloc<uint4>(Gcap * (uint64_t)sw4());
+        s.wcnt = dmalloc<uint32_t>(chunk_parents + 1);
+        s.wacc = dmalloc<uint32_t>(chunk_parents + 1);
+        s.pnm = dmalloc<uint32_t>(chunk_parents + 1);
+        s.wposw = dmalloc<uint32_t>(chunk_parents + 1);
+        s.ctick = dmalloc<uint32_t>(33 * 32);
+        HIPCHK(hipMemsetAsync(s.ctick, 0, 33 * 32 * 4, stream));
+        HIPCHK(hipMemsetAsync(s.wacc, 0, (chunk_parents + 1) * 4, stream));
+        s.bw = dmalloc<uint32_t>(1024);
+        s.bg = dmalloc<uint32_t>(1024);
+        s.boff = dmalloc<uint32_t>(1024);
+        s.bww = dmalloc<uint32_t>(1024);
+        s.boffw = dmalloc<uint32_t>(1024);
+        s.tickets = dmalloc<uint32_t>(4);
+        HIPCHK(hipMemsetAsync(s.tickets, 0, 16, stream));
+        s.ctl = dmalloc<LevelCtl>(1);
+        s.lrec = dmalloc<LevelRec>(LREC_CAP);
+        HIPCHK(hipHostMalloc((void **)&s.hctl, sizeof(LevelCtl), hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void **)&s.hsnap, 3 * sizeof(LevelCtl), hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void **)&s.hlrec, sizeof(LevelRec) * LREC_CAP, hipHostMallocDefault));
         if (W > 1) {
-            s.okey = dmalloc<uint32_t>(Gcap);
-            s.okey2 = dmalloc<uint32_t>(Gcap);
-            s.iota = dmalloc<uint32_t>(Gcap);
             s.perm = dmalloc<uint32_t>(Gcap);
-            s.sflag = dmalloc<uint32_t>(Gcap + 1);
-            s.spos = dmalloc<uint32_t>(Gcap + 1);
-            s.sfp = dmalloc<ulonglong2>(Gcap);
-            s.ocnt = dmalloc<unsigned long long>(64);
-            s.pick_idx = dmalloc<uint64_t>(2 * 65);
-            int bits = 0;
-            while ((1 << bits) < W) bits++;
-            HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, s.okey, s.okey2, s.iota, s.perm, (int)Gcap, 0,
-                                                      std::max(bits, 1), stream));
+            s.sflag = dmalloc<uint32_t>(Gcap);
+            s.ocnt = dmalloc<uint32_t>(64);
         }
-        s.tmp_bytes = std::max(t1, t2);
-        s.tmp = dmalloc<uint8_t>(s.tmp_bytes);
+        ensure_tmp(s, Gcap + 1);
         s.T_cap = 1ull << (cfg.seen_log2 ? cfg.seen_log2 : 22);
         s.T = dmalloc<ulonglong2>(s.T_cap);
         HIPCHK(hipMemsetAsync(s.T, 0, s.T_cap * 16, stream));
@@ -776,11 +768,12 @@ struct rmc_ctx {
 
     void free_shard(Shard &s) {
         dfree(s.R); dfree(s.cur_off); dfree(s.nxt_off); dfree(s.T); dfree(s.Tc); dfree(s.par); dfree(s.pslot);
-        dfree(s.cnt); dfree(s.off);
-        dfree(s.lslot); dfree(s.wflag); dfree(s.wpos); dfree(s.fp); dfree(s.L); dfree(s.LXY); dfree(s.tmp); dfree(s.okey);
-        dfree(s.okey2); dfree(s.iota); dfree(s.perm); dfree(s.sflag); dfree(s.spos); dfree(s.sfp); dfree(s.ocnt);
-        dfree(s.rfp); dfree(s.rlslot); dfree(s.rflag); dfree(s.rpos); dfree(s.rcount); dfree(s.sx); dfree(s.rx);
-        dfree(s.pick_idx); dfree(s.err); dfree(s.sum); dfree(s.flags);
+        dfree(s.cnt);
+        dfree(s.lslot); dfree(s.wpos); dfree(s.fp); dfree(s.L); dfree(s.LXY); dfree(s.tmp);
+        dfree(s.xs); dfree(s.xr); dfree(s.perm); dfree(s.sflag); dfree(s.rslot); dfree(s.rflag); dfree(s.ocnt);
+        dfree(s.OT); dfree(s.OK); dfree(s.ob); dfree(s.ib); dfree(s.oside); dfree(s.iside); dfree(s.ooff);
+        dfree(s.isz); dfree(s.ioff);
+        dfree(s.err); dfree(s.sum); dfree(s.flags);
         dfree(s.score); dfree(s.wcnt); dfree(s.wacc); dfree(s.pnm); dfree(s.wposw); dfree(s.ctick);
         dfree(s.bw); dfree(s.bg); dfree(s.boff); dfree(s.bww); dfree(s.boffw); dfree(s.tickets);
         dfree(s.ctl); dfree(s.lrec);
@@ -975,17 +968,40 @@ struct rmc_ctx {
         cap = nc;
     }
 
-    void grow_recv(Shard &s, uint64_t need) {
-        if (need + 1 <= s.rcap_x) return;
-        uint64_t nc = std::max<uint64_t>(need + need / 2 + 1, 1024);
-        dfree(s.rfp); dfree(s.rlslot); dfree(s.rflag); dfree(s.rpos);
-        s.rfp = dmalloc<ulonglong2>(nc);
-        s.rlslot = dmalloc<uint32_t>(nc);
-        s.rflag = dmalloc<uint32_t>(nc);
-        s.rpos = dmalloc<uint32_t>(nc);
-        HIPCHK(hipMemsetAsync(s.rflag, 0, nc * 4, stream));
-        s.rcap_x = nc;
-        if (!s.rcount) s.rcount = dmalloc<uint32_t>(4);
+    int sw4() const { return ks.N >= 4 ? 3 : 2; }  // staging uint4s per successor (Spec::SW4)
+
+    // scan scratch for n values
+    void ensure_tmp(Shard &s, uint64_t n) {
+        size_t t = 0;
+        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, t, s.cnt, s.cnt, (int)std::min<uint64_t>(n, INT32_MAX), stream));
+        if (t <= s.tmp_bytes) return;
+        HIPCHK(hipStreamSynchronize(stream));
+        dfree(s.tmp);
+        s.tmp_bytes = t + t / 2;
+        s.tmp = dmalloc<uint8_t>(s.tmp_bytes);
+    }
+
+    // owner election table of at least 2 * R slots, cleared for the round
+    uint64_t owner_table(Shard &o, uint64_t R) {
+        const uint64_t need = next_pow2(std::max<uint64_t>(2 * R, 1024));
+        if (need > o.ot_cap) {
+            HIPCHK(hipStreamSynchronize(stream));
+            dfree(o.OT);
+            dfree(o.OK);
+            o.OT = dmalloc<ulonglong2>(need);
+            o.OK = dmalloc<unsigned long long>(need);
+            o.ot_cap = need;
+        }
+        HIPCHK(hipMemsetAsync(o.OT, 0, need * 16, stream));
+        HIPCHK(hipMemsetAsync(o.OK, 0xFF, need * 8, stream));
+        return need;
+    }
+
+    // copy `words` linear words from src into the shard's ring at ring position `at` (wrapping)
+    void ring_copy_in(Shard &s, uint64_t at, const uint32_t *src, uint64_t words) {
+        const uint64_t n1 = std::min(words, s.rcap - at);
+        if (n1) HIPCHK(hipMemcpyAsync(s.R + at, src, n1 * 4, hipMemcpyDeviceToDevice, stream));
+        if (words > n1) HIPCHK(hipMemcpyAsync(s.R, src + n1, (words - n1) * 4, hipMemcpyDeviceToDevice, stream));
     }
 
     // Phase timing by event pairs on the engine's stream, read back at the next sync
@@ -1153,11 +1169,13 @@ struct rmc_ctx {
         P.fp = d_fp1;
         ks.fp_states(P, 1, stream);
         ks.inv_states(P, 1, d_inv, stream);
-        uint32_t owner = 0;
+        uint32_t owner = 0;  // the shard whose seen set takes Init's fingerprint
         replicated = W > 1 && shard_min > 1;
         if (W > 1 && !replicated) {
             launch_owner_of(d_fp1, (uint32_t)W, d_cnt1, stream);
             owner = d2h(d_cnt1);
+            glevel = {0};
+            L_shard = 1;
         }
         int32_t iv[7];
         HIPCHK(hipMemcpyAsync(iv, d_inv, sizeof iv, hipMemcpyDeviceToHost, stream));
@@ -1167,16 +1185,22 @@ struct rmc_ctx {
             s.level_start = {0};
             s.cur_n = 0;
             s.cur_wbase = s.cur_words = s.nxt_words = 0;
-            if (replicated ? &s != &sh[0] : (uint32_t)s.id != owner) continue;
+            // Init is global index 0 of level 1: block 0, shard 0 (W > 1 from the start)
+            const bool holds = replicated || W == 1 ? &s == &sh[0] : s.id == 0;
+            if (W > 1 && !replicated && (uint32_t)s.id == owner) {
+                launch_insert_fps(d_fp1, 1, s.seen(), stream);
+                s.T_count = 1;
+            }
+            if (!holds) continue;
             HIPCHK(hipMemcpyAsync(s.R, d_one, rw * 4, hipMemcpyDeviceToDevice, stream));
             HIPCHK(hipMemcpyAsync(s.cur_off, &zero, 8, hipMemcpyHostToDevice, stream));
-            launch_insert_fps(d_fp1, 1, s.seen(), stream);
+            if (W == 1 || replicated) launch_insert_fps(d_fp1, 1, s.seen(), stream);
             s.hpar.set(0, ~0ull);
             s.hslot.set(0, 0);
             s.tflushed = 1;
             s.cur_n = 1;
             s.cur_words = rw;
-            s.T_count = 1;
+            if (W == 1 || replicated) s.T_count = 1;
         }
         HIPCHK(hipStreamSynchronize(stream));
         total_generated = 1;  // TLC counts the initial state as generated
@@ -1189,7 +1213,7 @@ struct rmc_ctx {
             if (iv[b] != 1) {
                 status = iv[b] == 0 ? RMC_VIOLATION : RMC_EVAL_ERROR;
                 violated = b;
-                err_ref = ((uint64_t)owner << 48);
+                err_ref = 0;
                 err_last_slot = KEY_NONE;
                 queue_at_end = 0;
                 finished = true;
@@ -1223,50 +1247,63 @@ struct rmc_ctx {
         return (W == 1 || replicated) ? step_single(st) : step_sharded(st);
     }
 
-    // shard t takes over parents [o, o + n) of shard src's current level: records (their words)
-    // into t's ring from position 0, offsets rebased to the first of them
-    void take_parents(Shard &src, Shard &t, uint64_t o, uint64_t n) {
-        const uint64_t F = src.cur_n;
-        const uint64_t w_lo = o < F ? d2h(src.cur_off + o) : src.cur_words;
-        const uint64_t w_hi = o + n < F ? d2h(src.cur_off + o + n) : src.cur_words;
-        if (&src == &t) {
-            ensure_off(t.nxt_off, t.nxt_off_cap, 0, std::max<uint64_t>(n, 1));
-            launch_rebase(t.cur_off + o, n, w_lo, t.nxt_off, stream);
-            std::swap(t.cur_off, t.nxt_off);
-            std::swap(t.cur_off_cap, t.nxt_off_cap);
-            t.cur_wbase = ring_wrap(t.cur_wbase + w_lo, t.rcap);
-        } else {
-            t.cur_words = t.nxt_words = 0;
-            t.cur_wbase = 0;
-            ensure_ring(t, w_hi - w_lo, 0);
-            ring_copy_out(src, ring_wrap(src.cur_wbase + w_lo, src.rcap), w_hi - w_lo, t.R);
-            ensure_off(t.cur_off, t.cur_off_cap, 0, std::max<uint64_t>(n, 1));
-            launch_rebase(src.cur_off + o, n, w_lo, t.cur_off, stream);
-        }
-        t.cur_words = w_hi - w_lo;
-        t.cur_n = n;
-        HIPCHK(hipStreamSynchronize(stream));
-    }
-
     // Replicated -> sharded, at the start of the first level with >= shard_min states.  Every
-    // shard holds that level whole (and every state seen so far in its seen set); shard i keeps
-    // parents [F*i/W, F*(i+1)/W) as its frontier, so parent references of the next level,
-    // (i << 48 | gid), name shard i's copy of them.  Earlier replicated levels are referenced as
-    // shard 0's (tag 0), whose copy stays intact: each shard writes new states only past its range.
+    // shard holds that level whole (RCCL: each rank its own copy; virtual: shard 0), and every
+    // state seen so far in its seen set (a superset of what it owns).  Shard t keeps the blocks
+    // b = t, t + W, ... of B = chunk_parents parents (the level's block-cyclic layout) in a fresh
+    // ring, their offsets rebased, their trace entries moved to the local gids of that layout.
+    // Earlier levels stay replicated: global id == local gid, answered by shard 0 / rank 0.
     void enter_sharded() {
         Shard &s0 = sh[0];
-        const size_t L = s0.level_start.size();
-        const uint64_t F = s0.cur_n, base = s0.level_start[L - 1];
-        auto off = [&](int i) { return F * (uint64_t)i / (uint64_t)W; };
+        const size_t Lz = s0.level_start.size();
+        const uint64_t F = s0.cur_n, base = s0.level_start[Lz - 1], B = chunk_parents;
         HIPCHK(hipStreamSynchronize(stream));
-        if (virt) {
-            for (int i = 1; i < W; i++) {
-                Shard &t = sh[i];
-                const uint64_t o = off(i), n = off(i + 1) - o;
+        glevel = s0.level_start;
+        L_shard = (int)Lz;
+        std::vector<uint64_t> hoff(F + 1);
+        if (F) HIPCHK(hipMemcpy(hoff.data(), s0.cur_off, F * 8, hipMemcpyDeviceToHost));
+        hoff[F] = s0.cur_words;
+        uint32_t *src = s0.R;
+        const uint64_t src_cap = s0.rcap, src_wbase = s0.cur_wbase;
+        uint64_t *src_off = s0.cur_off;
+        std::vector<uint32_t *> old_rings;
+        for (size_t ti = sh.size(); ti-- > 0;) {  // shard 0 last: its trace entries move in place
+            Shard &t = sh[ti];
+            const int id = t.id;
+            uint64_t n = 0, words = 0;
+            for (uint64_t b = (uint64_t)id; b * B < F; b += (uint64_t)W) {
+                const uint64_t lo = b * B, hi = std::min(F, lo + B);
+                n += hi - lo;
+                words += hoff[hi] - hoff[lo];
+            }
+            const uint64_t cap = std::max<uint64_t>(std::max<uint64_t>(words + words / 2, 1ull << 14), &t == &s0 ? s0.rcap : 0);
+            uint32_t *nr = dmalloc<uint32_t>(cap);
+            uint64_t *noff = dmalloc<uint64_t>(std::max<uint64_t>(n + n / 2, 1 << 16));
+            uint64_t at = 0, wat = 0;
+            for (uint64_t b = (uint64_t)id; b * B < F; b += (uint64_t)W) {
+                const uint64_t lo = b * B, hi = std::min(F, lo + B), w = hoff[hi] - hoff[lo];
+                const uint64_t from = ring_wrap(src_wbase + hoff[lo], src_cap);
+                const uint64_t n1 = std::min(w, src_cap - from);
+                if (n1) HIPCHK(hipMemcpyAsync(nr + wat, src + from, n1 * 4, hipMemcpyDeviceToDevice, stream));
+                if (w > n1) HIPCHK(hipMemcpyAsync(nr + wat + n1, src, (w - n1) * 4, hipMemcpyDeviceToDevice, stream));
+                launch_rebase(src_off + lo, hi - lo, hoff[lo] - wat, noff + at, stream);
+                // trace entries: global id base + g -> local gid base + local index (at <= lo: a
+                // forward in-place move on shard 0)
+                for (uint64_t i = 0; i < hi - lo; i++) {
+                    t.hpar.set(base + at + i, s0.hpar.get(base + lo + i));
+                    t.hslot.set(base + at + i, s0.hslot.get(base + lo + i));
+                }
+                at += hi - lo;
+                wat += w;
+            }
+            HIPCHK(hipStreamSynchronize(stream));
+            if (&t != &s0) {
+                // the seen set so far (virtual shards share one device)
                 if (s0.Tc) {
                     if (!t.Tc || t.T_cap != s0.T_cap) {
                         dfree(t.T);
                         dfree(t.Tc);
+                        t.T = nullptr;
                         t.Tc = dmalloc<unsigned long long>(s0.T_cap);
                         t.T_cap = s0.T_cap;
                     }
@@ -1281,24 +1318,33 @@ struct rmc_ctx {
                 }
                 t.T_count = s0.T_count;
                 t.level_start = s0.level_start;
-                t.level_start.back() = base + o;
-                take_parents(s0, t, o, n);
-                t.hpar.copy_from(s0.hpar, base + o, n);
-                t.hslot.copy_from(s0.hslot, base + o, n);
-                t.tflushed = base + o + n;
                 t.epoch = std::max(t.epoch, s0.epoch);
+                dfree(t.R);
+                dfree(t.cur_off);
+            } else {
+                old_rings.push_back(s0.R);
+                old_off_ = s0.cur_off;
             }
-            take_parents(s0, s0, 0, off(1));
-            s0.tflushed = base + off(1);
-        } else {
-            const uint64_t o = off(rank), n = off(rank + 1) - o;
-            take_parents(s0, s0, o, n);
-            s0.level_start.back() = base + o;
-            s0.tflushed = base + o + n;
+            t.R = nr;
+            t.rcap = cap;
+            t.ring_fixed = false;
+            t.cur_off = noff;
+            t.cur_off_cap = std::max<uint64_t>(n + n / 2, 1 << 16);
+            t.cur_wbase = 0;
+            t.cur_words = words;
+            t.nxt_words = 0;
+            t.cur_n = n;
+            t.nxt_n = 0;
+            t.tflushed = base + n;
+            t.tdev = t.tflushed;
         }
         HIPCHK(hipStreamSynchronize(stream));
+        for (uint32_t *r : old_rings) dfree(r);
+        dfree(old_off_);
+        old_off_ = nullptr;
         replicated = false;
     }
+    uint64_t *old_off_ = nullptr;
 
     // First error in TLC order among the error slots: smaller (parent, slot) first; on a
     // tie the Assert wins (its sub-action's batch is discarded).
@@ -1614,16 +1660,16 @@ struct rmc_ctx {
         return nst;
     }
 
-    // TLC's counters at the moment the first error (in -workers 1 order) is reported.
-    void stop_on_error(int kind, unsigned long long ek, uint64_t p0, uint64_t nxt_before, uint64_t gid_cur,
-                       uint64_t gid_nxt, uint64_t gen_before_chunk, rmc_level_stats *st) {
-        Shard &s = sh[0];
+    // The erroring chunk's share of TLC's counters at its first error (key ek, level-local parent
+    // p of the chunk starting at p0): successors generated by the chunk's parents up to the error
+    // (the whole sub-action batch of an invariant error -- TLC adds a batch before fingerprinting
+    // it -- none of an Assert's), and the chunk's winners before it.
+    struct ErrCounts { uint64_t gen, win; };
+    ErrCounts error_counts(Shard &s, int kind, unsigned long long ek, uint64_t p0, bool route) {
         HIPCHK(hipStreamSynchronize(stream));
-        const uint64_t p = ek >> 24;                       // level-local parent
+        const uint64_t p = ek >> 24;
         const uint32_t slot = (uint32_t)((ek >> 8) & 0xFFFF);
-        const int which = (int)(ek & 0xFF);
         const uint64_t pl = p - p0;
-        // successors of the chunk's parents before p, and winners before p
         uint64_t off_p = 0;
         if (pl) {
             std::vector<uint32_t> cn(pl);
@@ -1631,14 +1677,15 @@ struct rmc_ctx {
             for (uint32_t x : cn) off_p += x;
         }
         const uint64_t wbase = (uint64_t)d2h(s.boff + pl / WTILE) + d2h(s.wpos + pl);
-        // winners among p's first `upto` successor slots (election table of this chunk)
+        // winners among p's first `upto` successor slots
         auto winners_in = [&](uint32_t upto) -> uint64_t {
             if (!upto) return 0;
             std::vector<uint32_t> ls(upto);
             HIPCHK(hipMemcpy(ls.data(), s.lslot + pl * ks.maxsucc, upto * 4, hipMemcpyDeviceToHost));
             uint64_t w = 0;
             for (uint32_t r = 0; r < upto; r++)
-                if (ls[r] < LS_ELECT && ((uint32_t)d2h(s.L + ls[r]) >> 2) == (uint32_t)(pl * ks.maxsucc + r)) w++;
+                w += route ? ls[r] == LS_WIN
+                           : (ls[r] < LS_ELECT && ((uint32_t)d2h(s.L + ls[r]) >> 2) == (uint32_t)(pl * ks.maxsucc + r));
             return w;
         };
         // successors of p, in order, to find the sub-action batch boundaries
@@ -1647,18 +1694,26 @@ struct rmc_ctx {
         bool af = false;
         expand_one(&keys, nullptr, nullptr, &af);
         const uint32_t grp = slot >> 7;  // (server, action)
-        uint32_t cut = 0, batch_end = 0;
+        uint32_t cut = 0, batch_end = 0, before = 0;
         for (uint32_t k : keys) {
             if ((k >> 7) < grp) cut++;
             if ((k >> 7) <= grp) batch_end++;
+            if (k < slot) before++;
         }
-        uint64_t gen = gen_before_chunk + off_p;
-        uint64_t winners_before;
+        if (kind == ERR_INV || kind == ERR_EVAL) return {off_p + batch_end, wbase + winners_in(before)};
+        if (kind == ERR_ASSERT) return {off_p + cut, wbase + winners_in(cut)};
+        return {off_p, wbase};
+    }
+
+    // TLC's counters at the moment the first error (in -workers 1 order) is reported.
+    void stop_on_error(int kind, unsigned long long ek, uint64_t p0, uint64_t nxt_before, uint64_t gid_cur,
+                       uint64_t gid_nxt, uint64_t gen_before_chunk, rmc_level_stats *st) {
+        Shard &s = sh[0];
+        const uint64_t p = ek >> 24;
+        const int which = (int)(ek & 0xFF);
+        const ErrCounts ec = error_counts(s, kind, ek, p0, false);
+        const uint64_t gen = gen_before_chunk + ec.gen, winners_before = ec.win;
         if (kind == ERR_INV || kind == ERR_EVAL) {
-            gen += batch_end;  // TLC adds the whole sub-action's batch before fingerprinting it
-            uint32_t rank_ = 0;
-            for (uint32_t k : keys) rank_ += k < slot;
-            winners_before = wbase + winners_in(rank_);
             err_ref = gid_nxt + nxt_before + winners_before;
             total_distinct += nxt_before + winners_before + 1;
             queue_at_end = (s.cur_n - p - 1) + nxt_before + winners_before;
@@ -1666,8 +1721,6 @@ struct rmc_ctx {
             violated = which;
             depth = (int)s.level_start.size() + 1;
         } else {
-            if (kind == ERR_ASSERT) gen += cut;  // the failing sub-action's batch is never counted
-            winners_before = wbase + (kind == ERR_ASSERT ? winners_in(cut) : 0);
             err_ref = gid_cur + p;
             total_distinct += nxt_before + winners_before;
             queue_at_end = (s.cur_n - p - 1) + nxt_before + winners_before;
@@ -1686,205 +1739,359 @@ struct rmc_ctx {
         build_trace();
     }
 
-    // ---- sharded level (W > 1): fingerprint-owner partition, exchange, owner election --
-    // Order: chunk c of every shard's frontier, then source shard, then TLC order within
-    // the source's chunk.  Identical to TLC -workers 1 order when W == 1.
+    // ---- sharded level (W > 1) ------------------------------------------------------------------
+    // The level is laid out block-cyclically (glevel): round c expands the global blocks cW ..
+    // cW + W - 1, block cW + t on shard t, so the rounds follow the level's order, and inside a
+    // round every successor carries its global key (parent's index in the level, rank among its
+    // successors).  Each successor goes to its fingerprint's owner shard, which drops those its
+    // seen set holds and elects the smallest key per new fingerprint: the successor TLC -workers 1
+    // meets first (Raft.tla:34-38 -- the VIEW hides variables, so which representative of a class
+    // is kept depends on that order).  The verdicts come back, every shard commits its winners in
+    // TLC order (the fused winner count + commit), and the winners go to the shards that own their
+    // global next-level indices, appended in source order -- the level's order.  Levels, counters
+    // at an error and traces are those of W = 1.
+    KParams round_params(const Shard &s, uint64_t gbase) const {
+        KParams Q = chunk_params(s);
+        Q.p_begin = s.p0;
+        Q.p_end = s.p0 + s.np;
+        Q.route = 1;
+        Q.gid_parent_base = gbase + s.gblk - s.p0;  // level-local parent p -> its global id
+        Q.next = s.ob;
+        Q.noff = s.ooff;
+        Q.nbase = 0;
+        Q.next_wbase = 0;
+        Q.next_base = 0;
+        Q.xside = s.oside;
+        Q.gid_next_base = 0;
+        Q.trace_base = 0;
+        return Q;
+    }
+
+    void grow_recv(Shard &o, uint64_t R) {
+        if (R + 1 <= o.xr_cap) return;
+        const uint64_t nc = std::max<uint64_t>(R + R / 2 + 1, 1024);
+        HIPCHK(hipStreamSynchronize(stream));
+        dfree(o.xr); dfree(o.rslot); dfree(o.rflag);
+        o.xr = dmalloc<XItem>(nc);
+        o.rslot = dmalloc<uint32_t>(nc);
+        o.rflag = dmalloc<uint32_t>(nc);
+        o.xr_cap = nc;
+    }
+    void grow_outbox(Shard &s, uint64_t words, uint64_t n) {
+        if (words + 1 > s.ob_cap || n + 1 > s.os_cap) HIPCHK(hipStreamSynchronize(stream));
+        if (words + 1 > s.ob_cap) {
+            dfree(s.ob);
+            s.ob_cap = std::max<uint64_t>(words + words / 2 + 1, 1 << 16);
+            s.ob = dmalloc<uint32_t>(s.ob_cap);
+        }
+        if (n + 1 > s.os_cap) {
+            dfree(s.oside); dfree(s.ooff);
+            s.os_cap = std::max<uint64_t>(n + n / 2 + 1, 1 << 12);
+            s.oside = dmalloc<uint4>(s.os_cap);
+            s.ooff = dmalloc<uint64_t>(s.os_cap);
+        }
+    }
+    void grow_inbox(Shard &o, uint64_t words, uint64_t n) {
+        if (words + 1 > o.ib_cap || n + 1 > o.is_cap) HIPCHK(hipStreamSynchronize(stream));
+        if (words + 1 > o.ib_cap) {
+            dfree(o.ib);
+            o.ib_cap = std::max<uint64_t>(words + words / 2 + 1, 1 << 16);
+            o.ib = dmalloc<uint32_t>(o.ib_cap);
+        }
+        if (n + 1 > o.is_cap) {
+            dfree(o.iside); dfree(o.isz); dfree(o.ioff);
+            o.is_cap = std::max<uint64_t>(n + n / 2 + 1, 1 << 12);
+            o.iside = dmalloc<uint4>(o.is_cap);
+            o.isz = dmalloc<uint32_t>(o.is_cap);
+            o.ioff = dmalloc<uint32_t>(o.is_cap);
+        }
+    }
+
+    static constexpr int TAB = 6;  // per-shard round row: generated, winners, words, inserted, kind + 1, key
+
+#ifdef RMC_SHARD_DEBUG
+#define SDBG(x) do { HIPCHK(hipStreamSynchronize(stream)); std::fprintf(stderr, "sharded L%d c%llu phase %s\n", L, (unsigned long long)c, x); } while (0)
+#else
+#define SDBG(x) do {} while (0)
+#endif
     int step_sharded(rmc_level_stats *st) {
         auto t0 = std::chrono::steady_clock::now();
         const int L = (int)sh[0].level_start.size();
         st->level = L;
-        uint64_t agg[2] = {0, 0};
-        for (Shard &s : sh) agg[0] = std::max<uint64_t>(agg[0], (s.cur_n + chunk_parents - 1) / chunk_parents);
-        for (Shard &s : sh) { st->expanded += s.cur_n; s.nxt_n = 0; s.nxt_words = 0; }
-        allreduce(agg, 1, true);
-        const uint64_t nchunks = agg[0];
+        const uint64_t B = chunk_parents, MS = (uint64_t)ks.maxsucc;
+        uint64_t Fg = 0;
+        for (Shard &s : sh) { Fg += s.cur_n; s.nxt_n = 0; s.nxt_words = 0; }
+        allreduce(&Fg, 1, false);
+        st->expanded = Fg;
+        const uint64_t gbase = glevel[L - 1], rounds = (Fg + B * W - 1) / (B * W);
         const size_t NL = sh.size();
-        uint64_t level_gen = 0, level_new = 0;
-        std::vector<std::vector<uint64_t>> scnt(W, std::vector<uint64_t>(W, 0)), soff(W, std::vector<uint64_t>(W + 1, 0)),
-            rcnt, roff(W, std::vector<uint64_t>(W + 1, 0)), swin(W, std::vector<uint64_t>(W, 0)),
-            swoff(W, std::vector<uint64_t>(W + 1, 0)), rwin, rwoff(W, std::vector<uint64_t>(W + 1, 0));
-        std::vector<const void *> sendp(W);
-        std::vector<void *> recvp(W);
-        const uint64_t XW = (uint64_t)RECW + 4;
-        for (uint64_t c = 0; c < nchunks; c++) {
-            // (A) expand, fingerprint, partition by owner -- every local shard as a source
+        uint64_t level_gen = 0, level_new = 0, level_words = 0;
+        using VV = std::vector<std::vector<uint64_t>>;
+        auto prefix = [](const std::vector<uint64_t> &c) {
+            std::vector<uint64_t> o(c.size() + 1, 0);
+            for (size_t i = 0; i < c.size(); i++) o[i + 1] = o[i] + c[i];
+            return o;
+        };
+        std::vector<const void *> sp(NL);
+        std::vector<void *> rp(NL);
+        for (uint64_t c = 0; c < rounds; c++) {
+            // (1) expand the round's block: fingerprints, staged rows; successors per owner
+            VV scnt(NL, std::vector<uint64_t>(W, 0)), rcnt, soff(NL), roff(NL);
+            for (Shard &s : sh) {
+                s.p0 = c * B;
+                s.np = s.cur_n > s.p0 ? std::min<uint64_t>(B, s.cur_n - s.p0) : 0;
+                s.gblk = (c * (uint64_t)W + (uint64_t)s.id) * B;
+                HIPCHK(hipMemsetAsync(s.ocnt, 0, 64 * 4, stream));
+                HIPCHK(hipMemsetAsync(s.sum + 9, 0, 8, stream));
+                if (!s.np) continue;
+                timed(PH_HASH, [&] { ks.fused(round_params(s, gbase), stream); });
+                launch_route_count(s.fp, s.cnt, s.np, (uint32_t)MS, (uint32_t)W, s.ocnt, stream);
+            }
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
-                const uint64_t gid_cur = s.level_start[L - 1];
-                s.p0 = c * chunk_parents;
-                s.np = s.cur_n > s.p0 ? std::min<uint64_t>(chunk_parents, s.cur_n - s.p0) : 0;
-                s.G = 0;
-                std::fill(scnt[li].begin(), scnt[li].end(), 0);
-                if (!s.np) continue;
-                KParams Q = base(s);
-                ring_params(s, Q);
-                Q.p_begin = s.p0; Q.p_end = s.p0 + s.np; Q.cnt = s.cnt; Q.off = s.off; Q.fp = s.fp;
-                Q.gid_parent_base = gid_cur;
-                timed(PH_COUNT, [&] {
-                    ks.count(Q, stream);
-                    HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.cnt, s.off, (int)s.np + 1, stream));
-                });
-                s.G = d2h(s.off + s.np);
-                collect_times(st);
-                if (!s.G) continue;
-                int bits = 0;
-                while ((1 << bits) < W) bits++;
-                timed(PH_HASH, [&] { ks.hash(Q, stream); });
-                timed(PH_XCHG, [&] {
-                    HIPCHK(hipMemsetAsync(s.ocnt, 0, 64 * 8, stream));
-                    launch_owner_keys(s.fp, s.G, (uint32_t)W, s.okey, s.iota, s.ocnt, stream);
-                    HIPCHK(hipcub::DeviceRadixSort::SortPairs(s.tmp, s.tmp_bytes, s.okey, s.okey2, s.iota, s.perm,
-                                                              (int)s.G, 0, bits, stream));
-                    launch_gather_fp(s.fp, s.perm, s.G, s.sfp, stream);
-                });
-                HIPCHK(hipMemcpyAsync(s.hsum, s.ocnt, W * 8, hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipMemcpyAsync(s.hsum, s.ocnt, 64 * 4, hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
-                collect_times(st);
-                for (int d = 0; d < W; d++) scnt[li][d] = s.hsum[d];
-                level_gen += s.G;
+                const uint32_t *hc = reinterpret_cast<const uint32_t *>(s.hsum);
+                for (int d = 0; d < W; d++) scnt[li][d] = hc[d];
+                soff[li] = prefix(scnt[li]);
+                s.G = soff[li][W];
             }
-            for (size_t li = 0; li < NL; li++) {
-                soff[li][0] = 0;
-                for (int d = 0; d < W; d++) soff[li][d + 1] = soff[li][d] + scnt[li][d];
-            }
+            collect_times(st);
             exchange_counts(scnt, rcnt);
+            SDBG("0");
+            // (2) successors to their owners: owner-grouped items, cursors preset to the groups
             for (size_t li = 0; li < NL; li++) {
-                roff[li][0] = 0;
-                for (int q = 0; q < W; q++) roff[li][q + 1] = roff[li][q] + rcnt[li][q];
-                grow_recv(sh[li], roff[li][W]);
-                sendp[li] = sh[li].sfp;
-                recvp[li] = sh[li].rfp;
+                Shard &s = sh[li];
+                roff[li] = prefix(rcnt[li]);
+                grow_recv(s, roff[li][W]);
+                if (s.G) {
+                    grow_plain(s.xs, s.xs_cap, s.G);
+                    uint32_t *hc = reinterpret_cast<uint32_t *>(s.hsum);
+                    for (int d = 0; d < W; d++) hc[d] = (uint32_t)soff[li][d];
+                    HIPCHK(hipMemcpyAsync(s.ocnt, hc, W * 4, hipMemcpyHostToDevice, stream));
+                    timed(PH_XCHG, [&] {
+                        launch_route_place(s.fp, s.cnt, s.np, (uint32_t)MS, (uint32_t)W, s.ocnt, s.gblk, s.xs, s.perm,
+                                           stream);
+                    });
+                    HIPCHK(hipStreamSynchronize(stream));  // hsum is reused below
+                }
+                sp[li] = s.xs;
+                rp[li] = s.xr;
             }
-            timed(PH_XCHG, [&] { exchange_items(sendp, scnt, soff, recvp, roff, 16); });
-            // (B) owners: seen-set probe + election of the first (source, j) per fingerprint
+            SDBG("1");
+            timed(PH_XCHG, [&] { exchange_items(sp, scnt, soff, rp, roff, sizeof(XItem)); });
+            SDBG("2");
+            // (3) owners: seen-set probe, smallest key per new fingerprint, verdicts, seen-set insert
             for (size_t li = 0; li < NL; li++) {
                 Shard &o = sh[li];
                 const uint64_t R = roff[li][W];
+                sp[li] = o.rflag;
+                rp[li] = o.sflag;
                 if (!R) continue;
-                uint32_t Rv = (uint32_t)R;
-                HIPCHK(hipMemcpyAsync(o.rcount, &Rv, 4, hipMemcpyHostToDevice, stream));
-                uint64_t Lcap = std::min(next_pow2(2 * R), Lcap_max);
-                if (R * 2 > Lcap_max) throw Fail(RMC_E_CAPACITY, "owner receive batch exceeds the election table");
-                ++o.epoch;
+                grow_seen(o, o.T_count + R);
+                const uint64_t cap = owner_table(o, R);
                 timed(PH_DEDUP, [&] {
-                    launch_dedup(o.rfp, o.rcount, R, o.seen(), o.L, Lcap - 1, o.epoch, o.rlslot, stream);
-                    launch_recv_flags(o.rlslot, o.L, R, o.rflag, stream);
+                    launch_owner_elect(o.xr, R, o.seen(), o.OT, o.OK, cap - 1, o.rslot, stream);
+                    launch_owner_flags(o.xr, R, o.rslot, o.OK, o.seen(), o.rflag, o.sum + 9, stream);
                 });
-                HIPCHK(hipStreamSynchronize(stream));
             }
-            // flags back to the sources (reverse exchange)
-            for (size_t li = 0; li < NL; li++) { sendp[li] = sh[li].rflag; recvp[li] = sh[li].sflag; }
-            {
-                std::vector<std::vector<uint64_t>> rev(W, std::vector<uint64_t>(W, 0));
-                for (size_t li = 0; li < NL; li++)
-                    for (int q = 0; q < W; q++) rev[li][q] = rcnt[li][q];
-                timed(PH_XCHG, [&] { exchange_items(sendp, rev, roff, recvp, soff, 4); });
+            SDBG("3");
+            timed(PH_XCHG, [&] { exchange_items(sp, rcnt, roff, rp, soff, 4); });
+            SDBG("4");
+            // (4) sources: verdicts on the slots, winners per parent and their words
+            for (Shard &s : sh) {
+                if (!s.np) continue;
+                timed(PH_DEDUP, [&] {
+                    launch_scatter_win(s.perm, s.sflag, s.G, s.score, (uint32_t)sw4(), s.pnm, (uint32_t)MS, s.lslot,
+                                       s.wacc, stream);
+                    ks.wincount(round_params(s, gbase), s.np, stream);
+                });
             }
-            // (C) sources: winner positions in owner-grouped order, materialize into exchange records
+            SDBG("5");
+            std::vector<uint64_t> tab((size_t)TAB * W, 0);
+            std::vector<uint64_t> ins(NL, 0), wnum(NL, 0), wwords(NL, 0);
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
-                std::fill(swin[li].begin(), swin[li].end(), 0);
-                if (!s.G) { std::fill(swoff[li].begin(), swoff[li].end(), 0); continue; }
-                HIPCHK(hipcub::DeviceScan::ExclusiveSum(s.tmp, s.tmp_bytes, s.sflag, s.spos, (int)s.G + 1, stream));
-                std::vector<uint64_t> idx(W + 1);
-                for (int d = 0; d <= W; d++) idx[d] = soff[li][d];
-                HIPCHK(hipMemcpyAsync(s.pick_idx, idx.data(), (W + 1) * 8, hipMemcpyHostToDevice, stream));
-                launch_pick(s.spos, s.pick_idx, W + 1, s.sum, stream);
-                HIPCHK(hipMemcpyAsync(s.hsum, s.sum, (W + 1) * 8, hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 10 * 8, hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
-                for (int d = 0; d <= W; d++) swoff[li][d] = s.hsum[d];
-                for (int d = 0; d < W; d++) swin[li][d] = swoff[li][d + 1] - swoff[li][d];
-                grow_plain(s.sx, s.sx_cap, swoff[li][W] * XW + 1);
-                launch_scatter_flags(s.perm, s.sflag, s.spos, s.G, s.wflag, s.wpos, stream);
-                KParams Q = base(s);
-                ring_params(s, Q);
-                Q.p_begin = s.p0; Q.p_end = s.p0 + s.np; Q.cnt = s.cnt; Q.off = s.off; Q.fp = s.fp;
-                Q.wflag = s.wflag; Q.wpos = s.wpos; Q.xrec = s.sx; Q.gid_parent_base = s.level_start[L - 1];
-                timed(PH_MAT, [&] { ks.materialize(Q, stream); });
-            }
-            exchange_counts(swin, rwin);
-            for (size_t li = 0; li < NL; li++) {
-                rwoff[li][0] = 0;
-                for (int q = 0; q < W; q++) rwoff[li][q + 1] = rwoff[li][q] + rwin[li][q];
-                grow_plain(sh[li].rx, sh[li].rx_cap, rwoff[li][W] * XW + 1);
-                sendp[li] = sh[li].sx;
-                recvp[li] = sh[li].rx;
-            }
-            timed(PH_XCHG, [&] { exchange_items(sendp, swin, swoff, recvp, rwoff, XW * 4); });
-            // (D) owners: append winners (source-major) to the next level, seen-set insert
-            for (size_t li = 0; li < NL; li++) {
-                Shard &o = sh[li];
-                const uint64_t n = rwoff[li][W];
-                const uint64_t gid_nxt = o.level_start[L - 1] + o.cur_n;
-                if (n) {
-                    ensure_ring(o, n * (uint64_t)RECW, 0);
-                    ensure_off(o.nxt_off, o.nxt_off_cap, o.nxt_n, o.nxt_n + n);
-                    grow_trace(o, n);
-                    grow_seen(o, o.T_count + n);
-                    trace_restart(o);
-                    const uint64_t tb = gid_nxt + o.nxt_n - o.tdev;  // == 0: everything earlier is flushed
-                    timed(PH_OTHER, [&] {
-                        for (int q = 0; q < W; q++) {
-                            const uint64_t k = rwin[li][q];
-                            if (!k) continue;
-                            launch_accept(o.rx + rwoff[li][q] * XW, k, (uint32_t)RECW, o.R, o.rcap, o.nbase(),
-                                          o.nxt_words + rwoff[li][q] * (uint64_t)RECW, o.nxt_off + o.nxt_n + rwoff[li][q],
-                                          o.par + tb + rwoff[li][q], o.pslot + tb + rwoff[li][q], (uint64_t)q << 48, stream);
-                        }
-                        launch_insert_flagged(o.rfp, o.rflag, roff[li][W], o.seen(), stream);
-                    });
-                    flush_trace(o, gid_nxt + o.nxt_n + n);
-                    o.nxt_n += n;
-                    o.nxt_words += n * (uint64_t)RECW;
-                    o.T_count += n;
-                    level_new += n;
+                ins[li] = s.hsum[9];
+                if (s.np) {
+                    tab[TAB * s.id + 0] = s.hsum[0];
+                    wnum[li] = s.hsum[1];
+                    wwords[li] = s.hsum[SUM_WORDS];
                 }
             }
-            // errors: first in (source shard, parent, slot) order
-            std::vector<uint64_t> ebuf(2 * W, ~0ull);
+            collect_times(st);
+            SDBG("6");
+            // (5) commit: every shard's winners, in TLC order, into its outbox (+ invariants)
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
-                HIPCHK(hipMemcpyAsync(s.hsum, s.err, ERR_NSLOTS * 8, hipMemcpyDeviceToHost, stream));
-                HIPCHK(hipMemcpyAsync(s.hsum + 8, s.flags, 4, hipMemcpyDeviceToHost, stream));
+                if (!s.np) continue;
+                grow_outbox(s, wwords[li], wnum[li]);
+                if (wwords[li] >= s.rcap) ensure_ring(s, wwords[li], 0);  // P.rcap also bounds the outbox
+                timed(PH_MAT, [&] { ks.commit(round_params(s, gbase), stream); });
+            }
+            for (size_t li = 0; li < NL; li++) {
+                Shard &s = sh[li];
+                s.T_count += ins[li];
+                if (!s.np) continue;
+                HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
-                if ((uint32_t)s.hsum[8]) throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
+                HIPCHK(hipGetLastError());
+                if (s.hsum[2 + ERR_NSLOTS])
+                    throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
+                uint64_t *row = &tab[TAB * s.id];
+                row[1] = wnum[li];
+                row[2] = wwords[li];
+                row[3] = ins[li];
                 unsigned long long best;
-                const int kind = first_error(s.hsum, &best);
-                if (kind >= 0) { ebuf[2 * s.id] = (uint64_t)kind; ebuf[2 * s.id + 1] = best; }
-                HIPCHK(hipMemsetAsync(s.err, 0xFF, ERR_NSLOTS * 8, stream));
+                const int kind = first_error(s.hsum + 2, &best);
+                if (kind >= 0) {
+                    const uint64_t g = s.gblk + ((best >> 24) - s.p0);
+                    row[4] = (uint64_t)kind + 1;
+                    row[5] = (((g << 16) | ((best >> 8) & 0xFFFF)) << 8) | (best & 0xFF);
+                }
             }
-            if (!virt && W > 1) {
-                // gather every rank's (kind, key): ranks contribute only their own slots
-                std::vector<uint64_t> g(2 * W, 0);
-                for (int q = 0; q < 2 * W; q++) g[q] = (q / 2 == rank) ? ebuf[q] + 1 : 0;  // +1: ~0 -> 0
-                allreduce(g.data(), 2 * W, false);
-                for (int q = 0; q < 2 * W; q++) ebuf[q] = g[q] - 1;
-            }
-            for (int q = 0; q < W; q++) {
-                if (ebuf[2 * q] == ~0ull) continue;
-                uint64_t glob[2] = {level_gen, level_new};
-                allreduce(glob, 2, false);
-                stop_sharded(q, (int)ebuf[2 * q], ebuf[2 * q + 1], L, glob[0], glob[1], st);
+            collect_times(st);
+            SDBG("7");
+            allreduce(tab.data(), TAB * W, false);  // rows: each shard's own, zero elsewhere
+            // (6) the first error of the round in the level's order
+            int ek_shard = -1;
+            for (int t = 0; t < W; t++)
+                if (tab[TAB * t + 4] && (ek_shard < 0 || (tab[TAB * t + 5] >> 8) < (tab[TAB * ek_shard + 5] >> 8)))
+                    ek_shard = t;
+            if (ek_shard >= 0) {
+                sharded_stop(ek_shard, (int)tab[TAB * ek_shard + 4] - 1, tab[TAB * ek_shard + 5], L, tab, level_gen,
+                             level_new, Fg, gbase, st);
                 st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
                 seconds += st->seconds;
                 return status;
             }
+            SDBG("8");
+            // (7) winners to the shards owning their global next-level indices
+            std::vector<uint64_t> A(W + 1, level_new);
+            for (int t = 0; t < W; t++) A[t + 1] = A[t] + tab[TAB * t + 1];
+            VV pc(NL, std::vector<uint64_t>(W, 0)), pw(NL, std::vector<uint64_t>(W, 0)), pco(NL), pwo(NL), rpc, rpw;
+            std::vector<const void *> sps(NL), spw(NL);
+            std::vector<void *> rps(NL), rpw_(NL);
+            for (size_t li = 0; li < NL; li++) {
+                Shard &s = sh[li];
+                const uint64_t x0 = A[s.id], w = A[s.id + 1] - x0;
+                pco[li].assign(W, 0);
+                pwo[li].assign(W, 0);
+                sps[li] = s.oside;
+                spw[li] = s.ob;
+                if (!w) continue;
+                struct Piece { int d; uint64_t i0, i1, w0, w1; };
+                std::vector<Piece> pcs;
+                std::vector<int> seen_d(W, 0);
+                bool repeat = false;
+                for (uint64_t x = x0; x < x0 + w;) {
+                    const uint64_t b = x / B, y = std::min(x0 + w, (b + 1) * B);
+                    const int d = (int)(b % (uint64_t)W);
+                    repeat |= seen_d[d]++ > 0;
+                    pcs.push_back({d, x - x0, y - x0, 0, 0});
+                    x = y;
+                }
+                for (Piece &pe : pcs) {
+                    pe.w0 = d2h(s.ooff + pe.i0);
+                    pe.w1 = pe.i1 < w ? d2h(s.ooff + pe.i1) : wwords[li];
+                    pc[li][pe.d] += pe.i1 - pe.i0;
+                    pw[li][pe.d] += pe.w1 - pe.w0;
+                }
+                if (!repeat) {
+                    for (const Piece &pe : pcs) { pco[li][pe.d] = pe.i0; pwo[li][pe.d] = pe.w0; }
+                } else {
+                    // a destination owns several of the pieces: group them (in order) by destination
+                    grow_inbox(s, wwords[li], w);  // the inbox holds the grouped copy until the exchange
+                    uint64_t at = 0, wat = 0;
+                    for (int d = 0; d < W; d++) {
+                        pco[li][d] = at;
+                        pwo[li][d] = wat;
+                        for (const Piece &pe : pcs) {
+                            if (pe.d != d) continue;
+                            HIPCHK(hipMemcpyAsync(s.iside + at, s.oside + pe.i0, (pe.i1 - pe.i0) * 16,
+                                                  hipMemcpyDeviceToDevice, stream));
+                            HIPCHK(hipMemcpyAsync(s.ib + wat, s.ob + pe.w0, (pe.w1 - pe.w0) * 4, hipMemcpyDeviceToDevice,
+                                                  stream));
+                            at += pe.i1 - pe.i0;
+                            wat += pe.w1 - pe.w0;
+                        }
+                    }
+                    // the grouped copy goes out of the outbox buffers (the inbox is refilled below)
+                    HIPCHK(hipMemcpyAsync(s.oside, s.iside, w * 16, hipMemcpyDeviceToDevice, stream));
+                    HIPCHK(hipMemcpyAsync(s.ob, s.ib, wwords[li] * 4, hipMemcpyDeviceToDevice, stream));
+                    HIPCHK(hipStreamSynchronize(stream));
+                }
+            }
+            SDBG("9");
+            exchange_counts(pc, rpc);
+            exchange_counts(pw, rpw);
+            VV rro(NL), rrw(NL);
+            for (size_t li = 0; li < NL; li++) {
+                Shard &o = sh[li];
+                rro[li] = prefix(rpc[li]);
+                rrw[li] = prefix(rpw[li]);
+                grow_inbox(o, rrw[li][W], rro[li][W]);
+                rps[li] = o.iside;
+                rpw_[li] = o.ib;
+            }
+            timed(PH_XCHG, [&] {
+                exchange_items(sps, pc, pco, rps, rro, 16);
+                exchange_items(spw, pw, pwo, rpw_, rrw, 4);
+            });
+            SDBG("10");
+            // (8) owners append what they received, in source order, to the next level
+            for (size_t li = 0; li < NL; li++) {
+                Shard &o = sh[li];
+                const uint64_t n = rro[li][W], words = rrw[li][W];
+                if (!n) continue;
+                uint64_t consumed = 0;
+                if (o.ring_fixed) {
+                    const uint64_t done = std::min(o.cur_n, (c + 1) * B);
+                    consumed = done < o.cur_n ? d2h(o.cur_off + done) : o.cur_words;
+                }
+                ensure_ring(o, words, consumed);
+                ensure_off(o.nxt_off, o.nxt_off_cap, o.nxt_n, o.nxt_n + n);
+                const uint64_t gid = o.level_start[L - 1] + o.cur_n + o.nxt_n;  // local gid of the first
+                grow_trace(o, n);
+                trace_restart(o);
+                ensure_tmp(o, n + 1);
+                timed(PH_OTHER, [&] {
+                    ring_copy_in(o, ring_wrap(o.nbase() + o.nxt_words, o.rcap), o.ib, words);
+                    launch_side_sizes(o.iside, n, o.isz, stream);
+                    HIPCHK(hipMemsetAsync(o.isz + n, 0, 4, stream));
+                    HIPCHK(hipcub::DeviceScan::ExclusiveSum(o.tmp, o.tmp_bytes, o.isz, o.ioff, (int)n + 1, stream));
+                    launch_accept_side(o.iside, o.ioff, n, o.nxt_words, o.nxt_off + o.nxt_n, o.par + (gid - o.tdev),
+                                       o.pslot + (gid - o.tdev), stream);
+                });
+                flush_trace(o, gid + n);
+                o.nxt_n += n;
+                o.nxt_words += words;
+            }
+            SDBG("11");
+            for (int t = 0; t < W; t++) {
+                level_gen += tab[TAB * t + 0];
+                level_new += tab[TAB * t + 1];
+                level_words += tab[TAB * t + 2];
+            }
+            HIPCHK(hipStreamSynchronize(stream));
+            collect_times(st);
         }
-        uint64_t glob[2] = {level_gen, level_new};
-        allreduce(glob, 2, false);
-        total_generated += glob[0];
-        total_distinct += glob[1];
-        st->generated = glob[0];
-        st->new_states = glob[1];
+        total_generated += level_gen;
+        total_distinct += level_new;
+        st->generated = level_gen;
+        st->new_states = level_new;
+        st->new_bytes = level_words * 4;
         for (Shard &s : sh) {
             const uint64_t gid_nxt = s.level_start[L - 1] + s.cur_n;
-            st->new_bytes += s.nxt_words * 4;
             s.peak_words = std::max(s.peak_words, s.cur_words + s.nxt_words);
             end_level(s, gid_nxt, L);
             if (!s.cur_n) s.level_start.push_back(gid_nxt);  // every shard keeps the same level count
         }
+        glevel.push_back(gbase + Fg);
         HIPCHK(hipStreamSynchronize(stream));
-        if (glob[1]) {
+        if (level_new) {
             depth = L + 1;
         } else {
             finished = true;
@@ -1893,56 +2100,77 @@ struct rmc_ctx {
         }
         st->total_generated = total_generated;
         st->total_distinct = total_distinct;
-        st->queue = glob[1];
+        st->queue = level_new;
         st->status = finished ? RMC_DONE : RMC_OK;
         st->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         seconds += st->seconds;
         return st->status;
     }
 
-    // Sharded stop: the error's shard q, kind, key (parent in q's level, slot).  Counters are
-    // those at the end of the chunk (every chunk is processed by all shards together).
-    void stop_sharded(int q, int kind, unsigned long long ek, int L, uint64_t gen, uint64_t nw, rmc_level_stats *st) {
-        const uint64_t p = ek >> 24;
-        const uint32_t slot = (uint32_t)((ek >> 8) & 0xFFFF);
-        total_generated += gen;
-        total_distinct += nw;
-        uint64_t gid_cur = 0;
+    // Sharded stop at the round's first error (shard e, kind, global key gk = (g << 16 | slot) << 8
+    // | which): TLC's counters -- every earlier round, the round's shards before e (their blocks
+    // come first in the level), and e's own share up to the error (error_counts).
+    void sharded_stop(int e, int kind, uint64_t gk, int L, const std::vector<uint64_t> &tab, uint64_t level_gen,
+                      uint64_t level_new, uint64_t Fg, uint64_t gbase, rmc_level_stats *st) {
+        const uint64_t g = gk >> 24;
+        const uint32_t slot = (uint32_t)((gk >> 8) & 0xFFFF);
+        uint64_t loc[2] = {0, 0};
         for (Shard &s : sh)
-            if (s.id == q) gid_cur = s.level_start[L - 1];
-        uint64_t g[1] = {virt ? gid_cur : (q == rank ? gid_cur : 0)};
-        allreduce(g, 1, false);
-        err_ref = ((uint64_t)q << 48) | (g[0] + p);
+            if (s.id == e) {
+                const uint64_t p = s.p0 + (g - s.gblk);
+                const unsigned long long ek = (((p << 16) | slot) << 8) | (gk & 0xFF);
+                const ErrCounts ec = error_counts(s, kind, ek, s.p0, true);
+                loc[0] = ec.gen;
+                loc[1] = ec.win;
+            }
+        allreduce(loc, 2, false);
+        uint64_t gen = level_gen + loc[0], winb = level_new + loc[1];
+        for (int t = 0; t < e; t++) {
+            gen += tab[TAB * t + 0];
+            winb += tab[TAB * t + 1];
+        }
+        err_ref = gbase + g;
+        queue_at_end = (Fg - g - 1) + winb;
         if (kind == ERR_INV || kind == ERR_EVAL) {
             status = kind == ERR_INV ? RMC_VIOLATION : RMC_EVAL_ERROR;
-            violated = (int)(ek & 0xFF);
+            violated = (int)(gk & 0xFF);
             err_last_slot = slot;
+            total_distinct += winb + 1;
             depth = L + 1;
         } else {
             status = kind == ERR_ASSERT ? RMC_ASSERT : RMC_DEADLOCK;
             err_last_slot = KEY_NONE;
+            total_distinct += winb;
+            if (winb) depth = L + 1;
         }
-        queue_at_end = 0;
+        total_generated += gen;
         st->generated = gen;
-        st->new_states = nw;
+        st->new_states = winb + ((kind == ERR_INV || kind == ERR_EVAL) ? 1 : 0);
         st->total_generated = total_generated;
         st->total_distinct = total_distinct;
+        st->queue = queue_at_end;
         st->status = status;
         finished = true;
         build_trace();
     }
 
-    // parent reference and slot of a state (shard << 48 | local gid), from whichever rank holds it
-    void fetch_par(uint64_t ref, uint64_t *par, uint16_t *slot) {
-        const int q = (int)(ref >> 48);
-        const uint64_t gid = ref & ((1ull << 48) - 1);
+    // parent's global id and slot of the state with global id G, from whichever shard holds it
+    void fetch_par(uint64_t G, uint64_t *par, uint16_t *slot) {
         uint64_t v[2] = {0, 0};
-        for (Shard &s : sh)
-            if (s.id == q) {
-                if (gid >= s.tflushed) throw Fail(RMC_E_STATE, "trace entry not on the host");
-                v[0] = s.hpar.get(gid) + 1;  // +1: the Init sentinel ~0 travels as 0
-                v[1] = s.hslot.get(gid);
-            }
+        auto take = [&](const Shard &s, uint64_t gid) {
+            if (gid >= s.tflushed) throw Fail(RMC_E_STATE, "trace entry not on the host");
+            v[0] = s.hpar.get(gid) + 1;  // +1: the Init sentinel ~0 travels as 0
+            v[1] = s.hslot.get(gid);
+        };
+        if (L_shard == 0 || G < glevel[L_shard - 1]) {
+            if (virt || rank == 0) take(sh[0], G);  // replicated levels: global id == local gid
+        } else {
+            const size_t k = (size_t)(std::upper_bound(glevel.begin(), glevel.end(), G) - glevel.begin()) - 1;
+            const uint64_t g = G - glevel[k], B = chunk_parents;
+            const int owner = (int)((g / B) % (uint64_t)W);
+            for (const Shard &s : sh)
+                if (s.id == owner) take(s, s.level_start[k] + (g / (B * W)) * B + g % B);
+        }
         allreduce(v, 2, false);
         *par = v[0] - 1;
         *slot = (uint16_t)v[1];
@@ -2190,6 +2418,9 @@ struct rmc_ctx {
         err_ref = 0;
         err_last_slot = KEY_NONE;
         seconds = 0;
+        glevel.clear();
+        L_shard = 0;
+        replicated = false;
     }
 
     void result(rmc_result *r) const {

@@ -96,8 +96,11 @@ struct KParams {
     // errors: atomicMin keys (p << 16 | slot), level-local p
     unsigned long long *err;
     uint32_t *flags;           // [0] msg-cap overflow, [1] violated invariant bit, [2] eval-error invariant bit
-    // sharded mode: winners go to owner-grouped exchange records (RECW_MAX + 4 words each)
-    uint32_t *xrec;
+    // sharded round (W > 1): expand writes fingerprints only (the owners probe and elect), commit
+    // takes lslot == LS_WIN as the verdict and writes each winner's trace entry to its sidecar
+    // xside[i] = {parent global id lo, hi, slot key, record words} instead of par / pslot
+    int route;
+    uint4 *xside;
     // fused single-shard level: expand (+hash, +seen-set probe, +election, +staging) -> wincount
     // -> commit.  Successor slot q = (p - p_begin) * maxsucc + rank is sparse and increases in
     // TLC order; it indexes fp, lslot and score (the staged successor: its acting server's row,
@@ -130,9 +133,6 @@ struct KParams {
 
 struct KernelSet {
     int N, V, MR, MCAP, CCW, RECW_MAX, maxsucc;
-    void (*count)(const KParams &, hipStream_t);
-    void (*hash)(const KParams &, hipStream_t);
-    void (*materialize)(const KParams &, hipStream_t);
     void (*single)(const KParams &, hipStream_t);           // all successors of front[0] -> next, fp, out_keys
     void (*fused)(const KParams &, hipStream_t);            // expand + hash + probe + election + staging
     void (*wincount)(const KParams &, uint64_t np, hipStream_t);  // winners per parent + their scan, successors generated
@@ -149,26 +149,29 @@ struct KernelSet {
 bool get_kernels(int N, int V, int msg_cap, KernelSet *ks);
 
 // generic (template-free) kernels
-void launch_dedup(const ulonglong2 *fp, const uint32_t *Gp, uint64_t Gub, Seen seen,
-                  unsigned long long *L, uint64_t Lmask, uint32_t epoch, uint32_t *lslot, hipStream_t s);
-constexpr uint32_t LS_SEEN = 0xFFFFFFFFu, LS_ELECT = 0xFFFFFFFEu;
-void launch_owner_keys(const ulonglong2 *fp, uint64_t G, uint32_t W, uint32_t *key, uint32_t *iota,
-                       unsigned long long *cnt, hipStream_t s);
-void launch_gather_fp(const ulonglong2 *fp, const uint32_t *perm, uint64_t G, ulonglong2 *out, hipStream_t s);
-void launch_recv_flags(const uint32_t *lslot, const unsigned long long *L, uint64_t R, uint32_t *flag, hipStream_t s);
-void launch_scatter_flags(const uint32_t *perm, const uint32_t *sflag, const uint32_t *spos, uint64_t G,
-                          uint32_t *wflag, uint32_t *wpos, hipStream_t s);
-// owner side: n exchange records (recw + 4 words each) -> the next level at ring position nbase,
-// level-relative word offsets rel0 + q * recw (noff), trace entries (par / pslot already offset)
-void launch_accept(const uint32_t *xrec, uint64_t n, uint32_t recw, uint32_t *ring, uint64_t rcap, uint64_t nbase,
-                   uint64_t rel0, uint64_t *noff, uint64_t *par, uint16_t *pslot, uint64_t src_tag, hipStream_t s);
-void launch_insert_flagged(const ulonglong2 *fp, const uint32_t *flag, uint64_t n, Seen seen, hipStream_t s);
-void launch_pick(const uint32_t *a, const uint64_t *idx, int n, unsigned long long *out, hipStream_t s);
-void launch_owner_of(const ulonglong2 *fp, uint32_t W, uint32_t *out, hipStream_t s);
+constexpr uint32_t LS_SEEN = 0xFFFFFFFFu, LS_ELECT = 0xFFFFFFFEu, LS_WIN = 0xFFFFFFFDu;
 // full-slot table -> (full or compact) table
 void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, Seen dst, hipStream_t s);
 void launch_insert_fps(const ulonglong2 *fp, uint64_t n, Seen seen, hipStream_t s);
 // out[i] = in[i] - sub (offset arrays rebased to a new level start)
 void launch_rebase(const uint64_t *in, uint64_t n, uint64_t sub, uint64_t *out, hipStream_t s);
+
+// sharded round (W > 1), rmc_engine.hip step_sharded: a successor on its way to its fingerprint's
+// owner shard -- the fingerprint and its global key (parent's index in the level << 8 | rank)
+struct XItem { unsigned long long x, y, key; };
+void launch_route_count(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
+                        uint32_t *ocnt, hipStream_t s);
+void launch_route_place(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
+                        uint32_t *cursor, uint64_t g0, XItem *items, uint32_t *perm, hipStream_t s);
+void launch_owner_elect(const XItem *it, uint64_t R, Seen seen, ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
+                        uint32_t *rslot, hipStream_t s);
+void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const unsigned long long *OK, Seen seen,
+                        uint32_t *flag, unsigned long long *inserted, hipStream_t s);
+void launch_scatter_win(const uint32_t *perm, const uint32_t *flag, uint64_t G, const uint4 *score, uint32_t sw4,
+                        const uint32_t *pnm, uint32_t maxsucc, uint32_t *lslot, uint32_t *wacc, hipStream_t s);
+void launch_side_sizes(const uint4 *side, uint64_t n, uint32_t *sz, hipStream_t s);
+void launch_accept_side(const uint4 *side, const uint32_t *off, uint64_t n, uint64_t rel0, uint64_t *noff,
+                        uint64_t *par, uint16_t *pslot, hipStream_t s);
+void launch_owner_of(const ulonglong2 *fp, uint32_t W, uint32_t *out, hipStream_t s);
 
 }  // namespace rmc

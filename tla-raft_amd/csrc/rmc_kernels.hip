@@ -54,7 +54,7 @@ extern "C" int rmc_debug_phases(unsigned long long *out, int reset) {
 
 namespace rmc {
 
-enum Mode { M_COUNT = 0, M_HASH = 1, M_MAT = 2, M_SINGLE = 3, M_FUSED = 4 };
+enum Mode { M_SINGLE = 3, M_FUSED = 4 };
 
 template <int N>
 __device__ __forceinline__ uint32_t sel(const uint32_t *a, int i) {
@@ -1073,7 +1073,7 @@ template <int N, int V, int MR, int MODE>
 __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void k_expand(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
-    constexpr bool SUMS = (MODE == M_HASH || MODE == M_SINGLE || MODE == M_FUSED);
+    constexpr bool SUMS = true;
     __shared__ uint16_t ids[S::MCAP];
     __shared__ ulonglong2 sPart[SUMS ? 64 : 1];         // partial minima per (successor, permutation block)
     __shared__ uint64_t M0[N * N], M1[N * N];
@@ -1144,7 +1144,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void 
         }
         const uint64_t pl = p - P.p_begin;  // chunk-local parent index
         uint64_t am = 0;
-        if (MODE == M_COUNT || MODE == M_SINGLE || MODE == M_FUSED) {
+        {
             bool ovf = false;
 #pragma unroll
             for (int r = 0; r <= MR; r++) ovf |= cand[r].key != KEY_NONE && W.nm + cand[r].nadd > (uint32_t)S::MCAP;
@@ -1159,13 +1159,12 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void 
                 if (lane == 0) atomicMin(&P.err[ERR_ASSERT], (((unsigned long long)p << 16) | best) << 8);
             }
         }
-        if (MODE == M_COUNT || MODE == M_FUSED) {
+        if (MODE == M_FUSED) {
             if (lane == 0) {
                 P.cnt[pl] = total;
                 if (MODE == M_FUSED) P.pnm[pl] = W.nm;
                 if (total == 0 && !am && P.check_deadlock) atomicMin(&P.err[ERR_DEADLOCK], ((unsigned long long)p << 16) << 8);
             }
-            if (MODE == M_COUNT) continue;
         }
         PHASE(2);
         if (MODE == M_FUSED) {
@@ -1269,6 +1268,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void 
                     // the seen set is read-only in this launch (commit inserts)
                     const uint64_t q = pl * (uint64_t)S::MAXS + lo;
                     P.fp[q] = f;
+                    if (P.route) return;  // sharded round: the fingerprint's owner probes and elects
                     // the election slot's first word goes out with the seen-set probe: one
                     // round trip fewer for a new fingerprint
                     const uint64_t g0 = l_index(f, P.Lmask);
@@ -1279,7 +1279,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void 
                                      ? LS_SEEN
                                      : elect_slot<S::MAXS>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g0, v0);
                 } else {
-                    P.fp[((MODE == M_HASH) ? (uint64_t)P.off[pl] : 0ull) + lo] = f;
+                    P.fp[lo] = f;
                 }
             };
             if (SIG) {
@@ -1398,56 +1398,20 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void 
             }
         }
         PHASE(5);
-        if (MODE == M_HASH || MODE == M_FUSED) continue;
-        // MATERIALIZE / SINGLE: write chosen successors
+        if (MODE == M_FUSED) continue;
+        // SINGLE: every successor, in TLC order
 #pragma unroll
         for (int r = 0; r <= MR; r++) {
-            bool win = false;
-            uint64_t out = 0;
-            if (cand[r].key != KEY_NONE) {
-                if (MODE == M_SINGLE) {
-                    win = true;
-                    out = rank[r];
-                    P.out_keys[out] = cand[r].key;
-                } else {
-                    // sharded: the winner goes to its owner's exchange slot with a sidecar
-                    // (parent reference, slot key); the owner inserts it into its seen set
-                    const uint64_t j = P.off[pl] + rank[r];
-                    win = P.wflag[j] != 0;
-                    if (win) {
-                        out = P.wpos[j];
-                        uint32_t *side = P.xrec + out * (uint64_t)(S::RECW_MAX + 4) + S::RECW_MAX;
-                        {
-                            const uint64_t pref = P.gid_parent_base + p;
-                            side[0] = (uint32_t)pref;
-                            side[1] = (uint32_t)(pref >> 32);
-                            side[2] = cand[r].key;
-                            side[3] = 0;
-                        }
-                        int which = 0;
-                        MsgView mv{P.front, W.idw, P.rcap, W.nm, 0u, 0u, cand[r].nadd, P.t.info};
-                        succ_adds(cand[r], &mv.add0, &mv.add1);
-                        uint32_t cc[Lo::NW];
-#pragma unroll
-                        for (int w = 0; w < Lo::NW; w++) cc[w] = cand[r].c[w];
-                        const int iv = check_invs<N, V>(cc, P.inv_order, &which, mv);
-                        if (iv != 1) {
-                            const unsigned long long ek =
-                                ((((unsigned long long)p << 16) | cand[r].key) << 8) | (unsigned long long)which;
-                            atomicMin(&P.err[iv == 0 ? ERR_INV : ERR_EVAL], ek);
-                        }
-                    }
-                }
-            }
-            const uint64_t stride = (MODE == M_MAT) ? (uint64_t)(S::RECW_MAX + 4) : (uint64_t)S::RECW_MAX;
-            uint32_t *dst = (MODE == M_MAT) ? P.xrec : P.next;
+            const bool win = cand[r].key != KEY_NONE;
+            const uint64_t out = rank[r];
+            if (win) P.out_keys[out] = cand[r].key;
             for (uint64_t m = __ballot(win); m; m &= m - 1) {
                 const int t = __ffsll((unsigned long long)m) - 1;
                 const uint64_t ot = rdlane64(out, t);
-                write_record<N, V, MR>(W, cand[r], t, lane, dst + ot * stride);
+                write_record<N, V, MR>(W, cand[r], t, lane, P.next + ot * (uint64_t)S::RECW_MAX);
             }
         }
-        if (MODE == M_SINGLE && lane == 0) *P.out_count = total;
+        if (lane == 0) *P.out_count = total;
     }
     PHASE_FLUSH;
 }
@@ -1709,7 +1673,7 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
             bool win = false;
             if (r < t) {
                 const uint32_t g = r0 == 0 ? g0 : P.lslot[q];
-                win = g < LS_ELECT && elect_q(P.L[g]) == (uint32_t)q;
+                win = P.route ? g == LS_WIN : (g < LS_ELECT && elect_q(P.L[g]) == (uint32_t)q);
             }
             const uint64_t m = __ballot(win);
             if (!m) continue;
@@ -1729,10 +1693,17 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
                 const uint32_t key = sb.z & 0xFFFFu, nadd = sb.z >> 16;
                 size = (uint32_t)S::CCW + ((nm + nadd + 1u) >> 1);
                 const uint64_t out = P.next_base + w0 + done + (uint32_t)__popcll(m & lt_mask);
-                const uint64_t gid = P.gid_next_base + out;
-                seen_insert(P.seen, P.fp[q]);
-                P.par[gid - P.trace_base] = P.gid_parent_base + p;
-                P.pslot[gid - P.trace_base] = (uint16_t)key;
+                if (P.route) {
+                    // sharded round: the owner already inserted the fingerprint; the trace entry
+                    // travels with the record to the state's next-level owner
+                    const uint64_t pref = P.gid_parent_base + p;
+                    P.xside[out] = make_uint4((uint32_t)pref, (uint32_t)(pref >> 32), key, size);
+                } else {
+                    const uint64_t gid = P.gid_next_base + out;
+                    seen_insert(P.seen, P.fp[q]);
+                    P.par[gid - P.trace_base] = P.gid_parent_base + p;
+                    P.pslot[gid - P.trace_base] = (uint16_t)key;
+                }
                 int which = 0;
                 const MsgView mv{P.front, idw, P.rcap, nm, sb.w, sc.x, nadd, P.t.info};
                 const int iv = check_invs<N, V>(c, P.inv_order, &which, mv);
@@ -1780,15 +1751,6 @@ static inline unsigned grid_for(uint64_t n) {
 
 template <int N, int V, int MR>
 struct Launch {
-    static void count(const KParams &P, hipStream_t s) {
-        hipLaunchKernelGGL((k_expand<N, V, MR, M_COUNT>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
-    }
-    static void hash(const KParams &P, hipStream_t s) {
-        hipLaunchKernelGGL((k_expand<N, V, MR, M_HASH>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
-    }
-    static void mat(const KParams &P, hipStream_t s) {
-        hipLaunchKernelGGL((k_expand<N, V, MR, M_MAT>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
-    }
     static void single(const KParams &P, hipStream_t s) {
         hipLaunchKernelGGL((k_expand<N, V, MR, M_SINGLE>), dim3(1), dim3(64), 0, s, P);
     }
@@ -1817,9 +1779,6 @@ static void fill(KernelSet *ks) {
     using S = Spec<N, V, MR>;
     ks->N = N; ks->V = V; ks->MR = MR; ks->MCAP = S::MCAP; ks->CCW = S::CCW; ks->RECW_MAX = S::RECW_MAX;
     ks->maxsucc = S::MAXS;
-    ks->count = &Launch<N, V, MR>::count;
-    ks->hash = &Launch<N, V, MR>::hash;
-    ks->materialize = &Launch<N, V, MR>::mat;
     ks->single = &Launch<N, V, MR>::single;
     ks->fused = &Launch<N, V, MR>::fused;
     ks->wincount = &Launch<N, V, MR>::wincount;
@@ -1841,40 +1800,6 @@ bool get_kernels(int N, int V, int msg_cap, KernelSet *ks) {
     RMC_CASE(5, 1, 2) RMC_CASE(5, 2, 2)
 #undef RMC_CASE
     return false;
-}
-
-// ---- seen-set / chunk dedup (thread per successor) -------------------------------------
-// Probe the global seen set (read-only in this launch) and, for fingerprints not in it, elect
-// the first successor in TLC order per fingerprint in the chunk table L (slots hold
-// chunk-local successor indices; index order == TLC order).
-__global__ __launch_bounds__(256) void k_dedup(const ulonglong2 *__restrict__ fp, const uint32_t *__restrict__ Gp,
-                                               Seen seen, unsigned long long *L, uint64_t Lmask, uint32_t epoch,
-                                               uint32_t *lslot) {
-    // L slots hold (epoch << 32) | j; a slot whose epoch is not this chunk's is empty, so
-    // the table never needs clearing.  atomicMin on the packed word keeps the smallest j
-    // (= first in TLC order) per fingerprint.
-    const uint64_t G = *Gp;
-    const unsigned long long tag = (unsigned long long)epoch << 32;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < G; j += (uint64_t)gridDim.x * blockDim.x) {
-        const ulonglong2 f = fp[j];
-        if (seen_contains(seen, f)) { lslot[j] = 0xFFFFFFFFu; continue; }
-        uint64_t g = (f.x ^ (f.x >> 31) ^ (f.y >> 7)) & Lmask;
-        const unsigned long long mine = tag | (unsigned long long)j;
-        for (;;) {
-            unsigned long long v = __hip_atomic_load(&L[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((v >> 32) != epoch) {
-                const unsigned long long prev = atomicCAS(&L[g], v, mine);
-                if (prev == v) break;
-                v = prev;
-            }
-            if ((v >> 32) == epoch) {
-                const ulonglong2 o = fp[(uint32_t)v];
-                if (o.x == f.x && o.y == f.y) { atomicMin(&L[g], mine); break; }
-            }
-            g = (g + 1) & Lmask;
-        }
-        lslot[j] = (uint32_t)g;
-    }
 }
 
 __global__ __launch_bounds__(256) void k_rehash(const ulonglong2 *__restrict__ Told, uint64_t old_cap, Seen dst) {
@@ -1901,10 +1826,6 @@ static inline unsigned grid256(uint64_t n) {
     return (unsigned)(b < cap ? (b ? b : 1) : cap);
 }
 
-void launch_dedup(const ulonglong2 *fp, const uint32_t *Gp, uint64_t Gub, Seen seen, unsigned long long *L,
-                  uint64_t Lmask, uint32_t epoch, uint32_t *lslot, hipStream_t s) {
-    hipLaunchKernelGGL(k_dedup, dim3(grid256(Gub)), dim3(256), 0, s, fp, Gp, seen, L, Lmask, epoch, lslot);
-}
 void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, Seen dst, hipStream_t s) {
     hipLaunchKernelGGL(k_rehash, dim3(grid256(old_cap)), dim3(256), 0, s, Told, old_cap, dst);
 }
@@ -1915,111 +1836,196 @@ void launch_rebase(const uint64_t *in, uint64_t n, uint64_t sub, uint64_t *out, 
     if (n) hipLaunchKernelGGL(k_rebase, dim3(grid256(n)), dim3(256), 0, s, in, n, sub, out);
 }
 
-// ---- sharded exchange helpers (one GPU per owner shard) -------------------------------------
-// owner(fp) = hi bits of fp mod W -- independent of the seen-set index bits
+// ---- sharded round (W > 1) -------------------------------------------------------------------
+// owner(fp) = high bits of fp.y mod W -- independent of the seen-set and election index bits
 __device__ __forceinline__ uint32_t fp_owner(const ulonglong2 f, uint32_t W) {
     return (uint32_t)((f.y >> 40) % W);
 }
 
-__global__ __launch_bounds__(256) void k_owner_keys(const ulonglong2 *__restrict__ fp, uint64_t G, uint32_t W,
-                                                    uint32_t *__restrict__ key, uint32_t *__restrict__ iota,
-                                                    unsigned long long *__restrict__ cnt) {
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < G; j += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t o = fp_owner(fp[j], W);
-        key[j] = o;
-        iota[j] = (uint32_t)j;
-        atomicAdd(&cnt[o], 1ull);
+// Source: successors of the round's parents (sparse slots q = pl * maxsucc + r, r < cnt[pl]) per
+// owner, into ocnt[W] (zeroed by the caller).
+__global__ __launch_bounds__(256) void k_route_count(const ulonglong2 *__restrict__ fp, const uint32_t *__restrict__ cnt,
+                                                     uint64_t np, uint32_t maxsucc, uint32_t W, uint32_t *__restrict__ ocnt) {
+    __shared__ uint32_t h[64];
+    if (threadIdx.x < 64) h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint64_t pl = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; pl < np; pl += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t t = cnt[pl];
+        for (uint32_t r = 0; r < t; r++) atomicAdd(&h[fp_owner(fp[pl * maxsucc + r], W)], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < W && h[threadIdx.x]) atomicAdd(&ocnt[threadIdx.x], h[threadIdx.x]);
+}
+
+// Source: every successor to its owner's segment of the send buffer (cursor[o] = the segment's
+// next free item, preset to its start): {fingerprint, global key = (parent's global index in the
+// level << 8) | rank among its successors} -- the key orders the level's successors as TLC
+// generates them -- and perm[item] = its slot q, for the owner's verdict to come back to.
+__global__ __launch_bounds__(256) void k_route_place(const ulonglong2 *__restrict__ fp, const uint32_t *__restrict__ cnt,
+                                                     uint64_t np, uint32_t maxsucc, uint32_t W, uint32_t *__restrict__ cursor,
+                                                     uint64_t g0, XItem *__restrict__ items, uint32_t *__restrict__ perm) {
+    __shared__ uint32_t h[64], base[64];
+    for (uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x; t0 < np; t0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t pl = t0 + threadIdx.x;
+        if (threadIdx.x < 64) h[threadIdx.x] = 0;
+        __syncthreads();
+        const uint32_t t = pl < np ? cnt[pl] : 0u;
+        for (uint32_t r = 0; r < t; r++) atomicAdd(&h[fp_owner(fp[pl * maxsucc + r], W)], 1u);
+        __syncthreads();
+        if (threadIdx.x < W) {
+            const uint32_t c = h[threadIdx.x];
+            base[threadIdx.x] = c ? atomicAdd(&cursor[threadIdx.x], c) : 0u;
+            h[threadIdx.x] = 0;
+        }
+        __syncthreads();
+        for (uint32_t r = 0; r < t; r++) {
+            const uint64_t q = pl * maxsucc + r;
+            const ulonglong2 f = fp[q];
+            const uint32_t o = fp_owner(f, W);
+            const uint32_t pos = base[o] + atomicAdd(&h[o], 1u);
+            items[pos] = XItem{f.x, f.y, ((g0 + pl) << 8) | r};
+            perm[pos] = (uint32_t)q;
+        }
+        __syncthreads();
     }
 }
 
-// gather fingerprints into owner-grouped order (perm from a stable radix sort by owner)
-__global__ __launch_bounds__(256) void k_gather_fp(const ulonglong2 *__restrict__ fp, const uint32_t *__restrict__ perm,
-                                                   uint64_t G, ulonglong2 *__restrict__ out) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (uint64_t)gridDim.x * blockDim.x)
-        out[i] = fp[perm[i]];
-}
-
-// owner: winner flags of the received items (plain u32 0/1), from the chunk election table
-__global__ __launch_bounds__(256) void k_recv_flags(const uint32_t *__restrict__ lslot,
-                                                    const unsigned long long *__restrict__ L, uint64_t R,
-                                                    uint32_t *__restrict__ flag) {
+// Owner: the received successors of the round.  A fingerprint already in the seen set loses;
+// otherwise it takes (or finds) its slot in the round's election table (OT: fingerprint, zero =
+// free, cleared before the round; OK: smallest key, all-ones before the round) and bids its key.
+__global__ __launch_bounds__(256) void k_owner_elect(const XItem *__restrict__ it, uint64_t R, Seen seen,
+                                                     ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
+                                                     uint32_t *__restrict__ rslot) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t g = lslot[i];
-        flag[i] = (g != 0xFFFFFFFFu && (uint32_t)L[g] == (uint32_t)i) ? 1u : 0u;
+        const XItem e = it[i];
+        const ulonglong2 f = make_ulonglong2(e.x, e.y);
+        if (seen_contains(seen, f)) { rslot[i] = LS_SEEN; continue; }
+        // one exit at the bottom (no break): a claimer stores its y inside the loop, in the same
+        // iteration as its CAS, before any lane of its wave waits for that y (a divergent break
+        // lets the compiler defer the claimer's store until every lane has left the loop)
+        uint64_t g = l_index(f, mask);
+        bool done = false;
+        while (!done) {
+            unsigned long long v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            bool next = false;
+            if (v == 0ull) {  // fp.x is odd (nonzero): 0 marks a free slot
+                const unsigned long long prev = atomicCAS(&OT[g].x, 0ull, f.x);
+                if (prev == 0ull) {
+                    __hip_atomic_store(&OT[g].y, f.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    done = true;
+                } else {
+                    v = prev;
+                }
+            }
+            if (!done) {
+                if (v == f.x) {
+                    const unsigned long long y = __hip_atomic_load(&OT[g].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (y == f.y) done = true;
+                    else if (y != 0ull) next = true;  // 0: the claimer's y not visible yet, this slot again
+                } else {
+                    next = true;
+                }
+            }
+            if (next) g = (g + 1) & mask;
+        }
+        atomicMin(&OK[g], e.key);
+        rslot[i] = (uint32_t)g;
     }
 }
 
-// source: flags/positions in owner-grouped order -> per successor j (TLC order within the chunk)
-__global__ __launch_bounds__(256) void k_scatter_flags(const uint32_t *__restrict__ perm,
-                                                       const uint32_t *__restrict__ sflag,
-                                                       const uint32_t *__restrict__ spos, uint64_t G,
-                                                       uint32_t *__restrict__ wflag, uint32_t *__restrict__ wpos) {
+// Owner: verdicts (1 = the fingerprint's first successor in TLC order among all shards, not seen
+// before); each winner goes into the seen set, *inserted counts them.
+__global__ __launch_bounds__(256) void k_owner_flags(const XItem *__restrict__ it, uint64_t R,
+                                                     const uint32_t *__restrict__ rslot,
+                                                     const unsigned long long *__restrict__ OK, Seen seen,
+                                                     uint32_t *__restrict__ flag, unsigned long long *inserted) {
+    uint32_t mine = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t g = rslot[i];
+        const XItem e = it[i];
+        const bool w = g != LS_SEEN && OK[g] == e.key;
+        flag[i] = w ? 1u : 0u;
+        if (w) {
+            seen_insert(seen, make_ulonglong2(e.x, e.y));
+            mine++;
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) mine += __shfl_xor(mine, d, 64);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(inserted, (unsigned long long)mine);
+}
+
+// Source: the owners' verdicts back on the successor slots (lslot = LS_WIN / LS_SEEN), and each
+// winner counted on its parent as the fused election would (wacc = winners | extra words << 12).
+__global__ __launch_bounds__(256) void k_scatter_win(const uint32_t *__restrict__ perm, const uint32_t *__restrict__ flag,
+                                                     uint64_t G, const uint4 *__restrict__ score, uint32_t sw4,
+                                                     const uint32_t *__restrict__ pnm, uint32_t maxsucc,
+                                                     uint32_t *__restrict__ lslot, uint32_t *__restrict__ wacc) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < G; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t j = perm[i];
-        wflag[j] = sflag[i];
-        wpos[j] = spos[i];
-    }
-}
-
-// owner: append received winner records (record + 4-word sidecar) to the next level (fixed
-// stride recw inside the frontier ring), parent pointers to the trace arrays
-__global__ __launch_bounds__(256) void k_accept(const uint32_t *__restrict__ xrec, uint64_t n, uint32_t recw,
-                                                uint32_t *__restrict__ ring, uint64_t rcap, uint64_t nbase,
-                                                uint64_t rel0, uint64_t *__restrict__ noff, uint64_t *__restrict__ par,
-                                                uint16_t *__restrict__ pslot, uint64_t src_tag) {
-    const uint64_t total = n * recw;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t q = i / recw, w = i - q * recw;
-        ring[ring_wrap(nbase + ring_wrap(rel0 + i, rcap), rcap)] = xrec[q * (recw + 4) + w];
-        if (w == 0) {
-            const uint32_t *side = xrec + q * (recw + 4) + recw;
-            noff[q] = rel0 + q * recw;
-            par[q] = src_tag | ((uint64_t)side[0] | ((uint64_t)side[1] << 32));
-            pslot[q] = (uint16_t)side[2];
+        const uint32_t q = perm[i];
+        const bool w = flag[i] != 0;
+        lslot[q] = w ? LS_WIN : LS_SEEN;
+        if (w) {
+            const uint32_t pl = q / maxsucc;
+            const uint32_t nadd = score[(uint64_t)q * sw4 + 1].z >> 16;
+            const uint32_t e = (nadd + (pnm[pl] & 1u) + 1u) >> 1;
+            atomicAdd(&wacc[pl], 1u + (e << 12));
         }
     }
 }
 
-__global__ __launch_bounds__(256) void k_insert_flagged(const ulonglong2 *__restrict__ fp,
-                                                        const uint32_t *__restrict__ flag, uint64_t n, Seen seen) {
+// Owner: record sizes of received winners (sidecar .w), for the offset scan
+__global__ __launch_bounds__(256) void k_side_sizes(const uint4 *__restrict__ side, uint64_t n, uint32_t *__restrict__ sz) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        if (flag[i]) seen_insert(seen, fp[i]);
+        sz[i] = side[i].w;
 }
 
-// values at a list of indices (segment boundaries of scans) -> out
-__global__ void k_pick(const uint32_t *__restrict__ a, const uint64_t *__restrict__ idx, int n,
-                       unsigned long long *__restrict__ out) {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = a[idx[i]];
+// Owner: received winners appended to the next level -- level-relative record offsets
+// (rel0 + scanned sizes) and trace entries (parent's global id, slot key)
+__global__ __launch_bounds__(256) void k_accept_side(const uint4 *__restrict__ side, const uint32_t *__restrict__ off,
+                                                     uint64_t n, uint64_t rel0, uint64_t *__restrict__ noff,
+                                                     uint64_t *__restrict__ par, uint16_t *__restrict__ pslot) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 e = side[i];
+        noff[i] = rel0 + off[i];
+        par[i] = (uint64_t)e.x | ((uint64_t)e.y << 32);
+        pslot[i] = (uint16_t)e.z;
+    }
 }
 
 __global__ void k_owner_of(const ulonglong2 *__restrict__ fp, uint32_t W, uint32_t *out) {
     if (threadIdx.x == 0) out[0] = fp_owner(fp[0], W);
 }
 
-void launch_owner_keys(const ulonglong2 *fp, uint64_t G, uint32_t W, uint32_t *key, uint32_t *iota,
-                       unsigned long long *cnt, hipStream_t s) {
-    hipLaunchKernelGGL(k_owner_keys, dim3(grid256(G)), dim3(256), 0, s, fp, G, W, key, iota, cnt);
+void launch_route_count(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
+                        uint32_t *ocnt, hipStream_t s) {
+    if (np) hipLaunchKernelGGL(k_route_count, dim3(grid256(np)), dim3(256), 0, s, fp, cnt, np, maxsucc, W, ocnt);
 }
-void launch_gather_fp(const ulonglong2 *fp, const uint32_t *perm, uint64_t G, ulonglong2 *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_gather_fp, dim3(grid256(G)), dim3(256), 0, s, fp, perm, G, out);
+void launch_route_place(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
+                        uint32_t *cursor, uint64_t g0, XItem *items, uint32_t *perm, hipStream_t s) {
+    if (np)
+        hipLaunchKernelGGL(k_route_place, dim3(grid256(np)), dim3(256), 0, s, fp, cnt, np, maxsucc, W, cursor, g0, items,
+                           perm);
 }
-void launch_recv_flags(const uint32_t *lslot, const unsigned long long *L, uint64_t R, uint32_t *flag, hipStream_t s) {
-    hipLaunchKernelGGL(k_recv_flags, dim3(grid256(R)), dim3(256), 0, s, lslot, L, R, flag);
+void launch_owner_elect(const XItem *it, uint64_t R, Seen seen, ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
+                        uint32_t *rslot, hipStream_t s) {
+    if (R) hipLaunchKernelGGL(k_owner_elect, dim3(grid256(R)), dim3(256), 0, s, it, R, seen, OT, OK, mask, rslot);
 }
-void launch_scatter_flags(const uint32_t *perm, const uint32_t *sflag, const uint32_t *spos, uint64_t G,
-                          uint32_t *wflag, uint32_t *wpos, hipStream_t s) {
-    hipLaunchKernelGGL(k_scatter_flags, dim3(grid256(G)), dim3(256), 0, s, perm, sflag, spos, G, wflag, wpos);
+void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const unsigned long long *OK, Seen seen,
+                        uint32_t *flag, unsigned long long *inserted, hipStream_t s) {
+    if (R) hipLaunchKernelGGL(k_owner_flags, dim3(grid256(R)), dim3(256), 0, s, it, R, rslot, OK, seen, flag, inserted);
 }
-void launch_accept(const uint32_t *xrec, uint64_t n, uint32_t recw, uint32_t *ring, uint64_t rcap, uint64_t nbase,
-                   uint64_t rel0, uint64_t *noff, uint64_t *par, uint16_t *pslot, uint64_t src_tag, hipStream_t s) {
-    hipLaunchKernelGGL(k_accept, dim3(grid256(n * recw)), dim3(256), 0, s, xrec, n, recw, ring, rcap, nbase, rel0, noff,
-                       par, pslot, src_tag);
+void launch_scatter_win(const uint32_t *perm, const uint32_t *flag, uint64_t G, const uint4 *score, uint32_t sw4,
+                        const uint32_t *pnm, uint32_t maxsucc, uint32_t *lslot, uint32_t *wacc, hipStream_t s) {
+    if (G)
+        hipLaunchKernelGGL(k_scatter_win, dim3(grid256(G)), dim3(256), 0, s, perm, flag, G, score, sw4, pnm, maxsucc,
+                           lslot, wacc);
 }
-void launch_insert_flagged(const ulonglong2 *fp, const uint32_t *flag, uint64_t n, Seen seen, hipStream_t s) {
-    hipLaunchKernelGGL(k_insert_flagged, dim3(grid256(n)), dim3(256), 0, s, fp, flag, n, seen);
+void launch_side_sizes(const uint4 *side, uint64_t n, uint32_t *sz, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_side_sizes, dim3(grid256(n)), dim3(256), 0, s, side, n, sz);
 }
-void launch_pick(const uint32_t *a, const uint64_t *idx, int n, unsigned long long *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_pick, dim3(1), dim3(256), 0, s, a, idx, n, out);
+void launch_accept_side(const uint4 *side, const uint32_t *off, uint64_t n, uint64_t rel0, uint64_t *noff,
+                        uint64_t *par, uint16_t *pslot, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_accept_side, dim3(grid256(n)), dim3(256), 0, s, side, off, n, rel0, noff, par, pslot);
 }
 void launch_owner_of(const ulonglong2 *fp, uint32_t W, uint32_t *out, hipStream_t s) {
     hipLaunchKernelGGL(k_owner_of, dim3(1), dim3(64), 0, s, fp, W, out);
