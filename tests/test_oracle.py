@@ -142,6 +142,35 @@ def test_shuffled_order_gives_same_counts_small():
     assert (a.distinct, a.levels) == (b.distinct, b.levels)
 
 
+ORDER_PROBE = os.path.join(GOLDEN, "order_probe.json")
+
+
+def test_order_probe_fixtures_order_insensitive(levels):
+    """SURVEY App. D.2 / VERDICT r1 item 7: the C oracle explored each configuration in TLC order (0),
+    with every level and every parent's successors reversed (1), and with a seeded shuffle of every
+    level (2) -- tests/golden/make_order_probe.py.  Identical per-level distinct and generated counts
+    (up to the violation, and its depth, for the seeded runs) say which representative of a VIEW class
+    is kept (Raft.tla:34-38) does not change what is reachable: the [TLC-ext] enumeration order and a
+    multi-GPU order could not move the counts.  Order 0 is the golden TLC-order run."""
+    probe = json.load(open(ORDER_PROBE))
+    for k in ("n3_v1_e2_r3", "n3_v2_e2_r3", "seeded_n3_v1_e2_r3", "seeded_n3_v2_e2_r3"):
+        assert k in probe, k
+    for name, rec in probe.items():
+        runs = rec["orders"]
+        assert set(runs) == {"0", "1", "2"}, name
+        assert rec["order_insensitive"], name
+        base = runs["0"]
+        for o in ("1", "2"):
+            r = runs[o]
+            assert (r["verdict"], r["depth"]) == (base["verdict"], base["depth"]), (name, o)
+            k = len(base["levels"]) if base["verdict"] == 0 else base["depth"] - 1
+            assert r["levels"][:k] == base["levels"][:k], (name, o)
+            assert r["gen_per_level"][:k - 1] == base["gen_per_level"][:k - 1], (name, o)
+        if name in levels and base["verdict"] == 0:
+            g = levels[name]
+            assert base["levels"] == g["levels"] and base["distinct"] == g["distinct"], name
+
+
 def test_no_all_commit_c_and_python_agree(corc):
     """NoAllCommit (tla:451-481) reads msgs: both restatements agree on a state that satisfies
     it and on each variant that drops or alters one of its three messages."""

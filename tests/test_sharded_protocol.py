@@ -1,6 +1,6 @@
-"""Multi-process (gloo, world_size 2) test of the sharding protocol the multi-GPU engine uses,
-restated over the oracle (tests/sharded_model.py): the owner-sharded BFS must reach exactly
-the golden per-level counts of TLC's single-worker order."""
+"""Multi-process (gloo, world_size 2 and 3) test of the sharding protocol the multi-GPU engine uses,
+restated over the oracle (tests/sharded_model.py): the block-cyclic, owner-elected BFS must reach
+exactly the golden per-level counts of TLC's single-worker order."""
 import json
 import os
 import socket
@@ -35,14 +35,15 @@ def _worker(rank, world, port, cfg_kw, chunk, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("name,chunk", [("n3_v1_e1_r3", 7), ("n2_v1_e2_r3", 50)])
-def test_two_rank_sharded_protocol_matches_golden(name, chunk):
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("name,chunk", [("n3_v1_e1_r3", 7), ("n2_v1_e2_r3", 5), ("n3_v2_e1_r3", 40)])
+def test_sharded_protocol_matches_golden(name, chunk, world):
     g = json.load(open(os.path.join(GOLDEN, "levels.json")))[name]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     kw = dict(n=g["n"], V=g["V"], max_election=g["E"], max_restart=g["R"])
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, kw, chunk, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kw, chunk, q)) for r in range(world)]
     for p in procs:
         p.start()
     levels, gen = q.get(timeout=300)

@@ -1807,7 +1807,8 @@ struct rmc_ctx {
         }
     }
 
-    static constexpr int TAB = 6;  // per-shard round row: generated, winners, words, inserted, kind + 1, key
+    // per-shard round row: generated, winners, words, inserted, error kind + 1, error key, -failure code
+    static constexpr int TAB = 7;
 
 #ifdef RMC_SHARD_DEBUG
 #define SDBG(x) do { HIPCHK(hipStreamSynchronize(stream)); std::fprintf(stderr, "sharded L%d c%llu phase %s\n", L, (unsigned long long)c, x); } while (0)
@@ -1834,6 +1835,25 @@ struct rmc_ctx {
         };
         std::vector<const void *> sp(NL);
         std::vector<void *> rp(NL);
+        // A shard that runs out of seen-set or ring room, or meets a state past msg_cap, must not
+        // leave the others waiting in a collective: it records the failure, skips its own kernels
+        // and keeps exchanging; the round's table (and a last check at the round's end) carries the
+        // failure to every rank, and all of them stop with it.
+        std::vector<int> fail(NL, 0);
+        std::string fail_msg;
+        auto guard = [&](size_t li, auto &&f) {
+            if (fail[li]) return;
+            try {
+                f();
+            } catch (const Fail &e) {
+                fail[li] = e.code;
+                fail_msg = e.msg;
+            }
+        };
+        auto agree = [&](uint64_t worst) {  // worst = max over shards of -code (0: all well)
+            if (!worst) return;
+            throw Fail(-(int)worst, fail_msg.empty() ? std::string("another shard failed (see its rank's error)") : fail_msg);
+        };
         for (uint64_t c = 0; c < rounds; c++) {
             // (1) expand the round's block: fingerprints, staged rows; successors per owner
             VV scnt(NL, std::vector<uint64_t>(W, 0)), rcnt, soff(NL), roff(NL);
@@ -1888,11 +1908,13 @@ struct rmc_ctx {
                 sp[li] = o.rflag;
                 rp[li] = o.sflag;
                 if (!R) continue;
-                grow_seen(o, o.T_count + R);
-                const uint64_t cap = owner_table(o, R);
-                timed(PH_DEDUP, [&] {
-                    launch_owner_elect(o.xr, R, o.seen(), o.OT, o.OK, cap - 1, o.rslot, stream);
-                    launch_owner_flags(o.xr, R, o.rslot, o.OK, o.seen(), o.rflag, o.sum + 9, stream);
+                guard(li, [&] {
+                    grow_seen(o, o.T_count + R);
+                    const uint64_t cap = owner_table(o, R);
+                    timed(PH_DEDUP, [&] {
+                        launch_owner_elect(o.xr, R, o.seen(), o.OT, o.OK, cap - 1, o.rslot, stream);
+                        launch_owner_flags(o.xr, R, o.rslot, o.OK, o.seen(), o.rflag, o.sum + 9, stream);
+                    });
                 });
             }
             SDBG("3");
@@ -1928,8 +1950,10 @@ struct rmc_ctx {
                 Shard &s = sh[li];
                 if (!s.np) continue;
                 grow_outbox(s, wwords[li], wnum[li]);
-                if (wwords[li] >= s.rcap) ensure_ring(s, wwords[li], 0);  // P.rcap also bounds the outbox
-                timed(PH_MAT, [&] { ks.commit(round_params(s, gbase), stream); });
+                guard(li, [&] {
+                    if (wwords[li] >= s.rcap) ensure_ring(s, wwords[li], 0);  // P.rcap also bounds the outbox
+                    timed(PH_MAT, [&] { ks.commit(round_params(s, gbase), stream); });
+                });
             }
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
@@ -1938,9 +1962,12 @@ struct rmc_ctx {
                 HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
                 HIPCHK(hipGetLastError());
-                if (s.hsum[2 + ERR_NSLOTS])
-                    throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
+                if (s.hsum[2 + ERR_NSLOTS] && !fail[li]) {
+                    fail[li] = RMC_E_CAPACITY;
+                    fail_msg = "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages";
+                }
                 uint64_t *row = &tab[TAB * s.id];
+                row[6] = (uint64_t)(-fail[li]);
                 row[1] = wnum[li];
                 row[2] = wwords[li];
                 row[3] = ins[li];
@@ -1954,7 +1981,13 @@ struct rmc_ctx {
             }
             collect_times(st);
             SDBG("7");
+            for (size_t li = 0; li < NL; li++) tab[TAB * sh[li].id + 6] = (uint64_t)(-fail[li]);
             allreduce(tab.data(), TAB * W, false);  // rows: each shard's own, zero elsewhere
+            {
+                uint64_t worst = 0;
+                for (int t = 0; t < W; t++) worst = std::max(worst, tab[TAB * t + 6]);
+                agree(worst);
+            }
             // (6) the first error of the round in the level's order
             int ek_shard = -1;
             for (int t = 0; t < W; t++)
@@ -2051,7 +2084,8 @@ struct rmc_ctx {
                     const uint64_t done = std::min(o.cur_n, (c + 1) * B);
                     consumed = done < o.cur_n ? d2h(o.cur_off + done) : o.cur_words;
                 }
-                ensure_ring(o, words, consumed);
+                guard(li, [&] { ensure_ring(o, words, consumed); });
+                if (fail[li]) continue;
                 ensure_off(o.nxt_off, o.nxt_off_cap, o.nxt_n, o.nxt_n + n);
                 const uint64_t gid = o.level_start[L - 1] + o.cur_n + o.nxt_n;  // local gid of the first
                 grow_trace(o, n);
@@ -2070,6 +2104,12 @@ struct rmc_ctx {
                 o.nxt_words += words;
             }
             SDBG("11");
+            {
+                uint64_t worst = 0;
+                for (size_t li = 0; li < NL; li++) worst = std::max(worst, (uint64_t)(-fail[li]));
+                allreduce(&worst, 1, true);
+                agree(worst);
+            }
             for (int t = 0; t < W; t++) {
                 level_gen += tab[TAB * t + 0];
                 level_new += tab[TAB * t + 1];
