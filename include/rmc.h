@@ -56,6 +56,9 @@ extern "C" {
 /* ---- spec variants ------------------------------------------------------------ */
 #define RMC_SPEC_RAFT 0    /* Raft.tla as shipped */
 #define RMC_SPEC_SEEDED 1  /* RaftSeeded: Median's threshold (Raft.tla:72) is Cardinality(Servers) */
+#define RMC_SPEC_BECOME_FOLLOWER 2  /* Raft.tla with Next's `\/ BecomeFollower(s)` uncommented (Raft.tla:420):
+                                       FollowerUpdateTerm / CandidateToFollower / LeaderToFollower
+                                       (Raft.tla:190-229) right after UpdateTerm; trace action id 12 */
 
 /* Model configuration: what Raft.cfg's CONSTANTS (Raft.cfg:1-21), INVARIANT
  * (Raft.cfg:33-34) and TLC's -deadlock flag (myrun.sh:3) bind.  VIEW view

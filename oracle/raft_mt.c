@@ -118,7 +118,9 @@ static void *phase_expand(void *arg) {
         ar_get(w->cur, i, ps);
         uint64_t rank = 0;
         for (int s = 0; s < c->n; s++)
-            for (int a = 0; a < N_ACTIONS; a++) {
+            for (int ai = 0; ai < N_ORDER; ai++) {
+                const int a = ACT_ORDER[ai];
+                if (a == A_BF && !c->bf) continue;
                 b.n = 0;
                 b.assert_fail = 0;
                 gen_action(c, ps, s, a, &b);
@@ -183,7 +185,7 @@ static void run_phase(worker_t *W, int T, void *(*fn)(void *)) {
 int orc_mt_run(int n, int V, int E, int R, int threads, uint64_t *distinct, uint64_t *generated, int *depth) {
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
-    ocfg_t c = {n, V, E, R, 0, 0, 1u << I_LHACE, 0, 0, 0};
+    ocfg_t c = {n, V, E, R, 0, 0, 1u << I_LHACE, 0, 0, 0, 0};
     perms_t *P = (perms_t *)malloc(sizeof(perms_t));
     make_perms(n, P);
     uint64_t seen_cap = 1u << 20;

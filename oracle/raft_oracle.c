@@ -50,6 +50,11 @@
 enum { R_F = 0, R_C = 1, R_L = 2 };
 enum { MT_VREQ = 0, MT_VRESP = 1, MT_AREQ = 2, MT_ARESP = 3 };
 enum { A_BC, A_UT, A_RV, A_BL, A_CR, A_LAE, A_FAE, A_FRE, A_HAR, A_LCC, A_RS, N_ACTIONS };
+/* BecomeFollower (tla:190-231): in Next only in the tla:420 variant, right after UpdateTerm */
+#define A_BF 12
+/* Next's disjuncts in TLC's enumeration order (tla:416-430) */
+static const int ACT_ORDER[] = {A_BC, A_UT, A_BF, A_RV, A_BL, A_CR, A_LAE, A_FAE, A_FRE, A_HAR, A_LCC, A_RS};
+#define N_ORDER 12
 enum { V_OK = 0, V_INVARIANT = 1, V_ASSERT = 2, V_EVAL_ERROR = 3, V_DEADLOCK = 4, V_LIMIT = 5, V_CAPACITY = 6 };
 
 /* invariant ids (bit positions of ocfg_t.inv_mask) */
@@ -64,7 +69,10 @@ typedef struct {
     int record_trace;
     int order;          /* 0 = TLC -workers 1 order; 1 = reversed; 2 = seeded shuffle (order-sensitivity probe) */
     uint64_t seed;
+    int bf;             /* the BecomeFollower variant (tla:420 uncommented) */
 } ocfg_t;
+/* spec flags of the C API's `seeded` argument: bit 0 RaftSeeded, bit 1 BecomeFollower variant */
+static void set_variant(ocfg_t *c, int flags) { c->seeded = flags & 1; c->bf = (flags >> 1) & 1; }
 
 typedef struct {
     int8_t vf[MAXN], ct[MAXN], role[MAXN], ci[MAXN], ll[MAXN];
@@ -224,6 +232,27 @@ static void gen_action(const ocfg_t *c, const st_t *st, int s, int a, batch_t *b
                     st_t *t = emit(b, w); copy_state(t, st);
                     t->role[s] = R_F;
                 }
+            }
+        }
+        return;
+    case A_BF: /* BecomeFollower tla:190-231 = FollowerUpdateTerm \/ CandidateToFollower \/
+                  LeaderToFollower: role[s] enables exactly one, each over msgs in order */
+        for (int w = 0; w < st->nm; w++) {
+            msg_t m; k_decode(st->m[w], &m);
+            if (m.dst != s) continue;
+            if (st->role[s] == R_F) {        /* FollowerUpdateTerm tla:191-197: votedFor kept */
+                if (m.term > st->ct[s]) { st_t *t = emit(b, w); copy_state(t, st); t->ct[s] = m.term; }
+            } else if (st->role[s] == R_C) { /* CandidateToFollower tla:200-212 */
+                if (m.term > st->ct[s]) {
+                    st_t *t = emit(b, w); copy_state(t, st);
+                    t->ct[s] = m.term; t->role[s] = R_F; t->vf[s] = -1;
+                } else if (m.term == st->ct[s] && m.type == MT_AREQ) {
+                    st_t *t = emit(b, w); copy_state(t, st);
+                    t->role[s] = R_F;
+                }
+            } else if (m.term > st->ct[s]) { /* LeaderToFollower tla:215-223 */
+                st_t *t = emit(b, w); copy_state(t, st);
+                t->ct[s] = m.term; t->role[s] = R_F; t->vf[s] = -1;
             }
         }
         return;
@@ -678,7 +707,8 @@ static void rec_state(orc_t *O, uint64_t id, uint64_t parent, uint32_t key, cons
 void *orc_create(int n, int V, int E, int R, int seeded, int check_deadlock, uint32_t inv_mask, int record_trace) {
     if (n < 1 || n > MAXN || V < 0 || V > MAXV || E < 0 || E > 7 || R < 0) return NULL;
     orc_t *O = (orc_t *)calloc(1, sizeof(orc_t));
-    O->c.n = n; O->c.V = V; O->c.E = E; O->c.R = R; O->c.seeded = seeded;
+    O->c.n = n; O->c.V = V; O->c.E = E; O->c.R = R;
+    set_variant(&O->c, seeded);
     O->c.check_deadlock = check_deadlock; O->c.inv_mask = inv_mask; O->c.record_trace = record_trace;
     make_perms(n, &O->P);
     return O;
@@ -752,7 +782,9 @@ int orc_run(void *h, uint64_t max_states) {
             if (ps->nm > O->max_nm) O->max_nm = ps->nm;
             int nsucc = 0;
             for (int s = 0; s < c->n; s++) {
-                for (int a = 0; a < N_ACTIONS; a++) {
+                for (int ai = 0; ai < N_ORDER; ai++) {
+                    const int a = ACT_ORDER[ai];
+                    if (a == A_BF && !c->bf) continue;
                     b.n = 0; b.assert_fail = 0;
                     gen_action(c, ps, s, a, &b);
                     if (g_overflow) { O->verdict = V_CAPACITY; goto done; }
@@ -844,13 +876,16 @@ int orc_trace_state(void *h, int idx, int32_t *out, int cap_ints, uint32_t *key)
 /* successors of an unpacked state in TLC order; returns count, -1 on Assert, -2 on capacity */
 int orc_successors(int n, int V, int E, int R, int seeded, const int32_t *in, int32_t *out, int stride_ints,
                    int cap_states, uint32_t *keys) {
-    ocfg_t c = {n, V, E, R, seeded, 0, 1, 0, 0, 0};
+    ocfg_t c = {n, V, E, R, 0, 0, 1, 0, 0, 0, 0};
+    set_variant(&c, seeded);
     st_t *st = (st_t *)malloc(sizeof(st_t));
     batch_t b; b.buf = (st_t *)malloc(sizeof(st_t) * BATCH_CAP); b.w = (int32_t *)malloc(sizeof(int32_t) * BATCH_CAP); b.cap = BATCH_CAP;
     int cnt = 0, ret = 0;
     if (pack_from(&c, in, st) < 0) { ret = -2; goto out; }
     for (int s = 0; s < n && ret == 0; s++)
-        for (int a = 0; a < N_ACTIONS; a++) {
+        for (int ai = 0; ai < N_ORDER; ai++) {
+            const int a = ACT_ORDER[ai];
+            if (a == A_BF && !c.bf) continue;
             b.n = 0; b.assert_fail = 0;
             gen_action(&c, st, s, a, &b);
             if (b.assert_fail) { ret = -1; break; }
@@ -868,7 +903,7 @@ out:
 }
 
 int orc_canon_hash(int n, int V, const int32_t *in, uint64_t *out2) {
-    ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0, 0, 0};
+    ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0, 0, 0, 0};
     perms_t *P = (perms_t *)malloc(sizeof(perms_t));
     make_perms(n, P);
     st_t *st = (st_t *)malloc(sizeof(st_t));
@@ -879,7 +914,7 @@ int orc_canon_hash(int n, int V, const int32_t *in, uint64_t *out2) {
 }
 
 int orc_inv(int n, int V, const int32_t *in, int inv_id) {
-    ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0, 0, 0};
+    ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0, 0, 0, 0};
     st_t *st = (st_t *)malloc(sizeof(st_t));
     int r = pack_from(&c, in, st);
     if (r >= 0) r = inv_eval(&c, st, inv_id);
@@ -900,7 +935,8 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "-V")) V = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-E")) E = atoi(argv[++i]);
         else if (!strcmp(argv[i], "-R")) R = atoi(argv[++i]);
-        else if (!strcmp(argv[i], "-seeded")) seeded = 1;
+        else if (!strcmp(argv[i], "-seeded")) seeded |= 1;
+        else if (!strcmp(argv[i], "-bf")) seeded |= 2;
         else if (!strcmp(argv[i], "-inv")) mask = (uint32_t)strtoul(argv[++i], 0, 0);
     }
     void *h = orc_create(n, V, E, R, seeded, 0, mask, trace);

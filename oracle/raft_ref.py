@@ -69,9 +69,12 @@ ACTIONS = (
     "HandleAppendResp",     # tla:374
     "LeaderCanCommit",      # tla:398
     "Restart",              # tla:409
+    "FollowerAppendEntry",  # tla:323 (A_FAPP, the tla:425 variant)
+    "BecomeFollower",       # tla:226 (A_BF, the tla:420 variant)
 )
 A_BC, A_UT, A_RV, A_BL, A_CR, A_LAE, A_FAE, A_FRE, A_HAR, A_LCC, A_RS = range(11)
 A_FAPP = 11  # FollowerAppendEntry (tla:323), in Next only in the tla:425 variant
+A_BF = 12    # BecomeFollower (tla:226), in Next only in the tla:420 variant (right after UpdateTerm)
 
 INVARIANTS = ("Inv", "LeaderHasAllCommittedEntries", "NoSplitVote", "RaftCanCommt",
               "FollowerCanCommit", "CommitAll", "NoAllCommit", "ExistLeaderAndCandidate")
@@ -178,6 +181,7 @@ class Config:
     check_deadlock: bool = False             # myrun.sh passes -deadlock (run:3)
     seeded: bool = False       # RaftSeeded: Median threshold Cardinality(Servers)
     follower_append_entry: bool = False  # variant: tla:425's `\/ FollowerAppendEntry(s)` uncommented
+    become_follower: bool = False  # variant: tla:420's `\/ BecomeFollower(s)` uncommented
     symmetry: bool = True      # SYMMETRY symmServers (cfg:24)
     view: bool = True          # VIEW view (cfg:26)
 
@@ -283,6 +287,34 @@ def update_term(cfg, st: State, s, msgs_sorted):
                     role=_set(st.role, s, FOLLOWER),
                     electionCount=st.electionCount, restartCount=st.restartCount,
                     pendingResponse=st.pendingResponse, valSent=st.valSent)
+
+
+def become_follower(cfg, st: State, s, msgs_sorted):
+    r"""BecomeFollower(s) (tla:226-229) = FollowerUpdateTerm(s) (tla:191-197) \/ CandidateToFollower(s)
+    (tla:200-212) \/ LeaderToFollower(s) (tla:215-223).  role[s] enables exactly one of the three,
+    each an \E m \in msgs; no Assert here (the candidate's AppendReq case just steps down)."""
+    r, ct = st.role[s], st.currentTerm[s]
+
+    def succ(term, role, voted):
+        return State(votedFor=_set(st.votedFor, s, voted), currentTerm=_set(st.currentTerm, s, term),
+                     logs=st.logs, matchIndex=st.matchIndex, nextIndex=st.nextIndex,
+                     commitIndex=st.commitIndex, msgs=st.msgs, role=_set(st.role, s, role),
+                     electionCount=st.electionCount, restartCount=st.restartCount,
+                     pendingResponse=st.pendingResponse, valSent=st.valSent)
+    for w, m in enumerate(msgs_sorted):
+        if mdst(m) != s:
+            continue
+        mt = mterm(m)
+        if r == FOLLOWER:
+            if mt > ct:  # FollowerUpdateTerm: votedFor and role unchanged
+                yield w, succ(mt, FOLLOWER, st.votedFor[s])
+        elif r == CANDIDATE:
+            if mt > ct:
+                yield w, succ(mt, FOLLOWER, NONE)
+            elif mt == ct and mtype(m) == "AppendReq":
+                yield w, succ(ct, FOLLOWER, st.votedFor[s])
+        elif mt > ct:  # LeaderToFollower
+            yield w, succ(mt, FOLLOWER, NONE)
 
 
 def response_vote(cfg, st: State, s, msgs_sorted):
@@ -555,6 +587,8 @@ def successor_batches(cfg: Config, st: State):
         gens = (
             (A_BC, lambda: become_candidate(cfg, st, s)),
             (A_UT, lambda: update_term(cfg, st, s, msgs_sorted)),
+            # variant only (tla:420)
+            (A_BF, lambda: become_follower(cfg, st, s, msgs_sorted)),
             (A_RV, lambda: response_vote(cfg, st, s, msgs_sorted)),
             (A_BL, lambda: become_leader(cfg, st, s)),
             (A_CR, lambda: client_req(cfg, st, s)),
@@ -568,7 +602,7 @@ def successor_batches(cfg: Config, st: State):
             (A_RS, lambda: restart(cfg, st, s)),
         )
         for a, mk in gens:
-            if a == A_FAPP and not cfg.follower_append_entry:
+            if (a == A_FAPP and not cfg.follower_append_entry) or (a == A_BF and not cfg.become_follower):
                 continue
             yield s, a, list(mk())
 

@@ -26,6 +26,10 @@ LEVELS_BIG = load("levels_big.json") if os.path.exists(os.path.join(GOLDEN, "lev
 PREFIX = load("levels_prefix.json") if os.path.exists(os.path.join(GOLDEN, "levels_prefix.json")) else {}
 SAMPLES = load("successors.json")
 TRACES = load("traces.json")
+# the BecomeFollower variant (Raft.tla:420 uncommented; tests/golden/make_golden_bf.py)
+LEVELS_BF = load("levels_bf.json")
+SAMPLES_BF = load("successors_bf.json")
+TRACES_BF = load("traces_bf.json")
 
 _cache = {}
 
@@ -156,11 +160,17 @@ def test_eval_error_state():
     assert mc.eval_invariant(s, "Inv") is None
 
 
+def spec_of(g):
+    if g.get("become_follower"):
+        return raftmc.SPEC_BECOME_FOLLOWER
+    return raftmc.SPEC_SEEDED if g["seeded"] else raftmc.SPEC_RAFT
+
+
 def run_cfg(g, **kw):
     mc = raftmc.ModelChecker(raftmc.ModelConfig(
         n_servers=g["n"], n_vals=g["V"], max_election=g["E"], max_restart=g["R"],
         invariants=tuple(g["invariants"]), check_deadlock=g["check_deadlock"],
-        spec_variant=raftmc.SPEC_SEEDED if g["seeded"] else raftmc.SPEC_RAFT, **kw))
+        spec_variant=spec_of(g), **kw))
     res = mc.run()
     return mc, res
 
@@ -518,3 +528,41 @@ def test_launcher_prints_tlc_counterexample(tmp_path):
         assert [l.replace(",  [", ", [") for l in blk[1:]] == want, (k, blk[1:], want)
     assert f"{g['generated']} states generated, {g['distinct']} distinct states found, " \
            f"{g['queue_left']} states left on queue." in out
+
+
+# ---- the BecomeFollower variant (Raft.tla:190-231, 420) ---------------------
+# Next with `\/ BecomeFollower(s)` uncommented: FollowerUpdateTerm / CandidateToFollower /
+# LeaderToFollower right after UpdateTerm, a second candidate per message lane (k_expand<..., BFV>).
+@pytest.mark.parametrize("name", sorted(SAMPLES_BF))
+def test_become_follower_successors_match_oracle(name):
+    g = SAMPLES_BF[name]
+    mc = checker(g["n"], g["V"], g["E"], g["R"], spec_variant=raftmc.SPEC_BECOME_FOLLOWER)
+    n_bf = 0
+    for it in g["items"]:
+        got = mc.successors(it["state"])
+        exp = it["successors"]
+        assert [list(k) for k, _, _ in got] == [e["key"] for e in exp]
+        for (k, st, _), e in zip(got, exp):
+            assert st == e["state"], (k, it["state"])
+        n_bf += sum(1 for e in exp if e["key"][1] == R.A_BF)
+    assert n_bf > 0  # the samples reach BecomeFollower steps
+
+
+@pytest.mark.parametrize("name", sorted(LEVELS_BF))
+def test_become_follower_bfs_matches_golden_levels(name):
+    g = LEVELS_BF[name]
+    mc, res = run_cfg(g)
+    check_levels(g, res)
+    if name in TRACES_BF:
+        tr = mc.trace()
+        assert [(list(k) if k else None, st) for k, st in tr] == [(e["key"], e["state"]) for e in TRACES_BF[name]["steps"]]
+    mc.close()
+
+
+@pytest.mark.parametrize("shards", [2, 4])
+def test_become_follower_sharded_identical(shards):
+    g = LEVELS_BF["bf_n3_v1_e2_r3"]
+    mc, res = run_cfg(g, virtual_shards=shards, chunk_successors=6000, shard_min_states=1)
+    check_levels(g, res)
+    mc.close()
+

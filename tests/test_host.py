@@ -150,3 +150,18 @@ def test_launcher_reports_cfg_errors(tmp_path):
     r = subprocess.run([LAUNCHER, "-deadlock", "-workers", "4", "-config", str(tmp_path / "Raft.cfg"),
                         str(tmp_path / "Raft.tla")], capture_output=True, text=True, env=env)
     assert r.returncode == 151 and "VIEW" in r.stdout
+
+
+def test_become_follower_variant_spec_recognised():
+    """tools/make_variant_spec.py --become-follower on Raft.tla (skipped where the reference is absent, as on
+    the GPU box): the launcher's parser maps the text to RMC_SPEC_BECOME_FOLLOWER."""
+    src = "/root/reference/Raft.tla"
+    if not os.path.exists(src):
+        pytest.skip("reference Raft.tla not present")
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    text = subprocess.check_output([sys.executable, os.path.join(root, "tools", "make_variant_spec.py"),
+                                    "--become-follower", src]).decode()
+    cfg = raftmc.parse_config(open("/root/reference/Raft.cfg").read(), tla_text=text)
+    assert cfg.spec_variant == raftmc.SPEC_BECOME_FOLLOWER

@@ -22,6 +22,9 @@ static const uint64_t FNV_RAFT_SEEDED = 0xc2b84ca613379636ULL;  // tools/make_se
 // msgs after its own SendMsg; oracle/raft_ref.py:follower_append_entry), so this text runs the
 // Raft.tla model unchanged.
 static const uint64_t FNV_RAFT_FAPP = 0x1319b28a1b001651ULL;
+// Raft.tla with Next's `\/ BecomeFollower(s)` uncommented (tla:420; tools/make_variant_spec.py
+// --become-follower): RMC_SPEC_BECOME_FOLLOWER.
+static const uint64_t FNV_RAFT_BF = 0xc3850410336560ebULL;
 
 uint64_t fnv1a_spec(const std::string &text) {
     uint64_t h = 0xcbf29ce484222325ULL;
@@ -268,6 +271,7 @@ bool parse_model(const std::string &cfg_text, const char *tla_text, ParsedModel 
         const uint64_t h = fnv1a_spec(tla_text);
         if (h == FNV_RAFT || h == FNV_RAFT_FAPP) { pm->cfg.spec_variant = RMC_SPEC_RAFT; pm->module = "Raft"; }
         else if (h == FNV_RAFT_SEEDED) { pm->cfg.spec_variant = RMC_SPEC_SEEDED; pm->module = "RaftSeeded"; }
+        else if (h == FNV_RAFT_BF) { pm->cfg.spec_variant = RMC_SPEC_BECOME_FOLLOWER; pm->module = "Raft"; }
         else {
             char buf[64];
             snprintf(buf, sizeof buf, "%016llx", (unsigned long long)h);

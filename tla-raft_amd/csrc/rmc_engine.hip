@@ -621,7 +621,9 @@ struct rmc_ctx {
         N = cfg.n_servers;
         V = cfg.n_vals;
         int cap = cfg.msg_cap ? cfg.msg_cap : (N <= 3 ? 64 : 128);
-        if (!get_kernels(N, V, cap, &ks))
+        if (cfg.spec_variant < RMC_SPEC_RAFT || cfg.spec_variant > RMC_SPEC_BECOME_FOLLOWER)
+            throw Fail(RMC_E_ARG, "unknown spec_variant " + std::to_string(cfg.spec_variant));
+        if (!get_kernels(N, V, cap, cfg.spec_variant == RMC_SPEC_BECOME_FOLLOWER, &ks))
             throw Fail(RMC_E_ARG, "no compiled kernels for n_servers=" + std::to_string(N) + " n_vals=" +
                                       std::to_string(V) + " msg_cap=" + std::to_string(cap));
         RECW = ks.RECW_MAX;
@@ -676,7 +678,7 @@ struct rmc_ctx {
         d_seeds = dmalloc<uint64_t>(seeds.size());
         HIPCHK(hipMemcpy(d_seeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
         // fingerprint scheme identity (checkpoints): seeds, message hashes, record codec, slot hash
-        scheme_hash = 0x5eed5c4e3e000004ull;  // 4: signature-coset minimum for n >= 4
+        scheme_hash = 0x5eed5c4e3e000005ull;  // 4: signature-coset minimum for n >= 4; 5: positional slot keys
         auto mixin = [&](uint64_t v) { scheme_hash = mix64(scheme_hash ^ (v + 0x9e3779b97f4a7c15ull)); };
         for (uint64_t s : seeds) mixin(s);
         for (const ulonglong2 &g : U.gmsg) { mixin(g.x); mixin(g.y); }

@@ -145,8 +145,9 @@ struct KernelSet {
     void (*decode)(const uint32_t *packed, uint32_t *nibble_core);
 };
 
-// returns false if (N, V) has no compiled instantiation
-bool get_kernels(int N, int V, int msg_cap, KernelSet *ks);
+// returns false if (N, V) has no compiled instantiation; become_follower: the tla:420 variant's kernels
+// (BecomeFollower candidates, maxsucc larger by msg_cap)
+bool get_kernels(int N, int V, int msg_cap, bool become_follower, KernelSet *ks);
 
 // generic (template-free) kernels
 constexpr uint32_t LS_SEEN = 0xFFFFFFFFu, LS_ELECT = 0xFFFFFFFEu, LS_WIN = 0xFFFFFFFDu;

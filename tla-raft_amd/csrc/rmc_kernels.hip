@@ -538,15 +538,24 @@ struct Wave {
 };
 
 // Evaluate the message lane (round r) -> at most one successor.
-template <int N, int V, int MR>
+// BFV (the tla:420 variant): ob gets the lane's BecomeFollower successor (tla:190-229) -- a second
+// candidate per message; with BFV false ob is not touched.
+template <int N, int V, int MR, bool BFV = false>
 __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> &W, const uint16_t *ids, int r, int lane,
-                         Succ<N, V, MR> &o, uint32_t &assert_key, uint32_t *ainf) {
+                         Succ<N, V, MR> &o, Succ<N, V, MR> &ob, uint32_t &assert_key, uint32_t *ainf) {
     using Lo = Layout<N, V>;
     o.key = KEY_NONE;
     o.nadd = 0;
     o.s = 0;
 #pragma unroll
     for (int a = 0; a < Spec<N, V, MR>::NADD; a++) o.add[a] = 0;
+    if (BFV) {
+        ob.key = KEY_NONE;
+        ob.nadd = 0;
+        ob.s = 0;
+#pragma unroll
+        for (int a = 0; a < Spec<N, V, MR>::NADD; a++) ob.add[a] = 0;
+    }
     const uint32_t k = (uint32_t)(r * 64 + lane);
     if (k >= W.nm) return;
     const uint32_t m = W.inf[r];
@@ -558,6 +567,25 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
     o.lw = W.lds[Lo::W_LOG + s];
     o.mirow = W.lds[Lo::W_MI + s];
     o.nirow = W.lds[Lo::W_NI + s];
+    if (BFV) {
+        // FollowerUpdateTerm (tla:191-197: votedFor, role kept), CandidateToFollower (tla:200-212),
+        // LeaderToFollower (tla:215-223): role[s] picks one; msgs unchanged
+        const bool up = mt > ct, step = mt == ct && typ == AREQ && role == CAN;
+        if (up || step) {
+#pragma unroll
+            for (int w = 0; w < Lo::NW; w++) ob.c[w] = W.c[w];
+            ob.s = s;
+            ob.lw = o.lw;
+            ob.mirow = o.mirow;
+            ob.nirow = o.nirow;
+            if (up) ob.c[Lo::W_CT] = setnib(ob.c[Lo::W_CT], s, mt);
+            if (role != FOL) {
+                ob.c[Lo::W_ROLE] = setnib(ob.c[Lo::W_ROLE], s, FOL);
+                if (up) ob.c[Lo::W_VF] = setnib(ob.c[Lo::W_VF], s, VF_NONE);
+            }
+            ob.key = slot_key(s, BF, k);
+        }
+    }
     if (mt > ct) {  // UpdateTerm, first disjunct (tla:178-182)
         o.c[Lo::W_ROLE] = setnib(o.c[Lo::W_ROLE], s, FOL);
         o.c[Lo::W_CT] = setnib(o.c[Lo::W_CT], s, mt);
@@ -1069,18 +1097,22 @@ __device__ __forceinline__ void unstage_core(const uint32_t *pc, const uint4 a, 
     c[Lo::W_MISC] = b.y;
 }
 
-template <int N, int V, int MR, int MODE>
-__global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void k_expand(KParams P) {
+// BFV: the BecomeFollower variant (tla:420) -- MR more candidates (one per message lane) and MR * 64
+// more successor slots per parent (MX)
+template <int N, int V, int MR, int MODE, bool BFV = false>
+__global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? 4 : ((BFV && N >= 4) ? 1 : RMC_WIDE_WAVES)) void k_expand(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
     constexpr bool SUMS = true;
+    constexpr int MX = S::MAXS + (BFV ? S::MCAP : 0);   // successor slots per parent
+    constexpr int NC = MR + 1 + (BFV ? MR : 0);         // candidates per lane: messages, slot, BecomeFollower
     __shared__ uint16_t ids[S::MCAP];
     __shared__ ulonglong2 sPart[SUMS ? 64 : 1];         // partial minima per (successor, permutation block)
     __shared__ uint64_t M0[N * N], M1[N * N];
     __shared__ uint32_t pcore[Lo::NW + N];
     constexpr bool SIG = SUMS && N >= 4;                // signature pre-sort (coset minimum)
     constexpr int NPM = (SUMS && !SIG) ? factorial(N) : 1;  // |Permutations(Servers)| (tla:21)
-    constexpr int MAXS = SUMS ? S::MCAP + N * S::SLOTS_PER_SERVER : 1;
+    constexpr int MAXS = SUMS ? MX : 1;
     constexpr int MAXG = SIG ? MAXS : 1;
     __shared__ uint64_t Rt[2][NPM * N], Tt[2][NPM];     // parent row terms / totals per permutation
     __shared__ uint64_t sdS[2][N], sdP[2][N * N];       // position seeds
@@ -1115,31 +1147,32 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void 
         Wave<N, V, MR> W;
         load_parent<N, V, MR, SUMS>(P, rec_start<S::RECW_MAX>(P, p), lane, W, ids, M0, M1, pcore);
         PHASE(0);
-        Succ<N, V, MR> cand[MR + 1];
+        Succ<N, V, MR> cand[NC];
         uint32_t akey = KEY_NONE;
 #pragma unroll
         for (int r = 0; r < MR; r++)
-            eval_msg<N, V, MR>(P, W, ids, r, lane, cand[r], akey, &sAinf[(r * 64 + lane) * S::NADD]);
+            eval_msg<N, V, MR, BFV>(P, W, ids, r, lane, cand[r], cand[BFV ? MR + 1 + r : r], akey,
+                                    &sAinf[(r * 64 + lane) * S::NADD]);
         eval_slot<N, V, MR>(P, W, ids, lane, cand[MR], &sAinf[(MR * 64 + lane) * S::NADD]);
         PHASE(1);
         // rank of every enabled successor in TLC order
-        uint64_t en[MR + 1];
+        uint64_t en[NC];
         uint32_t total = 0;
 #pragma unroll
-        for (int r = 0; r <= MR; r++) {
+        for (int r = 0; r < NC; r++) {
             en[r] = __ballot(cand[r].key != KEY_NONE);
             total += (uint32_t)__popcll(en[r]);
         }
-        uint32_t rank[MR + 1];
+        uint32_t rank[NC];
 #pragma unroll
-        for (int r = 0; r <= MR; r++) rank[r] = 0;
+        for (int r = 0; r < NC; r++) rank[r] = 0;
 #pragma unroll
-        for (int q = 0; q <= MR; q++) {
+        for (int q = 0; q < NC; q++) {
             for (uint64_t m = en[q]; m; m &= m - 1) {
                 const int t = __ffsll((unsigned long long)m) - 1;
                 const uint32_t kt = rdlane(cand[q].key, t);
 #pragma unroll
-                for (int r = 0; r <= MR; r++) rank[r] += kt < cand[r].key ? 1u : 0u;
+                for (int r = 0; r < NC; r++) rank[r] += kt < cand[r].key ? 1u : 0u;
             }
         }
         const uint64_t pl = p - P.p_begin;  // chunk-local parent index
@@ -1147,7 +1180,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void 
         {
             bool ovf = false;
 #pragma unroll
-            for (int r = 0; r <= MR; r++) ovf |= cand[r].key != KEY_NONE && W.nm + cand[r].nadd > (uint32_t)S::MCAP;
+            for (int r = 0; r < NC; r++) ovf |= cand[r].key != KEY_NONE && W.nm + cand[r].nadd > (uint32_t)S::MCAP;
             if (__ballot(ovf) && lane == 0) atomicOr(&P.flags[0], 1u);
             am = __ballot(akey != KEY_NONE);
             if (am) {
@@ -1171,9 +1204,9 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void 
             // stage every enabled successor at its slot q: the acting row and the added message ids
             // -- commit rebuilds the state from the parent's core and merges the ids
 #pragma unroll
-            for (int r = 0; r <= MR; r++) {
+            for (int r = 0; r < NC; r++) {
                 if (cand[r].key == KEY_NONE) continue;
-                const uint64_t q = pl * (uint64_t)S::MAXS + rank[r];
+                const uint64_t q = pl * (uint64_t)MX + rank[r];
                 stage_succ<N, V, MR>(cand[r], W.nm, P.score + q * (uint64_t)S::SW4);
             }
         }
@@ -1227,12 +1260,13 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void 
             }
             // (b) every enabled successor writes its acting row to LDS slot rank
 #pragma unroll
-            for (int r = 0; r <= MR; r++) {
+            for (int r = 0; r < NC; r++) {
                 if (cand[r].key == KEY_NONE) continue;
                 const Succ<N, V, MR> &o = cand[r];
                 const uint32_t sl = rank[r];
                 uint64_t row0[N], row1[N];
-                succ_row<N, V, MR>(o, M0, M1, &sAinf[(r * 64 + lane) * S::NADD], row0, row1);
+                // BecomeFollower candidates (r > MR) add no messages: their info words are never read
+                succ_row<N, V, MR>(o, M0, M1, &sAinf[((r <= MR ? r : 0) * 64 + lane) * S::NADD], row0, row1);
                 const uint32_t vfs = nib(o.c[Lo::W_VF], o.s);
                 const uint64_t u = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI],
                                                o.c[Lo::W_LL], o.lw, o.mirow, o.nirow, o.s);
@@ -1266,7 +1300,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void 
                 const ulonglong2 f = make_ulonglong2(best.x | 1ull, best.y);
                 if (MODE == M_FUSED) {
                     // the seen set is read-only in this launch (commit inserts)
-                    const uint64_t q = pl * (uint64_t)S::MAXS + lo;
+                    const uint64_t q = pl * (uint64_t)MX + lo;
                     P.fp[q] = f;
                     if (P.route) return;  // sharded round: the fingerprint's owner probes and elects
                     // the election slot's first word goes out with the seen-set probe: one
@@ -1277,7 +1311,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void 
                     const uint32_t e = ((uint32_t)sNa[lo] + (W.nm & 1u) + 1u) >> 1;
                     P.lslot[q] = seen_contains(P.seen, f)
                                      ? LS_SEEN
-                                     : elect_slot<S::MAXS>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g0, v0);
+                                     : elect_slot<MX>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g0, v0);
                 } else {
                     P.fp[lo] = f;
                 }
@@ -1401,7 +1435,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? 4 : RMC_WIDE_WAVES) void 
         if (MODE == M_FUSED) continue;
         // SINGLE: every successor, in TLC order
 #pragma unroll
-        for (int r = 0; r <= MR; r++) {
+        for (int r = 0; r < NC; r++) {
             const bool win = cand[r].key != KEY_NONE;
             const uint64_t out = rank[r];
             if (win) P.out_keys[out] = cand[r].key;
@@ -1635,10 +1669,11 @@ __device__ __forceinline__ bool last_commit_block(uint32_t *tick, uint32_t nb) {
 // its staged row, check the INVARIANTs (Raft.cfg:33) on it, append it to the next level (record
 // at the scanned word offset, its offset in noff), insert its fingerprint, record its parent
 // pointer and slot key.
-template <int N, int V, int MR>
+template <int N, int V, int MR, bool BFV = false>
 __global__ __launch_bounds__(64) void k_commit(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
+    constexpr int MX = S::MAXS + (BFV ? S::MCAP : 0);  // successor slots per parent (k_expand)
     if (!level_args(P)) return;
     const int lane = threadIdx.x;
     const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -1650,7 +1685,7 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
         const uint32_t wc = P.wcnt[pl];
         const uint32_t bo = P.boff[pl / WTILE], wp = P.wpos[pl], t = P.cnt[pl];
         const uint32_t bow = P.boffw[pl / WTILE], wpw = P.wposw[pl];
-        const uint32_t g0 = lane < S::MAXS ? P.lslot[pl * (uint64_t)S::MAXS + lane] : LS_SEEN;
+        const uint32_t g0 = lane < MX ? P.lslot[pl * (uint64_t)MX + lane] : LS_SEEN;
         if (!wc) continue;
         const uint64_t start = rec_start<S::RECW_MAX>(P, p);
         uint32_t pc[Lo::NW], ppk[S::CCW];
@@ -1669,7 +1704,7 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
         uint64_t done_w = 0;
         for (uint32_t r0 = 0; r0 < t; r0 += 64) {
             const uint32_t r = r0 + (uint32_t)lane;
-            const uint64_t q = pl * (uint64_t)S::MAXS + r;
+            const uint64_t q = pl * (uint64_t)MX + r;
             bool win = false;
             if (r < t) {
                 const uint32_t g = r0 == 0 ? g0 : P.lslot[q];
@@ -1741,7 +1776,7 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
     // the last block to leave finishes the level (finish_level)
     const uint64_t np = P.p_end - P.p_begin;
     const uint32_t nb = np < gridDim.x ? (np ? (uint32_t)np : 1u) : gridDim.x;
-    if (last_commit_block(P.ctick, nb)) finish_level<S::MAXS, S::RECW_MAX>(P);
+    if (last_commit_block(P.ctick, nb)) finish_level<MX, S::RECW_MAX>(P);
 }
 
 static inline unsigned grid_for(uint64_t n) {
@@ -1749,20 +1784,21 @@ static inline unsigned grid_for(uint64_t n) {
     return (unsigned)(n < cap ? (n ? n : 1) : cap);
 }
 
-template <int N, int V, int MR>
+template <int N, int V, int MR, bool BFV = false>
 struct Launch {
     static void single(const KParams &P, hipStream_t s) {
-        hipLaunchKernelGGL((k_expand<N, V, MR, M_SINGLE>), dim3(1), dim3(64), 0, s, P);
+        hipLaunchKernelGGL((k_expand<N, V, MR, M_SINGLE, BFV>), dim3(1), dim3(64), 0, s, P);
     }
     static void fused(const KParams &P, hipStream_t s) {
-        hipLaunchKernelGGL((k_expand<N, V, MR, M_FUSED>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
+        hipLaunchKernelGGL((k_expand<N, V, MR, M_FUSED, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s,
+                           P);
     }
     static void wincount(const KParams &P, uint64_t np, hipStream_t s) {
         const uint64_t tiles = (np + WTILE - 1) / WTILE;
         hipLaunchKernelGGL((k_wincount<N, V, MR>), dim3(tiles ? (unsigned)tiles : 1u), dim3(1024), 0, s, P);
     }
     static void commit(const KParams &P, hipStream_t s) {
-        hipLaunchKernelGGL((k_commit<N, V, MR>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
+        hipLaunchKernelGGL((k_commit<N, V, MR, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
     }
     static void fps(const KParams &P, uint64_t n, hipStream_t s) {
         hipLaunchKernelGGL((k_fp_states<N, V, MR>), dim3(grid_for(n)), dim3(64), 0, s, P, n);
@@ -1774,25 +1810,29 @@ struct Launch {
     static void dec(const uint32_t *w, uint32_t *c) { decode_core<N, V>(w, c); }
 };
 
-template <int N, int V, int MR>
+template <int N, int V, int MR, bool BFV>
 static void fill(KernelSet *ks) {
     using S = Spec<N, V, MR>;
     ks->N = N; ks->V = V; ks->MR = MR; ks->MCAP = S::MCAP; ks->CCW = S::CCW; ks->RECW_MAX = S::RECW_MAX;
-    ks->maxsucc = S::MAXS;
-    ks->single = &Launch<N, V, MR>::single;
-    ks->fused = &Launch<N, V, MR>::fused;
+    ks->maxsucc = S::MAXS + (BFV ? S::MCAP : 0);
+    ks->single = &Launch<N, V, MR, BFV>::single;
+    ks->fused = &Launch<N, V, MR, BFV>::fused;
     ks->wincount = &Launch<N, V, MR>::wincount;
-    ks->commit = &Launch<N, V, MR>::commit;
+    ks->commit = &Launch<N, V, MR, BFV>::commit;
     ks->fp_states = &Launch<N, V, MR>::fps;
     ks->inv_states = &Launch<N, V, MR>::invs;
     ks->encode = &Launch<N, V, MR>::enc;
     ks->decode = &Launch<N, V, MR>::dec;
 }
 
-bool get_kernels(int N, int V, int msg_cap, KernelSet *ks) {
+bool get_kernels(int N, int V, int msg_cap, bool become_follower, KernelSet *ks) {
     const int MR = msg_cap <= 64 ? 1 : 2;
-#define RMC_CASE(n, v, mr) \
-    if (N == n && V == v && MR == mr) { fill<n, v, mr>(ks); return true; }
+#define RMC_CASE(n, v, mr)                                        \
+    if (N == n && V == v && MR == mr) {                           \
+        if (become_follower) fill<n, v, mr, true>(ks);            \
+        else fill<n, v, mr, false>(ks);                           \
+        return true;                                              \
+    }
     RMC_CASE(2, 1, 1) RMC_CASE(2, 2, 1)
     RMC_CASE(3, 1, 1) RMC_CASE(3, 2, 1) RMC_CASE(3, 3, 1)
     RMC_CASE(3, 1, 2) RMC_CASE(3, 2, 2)

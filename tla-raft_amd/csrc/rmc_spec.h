@@ -20,8 +20,10 @@ namespace rmc {
 // ---- enumerations ---------------------------------------------------------------
 enum Role : uint32_t { FOL = 0, CAN = 1, LEA = 2 };            // Follower, Candidate, Leader (tla:14)
 enum MType : uint32_t { VREQ = 0, VRESP = 1, AREQ = 2, ARESP = 3 }; // tla:8
-// Next's disjuncts in textual order (tla:418-430): the enumeration order TLC uses.
-enum Act : uint32_t { BC = 0, UT, RV, BL, CR, LAE, FAE, FRE, HAR, LCC, RS, NACT };
+// Next's disjuncts in textual order (tla:418-430): the enumeration order TLC uses.  BF =
+// BecomeFollower, in Next only in the tla:420 variant (between UpdateTerm and ResponseVote); its
+// id follows the never-enabled FollowerAppendEntry's (11) so the ids of Raft.tla's actions stay put.
+enum Act : uint32_t { BC = 0, UT, RV, BL, CR, LAE, FAE, FRE, HAR, LCC, RS, NACT, FAPP = NACT, BF };
 constexpr uint32_t VF_NONE = 15;   // votedFor = None (tla:94)
 constexpr int MAXN = 5;
 constexpr int MAXV = 3;
@@ -275,10 +277,13 @@ RMC_HD MsgHash msg_hash(uint32_t info) {
             mix64((SEED_MSG + 0x632be59bd9b4e019ULL) ^ mix64(body * 0xc2b2ae3d27d4eb4fULL + 7))};
 }
 
-// slot key (16 bit): server<<11 | action<<7 | witness -- increasing in TLC order
-RMC_HD uint32_t slot_key(uint32_t s, uint32_t a, uint32_t w) { return (s << 11) | (a << 7) | w; }
+// slot key (16 bit): server<<11 | position<<7 | witness -- increasing in TLC order; the position
+// of an action is its place in Next (BF right after UT)
+RMC_HD uint32_t act_pos(uint32_t a) { return a <= UT ? a : (a == BF ? 2u : a + 1u); }
+RMC_HD uint32_t pos_act(uint32_t p) { return p <= 1u ? p : (p == 2u ? (uint32_t)BF : p - 1u); }
+RMC_HD uint32_t slot_key(uint32_t s, uint32_t a, uint32_t w) { return (s << 11) | (act_pos(a) << 7) | w; }
 RMC_HD uint32_t key_server(uint32_t k) { return k >> 11; }
-RMC_HD uint32_t key_action(uint32_t k) { return (k >> 7) & 15u; }
+RMC_HD uint32_t key_action(uint32_t k) { return pos_act((k >> 7) & 15u); }
 RMC_HD uint32_t key_witness(uint32_t k) { return k & 127u; }
 constexpr uint32_t KEY_NONE = 0xFFFFu;
 

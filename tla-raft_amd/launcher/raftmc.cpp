@@ -22,9 +22,11 @@
 
 namespace {
 
-const char *kActionNames[11] = {"BecomeCandidate", "UpdateTerm", "ResponseVote", "BecomeLeader",
+// rmc_trace_step.action ids (Raft.tla's Next disjuncts; 11 never appears, 12 only in the tla:420 variant)
+const char *kActionNames[13] = {"BecomeCandidate", "UpdateTerm", "ResponseVote", "BecomeLeader",
                                 "ClientReq", "LeaderAppendEntry", "FollowerAcceptEntry", "FollowerRejectEntry",
-                                "HandleAppendResp", "LeaderCanCommit", "Restart"};
+                                "HandleAppendResp", "LeaderCanCommit", "Restart", "FollowerAppendEntry",
+                                "BecomeFollower"};
 const char *kInvNames[7] = {"Inv", "NoSplitVote", "RaftCanCommt", "FollowerCanCommit", "CommitAll", "NoAllCommit",
                             "ExistLeaderAndCandidate"};
 
@@ -58,7 +60,11 @@ struct Loc {
     int l0 = 0, c0 = 0, l1 = 0, c1 = 0;
 };
 
-std::vector<Loc> action_locations(const std::string &tla) {
+// BecomeFollower (tla:226) is a disjunction of three actions; TLC names a step by the one taken,
+// which role[s] of the step's first state decides
+const char *kBfNames[3] = {"FollowerUpdateTerm", "CandidateToFollower", "LeaderToFollower"};
+
+std::vector<Loc> action_locations(const std::string &tla, const std::vector<std::string> &names) {
     std::vector<std::string> lines;
     std::stringstream ss(tla);
     std::string ln;
@@ -66,9 +72,9 @@ std::vector<Loc> action_locations(const std::string &tla) {
         if (!ln.empty() && ln.back() == '\r') ln.pop_back();
         lines.push_back(ln);
     }
-    std::vector<Loc> locs(11);
-    for (int a = 0; a < 11; a++) {
-        const std::string head = std::string(kActionNames[a]) + "(s) ==";
+    std::vector<Loc> locs(names.size());
+    for (size_t a = 0; a < names.size(); a++) {
+        const std::string head = names[a] + "(s) ==";
         for (size_t i = 0; i < lines.size(); i++) {
             if (lines[i].compare(0, head.size(), head) != 0) continue;
             // body starts at the first non-blank character after "=="
@@ -342,22 +348,27 @@ int main(int argc, char **argv) {
             exit_code = 11;
         }
         std::printf("Error: The behavior up to this point is:\n");
-        std::vector<Loc> locs = action_locations(tla);
+        std::vector<std::string> names(kActionNames, kActionNames + 13);
+        names.insert(names.end(), kBfNames, kBfNames + 3);  // 13..15
+        std::vector<Loc> locs = action_locations(tla, names);
         Printer pr{pm, cfg.n_servers, cfg.n_vals};
         std::vector<int32_t> buf(RMC_UNPACKED_INTS(5, 3, 256));
+        std::vector<int32_t> prev_role(cfg.n_servers, 0);
         for (uint32_t i = 0; i < res.trace_len; i++) {
             int32_t a, s, w;
             int nints = rmc_trace_state(ctx, i, buf.data(), buf.size(), &a, &s, &w);
             if (nints < 0) break;
             if (a < 0) std::printf("State %u: <Initial predicate>\n", i + 1);
             else {
-                const Loc &L = locs[a];
+                const int an = (a == 12 && s >= 0 && s < cfg.n_servers) ? 13 + prev_role[s] : a;  // role: 0 F, 1 C, 2 L
+                const Loc &L = locs[an];
                 if (L.l0)
                     std::printf("State %u: <%s line %d, col %d to line %d, col %d of module %s>\n", i + 1,
-                                kActionNames[a], L.l0, L.c0, L.l1, L.c1, pm.module.c_str());
+                                names[an].c_str(), L.l0, L.c0, L.l1, L.c1, pm.module.c_str());
                 else
-                    std::printf("State %u: <%s(%s)>\n", i + 1, kActionNames[a], pm.servers[s].c_str());
+                    std::printf("State %u: <%s(%s)>\n", i + 1, names[an].c_str(), pm.servers[s].c_str());
             }
+            for (int q = 0; q < cfg.n_servers; q++) prev_role[q] = buf[2 * cfg.n_servers + q];  // unpacked: vf, ct, role
             std::printf("%s\n", pr.state(buf.data()).c_str());
         }
     }

@@ -31,8 +31,9 @@ INVARIANT_BITS = {
 INVARIANT_BY_BIT = ["Inv", "NoSplitVote", "RaftCanCommt", "FollowerCanCommit", "CommitAll", "NoAllCommit",
                     "ExistLeaderAndCandidate"]
 ACTIONS = ("BecomeCandidate", "UpdateTerm", "ResponseVote", "BecomeLeader", "ClientReq", "LeaderAppendEntry",
-           "FollowerAcceptEntry", "FollowerRejectEntry", "HandleAppendResp", "LeaderCanCommit", "Restart")
-SPEC_RAFT, SPEC_SEEDED = 0, 1
+           "FollowerAcceptEntry", "FollowerRejectEntry", "HandleAppendResp", "LeaderCanCommit", "Restart",
+           "FollowerAppendEntry", "BecomeFollower")  # 11: never enabled (tla:425 variant); 12: tla:420 variant
+SPEC_RAFT, SPEC_SEEDED, SPEC_BECOME_FOLLOWER = 0, 1, 2
 
 
 class RmcError(RuntimeError):
