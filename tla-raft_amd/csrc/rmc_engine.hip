@@ -22,10 +22,13 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <fcntl.h>
@@ -158,6 +161,72 @@ uint64_t free_device_bytes() {
     return f;
 }
 
+// Pinned host blocks of one size, made ahead of need by a background thread once a run starts
+// taking them: pinning runs at a few GB/s, and done where a trace flush first needs the block it
+// stalls the level loop (a Raft.cfg exhaustion pins ~110 GB of trace).  A block the pool cannot
+// pin is pageable (new char[]).
+class PinnedPool {
+  public:
+    PinnedPool(size_t bytes, int ready) : bytes_(bytes), ready_(ready), th_([this] { run(); }) {}
+    ~PinnedPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+        for (void *p : free_) (void)hipHostFree(p);
+    }
+    void *take(bool *pinned) {
+        {
+            std::unique_lock<std::mutex> lk(m_);
+            demand_ = true;
+            if (!free_.empty()) {
+                void *p = free_.back();
+                free_.pop_back();
+                lk.unlock();
+                cv_.notify_all();
+                *pinned = true;
+                return p;
+            }
+        }
+        cv_.notify_all();
+        void *p = nullptr;
+        if (hipHostMalloc(&p, bytes_, hipHostMallocDefault) == hipSuccess) {
+            *pinned = true;
+            return p;
+        }
+        (void)hipGetLastError();
+        *pinned = false;
+        return new char[bytes_];
+    }
+
+  private:
+    void run() {
+        std::unique_lock<std::mutex> lk(m_);
+        while (!stop_) {
+            if (demand_ && !failed_ && (int)free_.size() < ready_) {
+                lk.unlock();
+                void *p = nullptr;
+                const bool ok = hipHostMalloc(&p, bytes_, hipHostMallocDefault) == hipSuccess;
+                if (!ok) (void)hipGetLastError();
+                lk.lock();
+                if (ok) free_.push_back(p);
+                else failed_ = true;
+                continue;
+            }
+            cv_.wait(lk);
+        }
+    }
+    const size_t bytes_;
+    const int ready_;
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::vector<void *> free_;
+    bool stop_ = false, demand_ = false, failed_ = false;
+    std::thread th_;
+};
+
 // Host array in pinned blocks (falls back to pageable blocks): the trace of every state the run
 // found, written by asynchronous device-to-host copies chunk by chunk, never reallocated.
 template <class T>
@@ -169,19 +238,20 @@ struct HostArr {
     };
     std::vector<Blk> blk;
     uint64_t n = 0;
+    PinnedPool *pool = nullptr;  // blocks of B * sizeof(T) bytes, pinned ahead of need
     HostArr() = default;
     HostArr(const HostArr &) = delete;
     HostArr &operator=(const HostArr &) = delete;
-    HostArr(HostArr &&o) noexcept : blk(std::move(o.blk)), n(o.n) { o.blk.clear(); o.n = 0; }
+    HostArr(HostArr &&o) noexcept : blk(std::move(o.blk)), n(o.n), pool(o.pool) { o.blk.clear(); o.n = 0; }
     HostArr &operator=(HostArr &&o) noexcept {
-        if (this != &o) { release(); blk = std::move(o.blk); n = o.n; o.blk.clear(); o.n = 0; }
+        if (this != &o) { release(); blk = std::move(o.blk); n = o.n; pool = o.pool; o.blk.clear(); o.n = 0; }
         return *this;
     }
     ~HostArr() { release(); }
     void release() {
         for (Blk &b : blk) {
             if (b.pinned) (void)hipHostFree(b.p);
-            else delete[] b.p;
+            else delete[] reinterpret_cast<char *>(b.p);
         }
         blk.clear();
         n = 0;
@@ -189,11 +259,13 @@ struct HostArr {
     void reserve_to(uint64_t m) {
         while ((uint64_t)blk.size() * B < m) {
             Blk b;
-            if (hipHostMalloc((void **)&b.p, B * sizeof(T), hipHostMallocDefault) == hipSuccess) {
+            if (pool) {
+                b.p = static_cast<T *>(pool->take(&b.pinned));
+            } else if (hipHostMalloc((void **)&b.p, B * sizeof(T), hipHostMallocDefault) == hipSuccess) {
                 b.pinned = true;
             } else {
                 (void)hipGetLastError();
-                b.p = new T[B];
+                b.p = reinterpret_cast<T *>(new char[B * sizeof(T)]);
             }
             blk.push_back(b);
         }
@@ -274,6 +346,8 @@ struct Shard {
     uint64_t tdev = 0;  // gid of device trace index 0 (set to tflushed when a kernel sequence starts)
     HostArr<uint64_t> hpar;
     HostArr<uint16_t> hslot;
+    hipEvent_t tev = nullptr;  // the last trace flush on the copy stream
+    bool tev_pending = false;
     std::vector<uint64_t> level_start;  // local gid of the first state of each level
     // chunk buffers (source side)
     uint32_t *cnt = nullptr, *lslot = nullptr, *wpos = nullptr;
@@ -321,6 +395,9 @@ struct rmc_ctx {
     Universe U;
     std::string err;
     hipStream_t stream = nullptr;
+    hipStream_t cstream = nullptr;  // trace flushes (device -> pinned host), overlapped with the level loop
+    hipEvent_t flush_ev = nullptr;  // the main stream's point a flush starts from
+    std::unique_ptr<PinnedPool> pool_par, pool_slot;
     int N = 0, V = 0, RECW = 0;  // RECW = the longest record (fixed-stride buffers)
     uint32_t inv_order = 0;      // invariants in cfg order (check_invs)
     int W = 1, rank = 0;  // shards in the run, this process's first shard
@@ -638,6 +715,10 @@ struct rmc_ctx {
         if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
             throw Fail(RMC_E_DEVICE, std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950");
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&flush_ev, hipEventDisableTiming));
+        pool_par.reset(new PinnedPool(HostArr<uint64_t>::B * 8, 4));
+        pool_slot.reset(new PinnedPool(HostArr<uint16_t>::B * 2, 4));
         if (W > 1 && !virt) {
 #ifdef RMC_WITH_RCCL
             if (!cfg.comm_unique_id) throw Fail(RMC_E_ARG, "world_size > 1 needs comm_unique_id (rmc_comm_unique_id)");
@@ -713,6 +794,9 @@ struct rmc_ctx {
 
     void alloc_shard(Shard &s, int id) {
         s.id = id;
+        s.hpar.pool = pool_par.get();
+        s.hslot.pool = pool_slot.get();
+        HIPCHK(hipEventCreateWithFlags(&s.tev, hipEventDisableTiming));
         s.cnt = dmalloc<uint32_t>(chunk_parents + 1);
         s.fp = dmalloc<ulonglong2>(Gcap);
         s.lslot = dmalloc<uint32_t>(Gcap);
@@ -786,10 +870,13 @@ struct rmc_ctx {
         s.hsum = nullptr; s.hctl = nullptr; s.hsnap = nullptr; s.hlrec = nullptr;
         s.hpar.release();
         s.hslot.release();
+        if (s.tev) (void)hipEventDestroy(s.tev);
+        s.tev = nullptr;
     }
 
     void release() {
         if (stream) (void)hipStreamSynchronize(stream);
+        if (cstream) (void)hipStreamSynchronize(cstream);
         for (Shard &s : sh) free_shard(s);
         sh.clear();
         dfree(d_info); dfree(d_nat2id); dfree(d_gmsg); dfree(d_perms); dfree(d_seeds);
@@ -807,6 +894,12 @@ struct rmc_ctx {
 #endif
         if (stream) (void)hipStreamDestroy(stream);
         stream = nullptr;
+        if (cstream) (void)hipStreamDestroy(cstream);
+        cstream = nullptr;
+        if (flush_ev) (void)hipEventDestroy(flush_ev);
+        flush_ev = nullptr;
+        pool_par.reset();
+        pool_slot.reset();
     }
 
     // ---- frontier storage --------------------------------------------------------------------
@@ -862,7 +955,8 @@ struct rmc_ctx {
     // device trace buffer for `need` entries from tflushed on (everything earlier is on the host)
     void grow_trace(Shard &s, uint64_t need) {
         if (need <= s.trace_cap) return;
-        HIPCHK(hipStreamSynchronize(stream));  // pending flushes read the old buffers
+        HIPCHK(hipStreamSynchronize(stream));
+        HIPCHK(hipStreamSynchronize(cstream));  // pending flushes read the old buffers
         const uint64_t nc = std::max<uint64_t>(need + need / 2, s.trace_cap * 2);
         dfree(s.par);
         dfree(s.pslot);
@@ -871,16 +965,29 @@ struct rmc_ctx {
         s.trace_cap = nc;
     }
 
-    // trace entries of gids [tflushed, upto) to the host (asynchronous, stream-ordered)
+    // trace entries of gids [tflushed, upto) to the host: on the copy stream, after everything
+    // enqueued so far on the main stream, overlapped with what follows there
     void flush_trace(Shard &s, uint64_t upto) {
         if (upto <= s.tflushed) return;
         const uint64_t n = upto - s.tflushed, at = s.tflushed - s.tdev;
-        s.hpar.from_device(s.par + at, s.tflushed, n, stream);
-        s.hslot.from_device(s.pslot + at, s.tflushed, n, stream);
+        HIPCHK(hipEventRecord(flush_ev, stream));
+        HIPCHK(hipStreamWaitEvent(cstream, flush_ev, 0));
+        s.hpar.from_device(s.par + at, s.tflushed, n, cstream);
+        s.hslot.from_device(s.pslot + at, s.tflushed, n, cstream);
+        HIPCHK(hipEventRecord(s.tev, cstream));
+        s.tev_pending = true;
         s.tflushed = upto;
     }
     // the device trace buffer starts over at the first gid not yet on the host
     void trace_restart(Shard &s) { s.tdev = s.tflushed; }
+    // before a launch that writes the device trace buffer: the flushes still reading it are done
+    void trace_fence(Shard &s) {
+        if (!s.tev_pending) return;
+        HIPCHK(hipStreamWaitEvent(stream, s.tev, 0));
+        s.tev_pending = false;
+    }
+    // the host trace arrays are complete (every flush landed)
+    void sync_trace() { HIPCHK(hipStreamSynchronize(cstream)); }
 
     // Seen set: keep the load <= 1/2 in the full (16-B) table, grown x4 by rehash, up to
     // 2^compact_log2 slots; then migrate once to the compact table sized from the budget, whose
@@ -1256,6 +1363,7 @@ struct rmc_ctx {
     // ring, their offsets rebased, their trace entries moved to the local gids of that layout.
     // Earlier levels stay replicated: global id == local gid, answered by shard 0 / rank 0.
     void enter_sharded() {
+        sync_trace();  // the replicated levels' trace is read below
         Shard &s0 = sh[0];
         const size_t Lz = s0.level_start.size();
         const uint64_t F = s0.cur_n, base = s0.level_start[Lz - 1], B = chunk_parents;
@@ -1434,6 +1542,7 @@ struct rmc_ctx {
                 grow_trace(s, Wub);
                 grow_seen(s, s.T_count + Wub);
             }
+            trace_fence(s);
             timed(PH_MAT, [&] { ks.commit(params(), stream); });  // + chunk summary
             HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
@@ -1518,6 +1627,7 @@ struct rmc_ctx {
         grow_trace(s, 4 * target);
         grow_seen(s, s.T_count + 2 * target);
         trace_restart(s);
+        trace_fence(s);
         LevelCtl &h = *s.hctl;
         std::memset(&h, 0, sizeof h);
         h.cur_n = s.cur_n;
@@ -2092,6 +2202,7 @@ struct rmc_ctx {
                 const uint64_t gid = o.level_start[L - 1] + o.cur_n + o.nxt_n;  // local gid of the first
                 grow_trace(o, n);
                 trace_restart(o);
+                trace_fence(o);
                 ensure_tmp(o, n + 1);
                 timed(PH_OTHER, [&] {
                     ring_copy_in(o, ring_wrap(o.nbase() + o.nxt_words, o.rcap), o.ib, words);
@@ -2220,6 +2331,7 @@ struct rmc_ctx {
 
     // Walk parent pointers from err_ref to Init, then replay the slots from Init.
     void build_trace() {
+        sync_trace();
         HIPCHK(hipStreamSynchronize(stream));  // pending trace copies
         std::vector<uint16_t> slots;
         if (err_last_slot != KEY_NONE) slots.push_back((uint16_t)err_last_slot);
@@ -2303,6 +2415,7 @@ struct rmc_ctx {
         if (!inited || finished) throw Fail(RMC_E_STATE, "checkpoint: between levels of a started, unfinished run");
         Shard &s = sh[0];
         HIPCHK(hipStreamSynchronize(stream));
+        sync_trace();
         CkptHeader h = ckpt_header();
         h.depth = depth;
         h.compact = s.Tc ? 1 : 0;
@@ -2440,6 +2553,7 @@ struct rmc_ctx {
     // Forget every explored state but keep all device buffers (repeat runs, benchmarks).
     void reset() {
         HIPCHK(hipStreamSynchronize(stream));
+        sync_trace();
         for (Shard &s : sh) {
             if (s.Tc) HIPCHK(hipMemsetAsync(s.Tc, 0, s.T_cap * 8, stream));
             else HIPCHK(hipMemsetAsync(s.T, 0, s.T_cap * 16, stream));

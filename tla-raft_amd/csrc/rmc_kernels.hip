@@ -246,19 +246,26 @@ __device__ __forceinline__ uint32_t mv_id(const MsgView &mv, uint32_t k) {
 // NoAllCommit tla:451-481.  The state conjuncts come first in the formula, so the message scans
 // (three \E m \in msgs, each short-circuiting on type before prevLogIndex/succ: no evaluation
 // error is possible) run only for a (s1, s2, s3) that passes them.
+// The words NoAllCommit reads, as scalars: the check is out of line (its message scans would
+// swell the commit kernel), and an out-of-line call given a pointer to the core -- or an aggregate,
+// passed in memory -- would put the core of every checked state on the stack.
 template <int N, int V>
-__device__ __noinline__ int inv_nac(const uint32_t *c, const MsgView &mv) {
-    using Lo = Layout<N, V>;
+__device__ __noinline__ int inv_nac(uint32_t role, uint32_t ci, uint32_t ct, uint32_t m0, uint32_t m1, uint32_t m2,
+                                    uint32_t m3, uint32_t m4, const uint32_t *ring, uint64_t start, uint64_t rcap,
+                                    uint32_t nm, uint32_t add0, uint32_t add1, uint32_t nadd, const uint32_t *info) {
+    struct { uint32_t role, ci, ct; } c{role, ci, ct};
+    const MsgView mv{ring, start, rcap, nm, add0, add1, nadd, info};
+    uint32_t mi_s1 = 0;
     for (int s1 = 0; s1 < N; s1++) {
-        if (nib(c[Lo::W_ROLE], s1) != LEA || nib(c[Lo::W_CI], s1) != 2) continue;
+        if (nib(c.role, s1) != LEA || nib(c.ci, s1) != 2) continue;
+        mi_s1 = s1 == 0 ? m0 : s1 == 1 ? m1 : s1 == 2 ? m2 : s1 == 3 ? m3 : m4;
         for (int s2 = 0; s2 < N; s2++) {
-            if (s2 == s1 || nib(c[Lo::W_ROLE], s2) != FOL || nib(c[Lo::W_CI], s2) != 2 ||
-                nib(c[Lo::W_MI + s1], s2) != 2)
+            if (s2 == s1 || nib(c.role, s2) != FOL || nib(c.ci, s2) != 2 || nib(mi_s1, s2) != 2)
                 continue;
             for (int s3 = 0; s3 < N; s3++) {
-                if (s3 == s2 || nib(c[Lo::W_ROLE], s3) != FOL) continue;
-                const uint32_t t3 = nib(c[Lo::W_CT], s3);
-                if (nib(c[Lo::W_CT], s1) != t3 || nib(c[Lo::W_CI], s3) != 1 || nib(c[Lo::W_MI + s1], s3) != 2)
+                if (s3 == s2 || nib(c.role, s3) != FOL) continue;
+                const uint32_t t3 = nib(c.ct, s3);
+                if (nib(c.ct, s1) != t3 || nib(c.ci, s3) != 1 || nib(mi_s1, s3) != 2)
                     continue;
                 bool c1 = false, c2 = false, c3 = false;
                 for (uint32_t k = 0; k < mv.nm + mv.nadd; k++) {
@@ -282,7 +289,13 @@ __device__ __forceinline__ int inv_eval(const uint32_t *c, int id, const MsgView
     using Lo = Layout<N, V>;
     switch (id) {
     case 0: return inv_lhace<N, V>(c);
-    case 5: return inv_nac<N, V>(c, mv);
+    case 5: {
+        uint32_t mi[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < N; q++) mi[q] = c[Lo::W_MI + q];
+        return inv_nac<N, V>(c[Lo::W_ROLE], c[Lo::W_CI], c[Lo::W_CT], mi[0], mi[1], mi[2], mi[3], mi[4], mv.ring,
+                             mv.start, mv.rcap, mv.nm, mv.add0, mv.add1, mv.nadd, mv.info);
+    }
     case 1: {  // NoSplitVote tla:444-448
 #pragma unroll
         for (int a = 0; a < N; a++)
