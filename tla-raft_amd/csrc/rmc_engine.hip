@@ -1655,7 +1655,7 @@ struct rmc_ctx {
         // with an event.  Group g + 2 is enqueued only once group g's snapshot says the loop is
         // still running, so the device always has a group queued and at most two groups of
         // no-op launches follow the last level.
-        const int GL = 4, ngroups = (K + GL - 1) / GL;
+        const int GL = 2, ngroups = (K + GL - 1) / GL;
         while ((int)gev.size() < 3) {
             hipEvent_t e;
             HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));

@@ -839,8 +839,15 @@ __device__ __forceinline__ void load_parent(const KParams &P, uint64_t start, in
                             uint64_t *M0, uint64_t *M1, uint32_t *pcore) {
     using Lo = Layout<N, V>;
     using S = Spec<N, V, MR>;
+    // the whole record in one round trip: lane k holds record word k (and 64 + k); the core is
+    // read across lanes, each lane's message ids are shuffled to it below -- no second dependent
+    // load for the ids (words past the record's end are read but never used)
+    const uint32_t rw0 = lane < S::RECW_MAX ? ring_word(P.front, start, (uint32_t)lane, P.rcap) : 0u;
+    const uint32_t rw1 = (MR > 1 && 64 + lane < S::RECW_MAX) ? ring_word(P.front, start, 64u + (uint32_t)lane, P.rcap) : 0u;
     uint32_t packed[S::CCW];
-    load_core<N, V>(P.front, start, P.rcap, lane, W.c, packed);
+#pragma unroll
+    for (int k = 0; k < S::CCW; k++) packed[k] = rdlane(rw0, k);
+    decode_core<N, V>(packed, W.c);
     if (lane == 0) {  // uniform values: one lane writes the LDS copy (no runtime-indexed register array)
 #pragma unroll
         for (int w = 0; w < Lo::NW; w++) pcore[w] = W.c[w];
@@ -853,9 +860,13 @@ __device__ __forceinline__ void load_parent(const KParams &P, uint64_t start, in
 #pragma unroll
     for (int r = 0; r < MR; r++) {
         const uint32_t k = (uint32_t)(r * 64 + lane);
+        const uint32_t wi = (uint32_t)S::CCW + (k >> 1);  // record word holding id k
+        const uint32_t a = __shfl(rw0, (int)(wi & 63u), 64);
+        const uint32_t b = MR > 1 ? __shfl(rw1, (int)(wi & 63u), 64) : 0u;
+        const uint32_t word = wi < 64u ? a : b;
         uint32_t id = 0xFFFFu, inf = 0;
         if (k < W.nm) {
-            id = ring_id(P.front, W.idw, k, P.rcap);
+            id = (word >> ((k & 1u) * 16u)) & 0xFFFFu;
             inf = P.t.info[id];
             if (SUMS) {
                 const ulonglong2 g = P.t.gmsg[id];
@@ -1431,6 +1442,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? 4 : ((BFV && N >=
                     }
                     sPart[lane] = make_ulonglong2(m0, m1);
                     __syncthreads();
+                    PHASE(5);
                     const uint32_t lo = b0 + (uint32_t)lane;
                     if ((uint32_t)lane < SB && lo < total) {
                         ulonglong2 best = sPart[lane * PB];
@@ -1441,6 +1453,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? 4 : ((BFV && N >=
                         emit(lo, best);
                     }
                     __syncthreads();
+                    PHASE(6);
                 }
             }
         }
@@ -1701,15 +1714,24 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
         const uint32_t g0 = lane < MX ? P.lslot[pl * (uint64_t)MX + lane] : LS_SEEN;
         if (!wc) continue;
         const uint64_t start = rec_start<S::RECW_MAX>(P, p);
+        // the parent's record in one round trip (as load_parent)
+        const uint32_t rw0 = lane < S::RECW_MAX ? ring_word(P.front, start, (uint32_t)lane, P.rcap) : 0u;
+        const uint32_t rw1 =
+            (MR > 1 && 64 + lane < S::RECW_MAX) ? ring_word(P.front, start, 64u + (uint32_t)lane, P.rcap) : 0u;
         uint32_t pc[Lo::NW], ppk[S::CCW];
-        load_core<N, V>(P.front, start, P.rcap, lane, pc, ppk);
+#pragma unroll
+        for (int k = 0; k < S::CCW; k++) ppk[k] = rdlane(rw0, k);
+        decode_core<N, V>(ppk, pc);
         const uint32_t nm = (pc[Lo::W_MISC] >> 16) & 0xFFu;
         const uint64_t idw = ring_wrap(start + S::CCW, P.rcap);
         uint32_t id[MR];
 #pragma unroll
         for (int r = 0; r < MR; r++) {
             const uint32_t k = (uint32_t)(r * 64 + lane);
-            id[r] = k < nm ? ring_id(P.front, idw, k, P.rcap) : 0xFFFFu;
+            const uint32_t wi = (uint32_t)S::CCW + (k >> 1);
+            const uint32_t a = __shfl(rw0, (int)(wi & 63u), 64);
+            const uint32_t b = MR > 1 ? __shfl(rw1, (int)(wi & 63u), 64) : 0u;
+            id[r] = k < nm ? (((wi < 64u ? a : b) >> ((k & 1u) * 16u)) & 0xFFFFu) : 0xFFFFu;
         }
         const uint32_t w0 = bo + wp;
         const uint64_t wd0 = P.next_wbase + bow + wpw;

@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.join(ROOT, "tla-raft_amd"))
 import raftmc  # noqa: E402
 
 NAMES = ["load parent", "evaluate actions", "ranks + error keys", "staging", "hash inputs",
-         "symmetry min (+probe/elect n3)", "probe + elect (n>=4)", "-"]
+         "symmetry min", "seen-set probe + election", "-"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("n", type=int)
