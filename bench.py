@@ -108,6 +108,80 @@ def cpu_baseline(w, budget_s=12.0):
                       f"box), {dt:.1f} s"}
 
 
+SHARDED_TIMEOUT_S = 420  # the multi-GPU Raft.cfg exhaustion (child processes) must finish within this
+
+
+def sharded_child(args):
+    """One rank of the multi-GPU Raft.cfg exhaustion (configs[2] at N GPUs), run in a child process of
+    each bench rank before the bench touches the GPU: the levels are sharded over the N GPUs (RCCL,
+    block-cyclic frontier, fingerprint-owner seen set) from the first level of
+    >= 2^20 states.  Rank 0 writes the result to args.sharded_out."""
+    import torch
+    import torch.distributed as dist
+    import raftmc
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    port = int(os.environ.get("MASTER_PORT", "29500")) + 17
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    idt = torch.zeros(128, dtype=torch.uint8)
+    if rank == 0:
+        idt = torch.tensor(list(raftmc.comm_unique_id()), dtype=torch.uint8)
+    dist.broadcast(idt, 0)
+    w = WORKLOADS["raftcfg"]
+    cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
+                             invariants=("Inv",), check_deadlock=False, device=local, rank=rank, world_size=world,
+                             comm_unique_id=bytes(idt.tolist()))
+    with raftmc.ModelChecker(cfg) as mc:
+        dist.barrier()
+        t0 = time.perf_counter()
+        res = mc.run()
+        dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    if rank == 0:
+        gold = {}
+        gpath = os.path.join(ROOT, "tests", "golden", "levels_prefix.json")
+        if os.path.exists(gpath):
+            gold = json.load(open(gpath)).get("n3_v2_e3_r3", {})
+        got = [ls.new_states for ls in res.levels]
+        out = {"workload": w["desc"], "n_gpus": world, "parallelism": f"rccl-{world}: block-cyclic levels, "
+               "fingerprint-owner seen set, TLC-order global-key election, from the first level of >= 2^20 states",
+               "distinct_states": res.distinct, "states_generated": res.generated, "depth": res.depth,
+               "verdict": "Inv holds" if res.status == "done" else res.status,
+               "seconds_to_exhaust": round(dt, 3), "distinct_per_s": round(res.distinct / dt, 1),
+               "matches_c_oracle_prefix_levels": (got[:len(gold["levels"])] == gold["levels"]) if gold else None}
+        with open(args.sharded_out, "w") as f:
+            json.dump(out, f)
+    dist.destroy_process_group()
+
+
+def run_sharded_children(args):
+    """Start this rank's sharded Raft.cfg child (before this process initialises the GPU), wait for it
+    with a time limit, and return rank 0's result (or what went wrong)."""
+    import subprocess
+    import tempfile
+    rank = int(os.environ.get("RANK", "0"))
+    out = os.path.join(tempfile.gettempdir(), f"rmc_sharded_{os.environ.get('MASTER_PORT', '0')}.json")
+    if rank == 0 and os.path.exists(out):
+        os.remove(out)
+    cmd = [sys.executable, os.path.abspath(__file__), "--sharded-child", "--sharded-out", out]
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, stdout=sys.stderr, stderr=sys.stderr)
+    try:
+        rc = p.wait(timeout=SHARDED_TIMEOUT_S)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.wait()
+        return {"error": f"timed out after {SHARDED_TIMEOUT_S} s", "wall_s": round(time.perf_counter() - t0, 1)}
+    if rank != 0:
+        return None
+    if rc != 0 or not os.path.exists(out):
+        return {"error": f"child exited with {rc}", "wall_s": round(time.perf_counter() - t0, 1)}
+    with open(out) as f:
+        return json.load(f)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -116,8 +190,17 @@ def main():
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe-peak", action="store_true")
-    ap.add_argument("--no-scale", action="store_true", help="skip the at-scale reference exhaustion (N=1)")
+    ap.add_argument("--no-scale", action="store_true", help="skip the at-scale reference exhaustion (N=1) / the "
+                    "multi-GPU Raft.cfg exhaustion (N>1)")
+    ap.add_argument("--sharded-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--sharded-out", default="", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.sharded_child:
+        sharded_child(args)
+        return
+    sharded = None
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not args.no_scale:
+        sharded = run_sharded_children(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -263,6 +346,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_scale:
         line["at_scale"] = at_scale(local)
+    if rank == 0 and sharded is not None:
+        line["at_scale_sharded"] = sharded
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(w)
     if rank == 0:
@@ -320,9 +405,11 @@ def at_scale(device, workload="raftcfg"):
             "expand_frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
 
 
-KERNEL_NAME = {"expand_hash": "void rmc::k_expand<{n}, {V}, {mr}, 4>(rmc::KParams)",
-               "dedup": "void rmc::k_wincount<{n}, {V}, {mr}>(rmc::KParams)",
-               "materialize": "void rmc::k_commit<{n}, {V}, {mr}>(rmc::KParams)"}
+KERNEL_NAME = {"expand_hash": ["void rmc::k_expand<{n}, {V}, {mr}, 4, false>(rmc::KParams)",
+                               "void rmc::k_expand<{n}, {V}, {mr}, 4>(rmc::KParams)"],
+               "dedup": ["void rmc::k_wincount<{n}, {V}, {mr}>(rmc::KParams)"],
+               "materialize": ["void rmc::k_commit<{n}, {V}, {mr}, false>(rmc::KParams)",
+                               "void rmc::k_commit<{n}, {V}, {mr}>(rmc::KParams)"]}
 
 
 PMC_RUNS = 6  # tools/pmc.sh: bench.py --steps 5 --warmup 1 per counter pass
@@ -339,9 +426,10 @@ def pmc_kernel(mc, phase, workload, depth):
         return {}
     n, V = mc.cfg.n_servers, mc.cfg.n_vals
     mr = 1 if (mc.cfg.msg_cap or (64 if n <= 3 else 128)) <= 64 else 2
-    name = KERNEL_NAME[phase].format(n=n, V=V, mr=mr)
     d = json.load(open(files[-1]))
-    e = d.get(name)
+    e = None
+    for name in KERNEL_NAME[phase]:  # kernel names before / after the spec-variant template argument
+        e = e or d.get(name.format(n=n, V=V, mr=mr))
     if not e:
         return {}
     # the device-driven level loop enqueues a few levels past the last one, whose launches
