@@ -88,7 +88,8 @@ typedef struct rmc_config {
                                   rmc_run_levels (0 = auto, 1 = the host drives every level) */
     uint64_t shard_min_states; /* world_size or virtual_shards > 1: levels with fewer states than this are
                                   expanded whole on every shard (replicated, no exchange, TLC order); the run
-                                  switches to fingerprint-owner sharding at the first level that reaches it
+                                  switches to the sharded level (block-cyclic frontier, fingerprint-owner seen
+                                  set, TLC-order election by global key) at the first level that reaches it
                                   and stays sharded (0 = auto: 2^20; 1 = sharded from Init's level) */
     /* ---- ABI 3 ---- */
     uint32_t invariant_order;  /* the INVARIANTs in cfg order (Raft.cfg:33-34; TLC checks them in that order):
@@ -107,7 +108,7 @@ typedef struct rmc_config {
 typedef struct rmc_level_stats {
     int32_t level;            /* BFS level whose states were just expanded (1 = Init's level) */
     int32_t status;           /* RMC_OK / RMC_DONE / RMC_VIOLATION / ... */
-    uint64_t expanded;        /* states of that level expanded (this rank) */
+    uint64_t expanded;        /* states of that level expanded (all ranks) */
     uint64_t generated;       /* successors generated while expanding it (all ranks) */
     uint64_t new_states;      /* distinct states first found (all ranks) */
     uint64_t total_generated; /* TLC "states generated", Init included */
