@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <filesystem>
 #include <fstream>
 #include <sstream>
 #include <string>
@@ -310,7 +311,9 @@ int main(int argc, char **argv) {
         if (rc == RMC_OK && ckpt_minutes > 0 && since >= ckpt_minutes * 60.0) {
             // TLC -checkpoint: the run so far, between two levels (rmc_checkpoint)
             std::printf("Checkpointing of run %s\n", metadir.c_str());
-            (void)std::system(("mkdir -p '" + metadir + "'").c_str());
+            std::error_code ec;
+            std::filesystem::create_directories(metadir, ec);  // TLC's states/ metadir (no shell)
+            if (ec) std::fprintf(stderr, "raftmc: cannot create %s: %s\n", metadir.c_str(), ec.message().c_str());
             const std::string f = metadir + "/raftmc.ckpt";
             if (rmc_checkpoint(ctx, f.c_str()) < 0) std::printf("Warning: checkpoint failed: %s\n", rmc_last_error(ctx));
             else std::printf("Checkpointing completed at (%s)\n", now_str().c_str());
