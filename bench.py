@@ -70,6 +70,26 @@ def alg_bytes(phase, F, G, N, S, CCWB, slot_bytes=16, SWB=32):
     return 0
 
 
+def survey_roofline(levels, S, wall_s, probes_per_s):
+    """SURVEY.md 8(d)'s whole-run model: B_L = F_L*S + G_L*64 + N_{L+1}*(S + 16) algorithmic bytes per
+    level (one 64-B bucket probe per generated successor), roofline time = sum_L G_L*64 / BW_rand +
+    (F_L*S + N_{L+1}*(S + 16)) / BW_stream with BW_stream = 8 TB/s and BW_rand = the measured random
+    64-B probe rate of this GPU (rmc_probe_peak, HBM-resident table).  frac = roofline time / wall."""
+    F = sum(ls.expanded for ls in levels)
+    G = sum(ls.generated for ls in levels[1:])
+    N = sum(ls.new_states for ls in levels[1:])
+    rand_b = G * 64
+    stream_b = F * S + N * (S + 16)
+    out = {"bytes": int(rand_b + stream_b), "achieved_GBps": round((rand_b + stream_b) / wall_s / 1e9, 2),
+           "record_bytes_avg": round(S, 2)}
+    if probes_per_s:
+        bw_rand = probes_per_s * 64
+        t = rand_b / bw_rand + stream_b / (HBM_PEAK_GBS * 1e9)
+        out.update({"bw_rand_GBps": round(bw_rand / 1e9, 1), "roofline_s": round(t, 6), "wall_s": round(wall_s, 6),
+                    "frac": round(t / wall_s, 4)})
+    return out
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -318,6 +338,7 @@ def main():
     probes = (res.generated + res.distinct) * args.steps * (world if parallelism.startswith("replicas") else 1)
     seen = {"probes_per_step": res.generated + res.distinct,
             "achieved_probes_per_s": round(probes / elapsed, 1)}
+    pk_hbm = None
     if rank == 0 and not args.no_probe_peak:
         pk_small = raftmc.probe_peak(local, 22, 1 << 26)
         pk_hbm = raftmc.probe_peak(local, 28, 1 << 28)
@@ -343,9 +364,10 @@ def main():
                    "parallelism": parallelism},
         "roofline": roof,
         "seen_set": seen,
+        "survey_roofline": survey_roofline(res.levels, S, elapsed / args.steps, pk_hbm),
     }
     if rank == 0 and world == 1 and not args.no_scale:
-        line["at_scale"] = at_scale(local)
+        line["at_scale"] = at_scale(local, probes_per_s=pk_hbm)
     if rank == 0 and sharded is not None:
         line["at_scale_sharded"] = sharded
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -357,7 +379,7 @@ def main():
         dist.destroy_process_group()
 
 
-def at_scale(device, workload="raftcfg"):
+def at_scale(device, workload="raftcfg", probes_per_s=None):
     """configs[0]/[2] -- Raft.cfg as shipped -- exhausted on this GPU (not the headline: one run is
     ~75 s).  The first run includes growing every buffer (the seen set's move to 8-B slots, the
     frontier ring, the pinned host trace); the second, after rmc_reset, is the steady state.  Its
@@ -402,7 +424,8 @@ def at_scale(device, workload="raftcfg"):
             "frontier_ring_bytes": res.frontier_ring_bytes, "frontier_peak_bytes": res.frontier_peak_bytes,
             "record_bytes_avg": round(S, 2),
             "expand_kernel_ms": round(ms, 3), "expand_alg_GBps": round(gbs, 1),
-            "expand_frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
+            "expand_frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+            "survey_roofline": survey_roofline(res.levels, S, dt, probes_per_s)}
 
 
 KERNEL_NAME = {"expand_hash": ["void rmc::k_expand<{n}, {V}, {mr}, 4, false>(rmc::KParams)",
