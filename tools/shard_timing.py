@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
-"""Time the sharded (fingerprint-owner) path with virtual shards on one GPU against the fused
-single-GPU path, on BASELINE configs[1]: where the per-level exchange cost goes."""
+"""Time the sharded path (block-cyclic levels, fingerprint-owner election) run as
+virtual shards on one GPU -- every shard's work in one process, device copies as the transport -- against
+the single-GPU path.  The shards run one after another, so the extra time over one GPU is the sharding
+overhead (routing, owner election, record exchange, host round trips per round), not a speed-up.
+
+usage: shard_timing.py [n V E R] [--shard-min K] [--reps R]"""
+import argparse
 import os
 import sys
 import time
@@ -9,8 +14,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tla-raft_amd"))
 import raftmc  # noqa: E402
 
+PH = ["count", "expand", "wincount", "commit", "exchange", "other"]
 
-def timed(cfg, reps=5):
+
+def timed(cfg, reps):
     with raftmc.ModelChecker(cfg) as mc:
         mc.run()
         t0 = time.perf_counter()
@@ -25,9 +32,19 @@ def timed(cfg, reps=5):
         return res, dt, ms
 
 
+ap = argparse.ArgumentParser()
+ap.add_argument("cfg", nargs="*", type=int, default=[3, 1, 2, 3])
+ap.add_argument("--shard-min", type=int, default=1)
+ap.add_argument("--reps", type=int, default=3)
+a = ap.parse_args()
+n, V, E, R = a.cfg
+base = None
 for vs in [1, 2, 4, 8]:
-    cfg = raftmc.ModelConfig(n_servers=3, n_vals=1, max_election=2, max_restart=3, device=0,
-                             virtual_shards=vs if vs > 1 else 0, timing_phases=0x3F)
-    res, dt, ms = timed(cfg)
-    print(f"shards={vs}: {res.distinct} distinct, depth {res.depth}, {dt * 1e3:.2f} ms/exhaustion, "
-          f"{res.distinct / dt / 1e6:.1f} M states/s; phase ms {[round(x, 2) for x in ms]}", flush=True)
+    cfg = raftmc.ModelConfig(n_servers=n, n_vals=V, max_election=E, max_restart=R, device=0,
+                             virtual_shards=vs if vs > 1 else 0, shard_min_states=a.shard_min, timing_phases=0x3F)
+    res, dt, ms = timed(cfg, a.reps)
+    base = base or dt
+    tot = sum(ms) or 1.0
+    print(f"shards={vs}: {res.distinct} distinct, depth {res.depth}, {dt * 1e3:.2f} ms/exhaustion "
+          f"({dt / base:.2f}x one GPU), kernel ms " + ", ".join(f"{PH[i]} {ms[i]:.1f}" for i in range(6) if ms[i]) +
+          f"; exchange {100 * ms[4] / tot:.0f} % of kernel time", flush=True)
