@@ -78,8 +78,9 @@ typedef struct rmc_config {
     int32_t seen_log2;      /* initial seen-set slots = 2^seen_log2 (0 = auto); grows on demand */
     int32_t no_symmetry;    /* 0 = SYMMETRY symmServers (Raft.cfg:24); 1 = cfg without SYMMETRY */
     uint64_t chunk_successors; /* successors per device chunk (0 = auto) */
-    /* multi-GPU (one process per GPU): world_size 1 = single GPU */
-    int32_t rank, world_size;  /* world_size 0 or 1 = single GPU */
+    /* multi-GPU (one process per GPU): world_size 0 or 1 = single GPU */
+    int32_t rank, world_size;  /* world_size 0 or 1 = single GPU; world_size 1 WITH comm_unique_id = a one-rank
+                                  RCCL communicator running the sharded protocol (self send/recv) */
     const void *comm_unique_id; /* 128-byte RCCL unique id (rmc_comm_unique_id on rank 0), same on every rank */
     int32_t virtual_shards;    /* > 1: run that many fingerprint-owner shards in this process on one device
                                   (the multi-GPU partition/exchange logic with device copies for transport) */

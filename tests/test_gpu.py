@@ -361,6 +361,25 @@ def test_sharded_bfs_identical_to_one_shard(name, shards, shard_min):
     mc.close()
 
 
+# The same protocol through the RCCL transport: world_size 1 with a unique id is a one-rank
+# communicator, so every collective of step_sharded (all-reduce of the level size, all-to-all of
+# the owner counts, grouped ncclSend/ncclRecv of successors, verdicts and winner records, the
+# round's failure table) runs through RCCL on the stream.  A one-GPU box cannot hold two ranks
+# (RCCL refuses two ranks on one device); this is the RCCL code path short of the xGMI hop.
+@pytest.mark.parametrize("shard_min", [1, 40])
+@pytest.mark.parametrize("name", ["n3_v1_e2_r3", "n4_v1_e1_r3", "seeded_n3_v2_e2_r3", "deadlock_n3_v1_e1_r3",
+                                  "n2_v2_e3_r3", "exist_lc_n3_v1_e2_r3"])
+def test_rccl_one_rank_identical_to_single(name, shard_min):
+    g = LEVELS[name]
+    mc, res = run_cfg(g, world_size=1, rank=0, comm_unique_id=raftmc.comm_unique_id(), chunk_successors=3000,
+                      shard_min_states=shard_min)
+    check_levels(g, res)
+    if name in TRACES:
+        assert [(list(k) if k else None, st) for k, st in mc.trace()] == \
+               [(e["key"], e["state"]) for e in TRACES[name]["steps"]]
+    mc.close()
+
+
 @pytest.mark.parametrize("shards", [2, 3, 8])
 @pytest.mark.parametrize("name", ["seeded_n3_v2_e2_r3", "deadlock_n3_v1_e1_r3", "n3_v2_e1_r3"])
 def test_sharded_level_stats_equal_single(name, shards):

@@ -402,6 +402,8 @@ struct rmc_ctx {
     uint32_t inv_order = 0;      // invariants in cfg order (check_invs)
     int W = 1, rank = 0;  // shards in the run, this process's first shard
     bool virt = false;    // all W shards live in this process
+    bool multi = false;   // the sharded protocol runs (W > 1, or one RCCL rank talking to itself)
+    bool rccl = false;    // shards exchange through an RCCL communicator (not device copies)
 #ifdef RMC_WITH_RCCL
     ncclComm_t comm = nullptr;
 #endif
@@ -694,6 +696,11 @@ struct rmc_ctx {
         virt = cfg.virtual_shards > 1;
         W = virt ? cfg.virtual_shards : ws;
         rank = virt ? 0 : (ws > 1 ? cfg.rank : 0);
+        // world_size == 1 with a unique id: a one-rank communicator; the sharded protocol then
+        // runs through RCCL (self send/recv, one-rank all-reduce/all-to-all) -- its transport
+        // exercised on a one-GPU machine
+        rccl = !virt && (ws > 1 || (cfg.world_size == 1 && cfg.comm_unique_id));
+        multi = W > 1 || rccl;
         if (rank < 0 || rank >= W) throw Fail(RMC_E_ARG, "rank out of range");
         N = cfg.n_servers;
         V = cfg.n_vals;
@@ -719,7 +726,7 @@ struct rmc_ctx {
         HIPCHK(hipEventCreateWithFlags(&flush_ev, hipEventDisableTiming));
         pool_par.reset(new PinnedPool(HostArr<uint64_t>::B * 8, 4));
         pool_slot.reset(new PinnedPool(HostArr<uint16_t>::B * 2, 4));
-        if (W > 1 && !virt) {
+        if (rccl) {
 #ifdef RMC_WITH_RCCL
             if (!cfg.comm_unique_id) throw Fail(RMC_E_ARG, "world_size > 1 needs comm_unique_id (rmc_comm_unique_id)");
             ncclUniqueId id;
@@ -768,11 +775,11 @@ struct rmc_ctx {
 
         // successor slots per chunk: dense for the sharded path, sparse (parents x maxsucc) for
         // the fused single-GPU path, whose staging holds SW4 * 16 + 36 bytes per slot
-        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (W > 1 ? (virt ? (1ull << 23) : (1ull << 26)) : (1ull << 26));
+        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (multi ? (virt ? (1ull << 23) : (1ull << 26)) : (1ull << 26));
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 30)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^30");
         chunk_parents = Gcap / ks.maxsucc;
-        shard_min = W > 1 ? (cfg.shard_min_states ? cfg.shard_min_states : (1ull << 20)) : 0;
+        shard_min = multi ? (cfg.shard_min_states ? cfg.shard_min_states : (1ull << 20)) : 0;
         chunk_parents = std::min<uint64_t>(chunk_parents, (uint64_t)WTILE * 1024);  // winner-count tiles
         Lcap_max = next_pow2(2 * Gcap);
 
@@ -827,7 +834,7 @@ struct rmc_ctx {
         HIPCHK(hipHostMalloc((void **)&s.hctl, sizeof(LevelCtl), hipHostMallocDefault));
         HIPCHK(hipHostMalloc((void **)&s.hsnap, 3 * sizeof(LevelCtl), hipHostMallocDefault));
         HIPCHK(hipHostMalloc((void **)&s.hlrec, sizeof(LevelRec) * LREC_CAP, hipHostMallocDefault));
-        if (W > 1) {
+        if (multi) {
             s.perm = dmalloc<uint32_t>(Gcap);
             s.sflag = dmalloc<uint32_t>(Gcap);
             s.ocnt = dmalloc<uint32_t>(64);
@@ -1158,7 +1165,7 @@ struct rmc_ctx {
     // Every host value handed to these is this process's contribution (virtual mode: the
     // sum/max over all local shards already IS the global value).
     void allreduce(uint64_t *v, int n, bool is_max) {
-        if (W == 1 || virt) return;
+        if (!rccl) return;
 #ifdef RMC_WITH_RCCL
         for (int i = 0; i < n; i++) h_red[i] = v[i];
         HIPCHK(hipMemcpyAsync(d_red, h_red, n * 8, hipMemcpyHostToDevice, stream));
@@ -1173,7 +1180,7 @@ struct rmc_ctx {
     // counts: c_out[local d][s] = c_in[local s][d]
     void exchange_counts(const std::vector<std::vector<uint64_t>> &in, std::vector<std::vector<uint64_t>> &out) {
         out.assign(sh.size(), std::vector<uint64_t>(W, 0));
-        if (virt || W == 1) {
+        if (!rccl) {
             for (int s = 0; s < W && s < (int)in.size(); s++)
                 for (int d = 0; d < (int)sh.size(); d++) out[d][s] = in[s][d];
             return;
@@ -1194,7 +1201,7 @@ struct rmc_ctx {
     void exchange_items(const std::vector<const void *> &send, const std::vector<std::vector<uint64_t>> &scnt,
                         const std::vector<std::vector<uint64_t>> &soff, const std::vector<void *> &recv,
                         const std::vector<std::vector<uint64_t>> &roff, size_t elem) {
-        if (virt || W == 1) {
+        if (!rccl) {
             for (int s = 0; s < W; s++)
                 for (int d = 0; d < W; d++) {
                     const uint64_t n = scnt[s][d];
@@ -1279,8 +1286,8 @@ struct rmc_ctx {
         ks.fp_states(P, 1, stream);
         ks.inv_states(P, 1, d_inv, stream);
         uint32_t owner = 0;  // the shard whose seen set takes Init's fingerprint
-        replicated = W > 1 && shard_min > 1;
-        if (W > 1 && !replicated) {
+        replicated = multi && shard_min > 1;
+        if (multi && !replicated) {
             launch_owner_of(d_fp1, (uint32_t)W, d_cnt1, stream);
             owner = d2h(d_cnt1);
             glevel = {0};
@@ -1295,21 +1302,21 @@ struct rmc_ctx {
             s.cur_n = 0;
             s.cur_wbase = s.cur_words = s.nxt_words = 0;
             // Init is global index 0 of level 1: block 0, shard 0 (W > 1 from the start)
-            const bool holds = replicated || W == 1 ? &s == &sh[0] : s.id == 0;
-            if (W > 1 && !replicated && (uint32_t)s.id == owner) {
+            const bool holds = replicated || !multi ? &s == &sh[0] : s.id == 0;
+            if (multi && !replicated && (uint32_t)s.id == owner) {
                 launch_insert_fps(d_fp1, 1, s.seen(), stream);
                 s.T_count = 1;
             }
             if (!holds) continue;
             HIPCHK(hipMemcpyAsync(s.R, d_one, rw * 4, hipMemcpyDeviceToDevice, stream));
             HIPCHK(hipMemcpyAsync(s.cur_off, &zero, 8, hipMemcpyHostToDevice, stream));
-            if (W == 1 || replicated) launch_insert_fps(d_fp1, 1, s.seen(), stream);
+            if (!multi || replicated) launch_insert_fps(d_fp1, 1, s.seen(), stream);
             s.hpar.set(0, ~0ull);
             s.hslot.set(0, 0);
             s.tflushed = 1;
             s.cur_n = 1;
             s.cur_words = rw;
-            if (W == 1 || replicated) s.T_count = 1;
+            if (!multi || replicated) s.T_count = 1;
         }
         HIPCHK(hipStreamSynchronize(stream));
         total_generated = 1;  // TLC counts the initial state as generated
@@ -1353,7 +1360,7 @@ struct rmc_ctx {
         if (!st) st = &local;
         std::memset(st, 0, sizeof *st);
         if (replicated && sh[0].cur_n >= shard_min) enter_sharded();
-        return (W == 1 || replicated) ? step_single(st) : step_sharded(st);
+        return (!multi || replicated) ? step_single(st) : step_sharded(st);
     }
 
     // Replicated -> sharded, at the start of the first level with >= shard_min states.  Every
@@ -1599,7 +1606,7 @@ struct rmc_ctx {
     bool batch_ok() const {
         const Shard &s = sh[0];
         const uint64_t first = s.cur_n * (uint64_t)ks.maxsucc;
-        return (W == 1 || (replicated && s.cur_n < shard_min)) && inited && !finished && cfg.device_levels != 1 &&
+        return (!multi || (replicated && s.cur_n < shard_min)) && inited && !finished && cfg.device_levels != 1 &&
                s.cur_n > 0 && s.cur_n <= dev_parents() && ring_room(s, first * (uint64_t)ks.RECW_MAX, 0) &&
                seen_room(s, s.T_count + 2 * first);
     }
@@ -2411,7 +2418,7 @@ struct rmc_ctx {
     // Written to path + ".tmp", flushed to disk, then renamed over path: the previous checkpoint
     // survives until the new one is complete.
     void checkpoint(const char *path) {
-        if (W != 1) throw Fail(RMC_E_ARG, "checkpoint: single-GPU runs only");
+        if (multi) throw Fail(RMC_E_ARG, "checkpoint: single-GPU runs only");
         if (!inited || finished) throw Fail(RMC_E_STATE, "checkpoint: between levels of a started, unfinished run");
         Shard &s = sh[0];
         HIPCHK(hipStreamSynchronize(stream));
@@ -2458,7 +2465,7 @@ struct rmc_ctx {
     }
 
     void resume(const char *path) {
-        if (W != 1) throw Fail(RMC_E_ARG, "resume: single-GPU runs only");
+        if (multi) throw Fail(RMC_E_ARG, "resume: single-GPU runs only");
         if (inited) throw Fail(RMC_E_STATE, "resume: needs a context not yet initialised (rmc_create or rmc_reset)");
         FILE *f = std::fopen(path, "rb");
         if (!f) throw Fail(RMC_E_ARG, std::string("resume: cannot read ") + path);
