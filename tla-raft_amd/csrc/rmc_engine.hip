@@ -361,7 +361,8 @@ struct Shard {
     uint32_t *wcnt = nullptr, *wacc = nullptr, *pnm = nullptr, *wposw = nullptr, *ctick = nullptr;
     uint32_t *bw = nullptr, *bg = nullptr, *boff = nullptr, *bww = nullptr, *boffw = nullptr, *tickets = nullptr;
     // device-driven level loop: control block, per-level records, and their pinned host copies
-    LevelCtl *ctl = nullptr, *hctl = nullptr, *hsnap = nullptr;
+    LevelCtl *ctl = nullptr, *hctl = nullptr;
+    HostLoop *hloop = nullptr, *dloop = nullptr;  // device-loop mirror in mapped pinned memory (host / device view)
     LevelRec *lrec = nullptr, *hlrec = nullptr;
     void *tmp = nullptr;
     size_t tmp_bytes = 0;
@@ -407,6 +408,11 @@ struct rmc_ctx {
 #ifdef RMC_WITH_RCCL
     ncclComm_t comm = nullptr;
 #endif
+    // Init's record, fingerprint and invariant verdicts, cached by the first single-GPU Init
+    uint32_t *d_init_rec = nullptr;
+    ulonglong2 *d_init_fp = nullptr;
+    int32_t init_iv[7] = {0};
+    bool init_cached = false;
 
     // device tables
     uint32_t *d_info = nullptr;
@@ -832,7 +838,8 @@ struct rmc_ctx {
         s.ctl = dmalloc<LevelCtl>(1);
         s.lrec = dmalloc<LevelRec>(LREC_CAP);
         HIPCHK(hipHostMalloc((void **)&s.hctl, sizeof(LevelCtl), hipHostMallocDefault));
-        HIPCHK(hipHostMalloc((void **)&s.hsnap, 3 * sizeof(LevelCtl), hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void **)&s.hloop, sizeof(HostLoop), hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer((void **)&s.dloop, s.hloop, 0));
         HIPCHK(hipHostMalloc((void **)&s.hlrec, sizeof(LevelRec) * LREC_CAP, hipHostMallocDefault));
         if (multi) {
             s.perm = dmalloc<uint32_t>(Gcap);
@@ -872,9 +879,9 @@ struct rmc_ctx {
         dfree(s.ctl); dfree(s.lrec);
         if (s.hsum) (void)hipHostFree(s.hsum);
         if (s.hctl) (void)hipHostFree(s.hctl);
-        if (s.hsnap) (void)hipHostFree(s.hsnap);
+        if (s.hloop) (void)hipHostFree(s.hloop);
         if (s.hlrec) (void)hipHostFree(s.hlrec);
-        s.hsum = nullptr; s.hctl = nullptr; s.hsnap = nullptr; s.hlrec = nullptr;
+        s.hsum = nullptr; s.hctl = nullptr; s.hloop = nullptr; s.dloop = nullptr; s.hlrec = nullptr;
         s.hpar.release();
         s.hslot.release();
         if (s.tev) (void)hipEventDestroy(s.tev);
@@ -887,7 +894,7 @@ struct rmc_ctx {
         for (Shard &s : sh) free_shard(s);
         sh.clear();
         dfree(d_info); dfree(d_nat2id); dfree(d_gmsg); dfree(d_perms); dfree(d_seeds);
-        dfree(d_one); dfree(d_out); dfree(d_keys); dfree(d_cnt1); dfree(d_fp1); dfree(d_inv); dfree(d_err1);
+        dfree(d_one); dfree(d_init_rec); dfree(d_init_fp); dfree(d_out); dfree(d_keys); dfree(d_cnt1); dfree(d_fp1); dfree(d_inv); dfree(d_err1);
         dfree(d_flags1); dfree(d_red);
         if (h_red) (void)hipHostFree(h_red);
         h_red = nullptr;
@@ -1279,6 +1286,36 @@ struct rmc_ctx {
         auto t0 = std::chrono::steady_clock::now();
         std::vector<uint32_t> rec = init_record();
         const uint32_t rw = record_words(rec.data());
+        int32_t iv[7];
+        replicated = multi && shard_min > 1;
+        if (!multi && init_cached) {
+            // Init's record, fingerprint and invariant verdicts are fixed by the configuration:
+            // one kernel puts the level in place (no copies, no host round trip)
+            Shard &s = sh[0];
+            std::memcpy(iv, init_iv, sizeof iv);
+            s.level_start = {0};
+            s.cur_wbase = s.nxt_words = 0;
+            launch_init_level(s.R, d_init_rec, rw, s.cur_off, d_init_fp, s.seen(), stream);
+            s.hpar.set(0, ~0ull);
+            s.hslot.set(0, 0);
+            s.tflushed = 1;
+            s.cur_n = 1;
+            s.cur_words = rw;
+            s.T_count = 1;
+        } else {
+            init_full(rec, rw, iv);
+        }
+        total_generated = 1;  // TLC counts the initial state as generated
+        total_distinct = 1;
+        depth = 1;
+        inited = true;
+        status = RMC_OK;
+        return init_verdict(iv, rw, t0, st);
+    }
+
+    // First Init of the run (or every Init of a sharded run): record, fingerprint and invariants
+    // on the device; the single-GPU path caches them for later runs (rmc_reset).
+    void init_full(const std::vector<uint32_t> &rec, uint32_t rw, int32_t *iv) {
         HIPCHK(hipMemcpy(d_one, rec.data(), RECW * 4, hipMemcpyHostToDevice));
         KParams P = base(sh[0]);
         P.front = d_one;
@@ -1286,16 +1323,24 @@ struct rmc_ctx {
         ks.fp_states(P, 1, stream);
         ks.inv_states(P, 1, d_inv, stream);
         uint32_t owner = 0;  // the shard whose seen set takes Init's fingerprint
-        replicated = multi && shard_min > 1;
         if (multi && !replicated) {
             launch_owner_of(d_fp1, (uint32_t)W, d_cnt1, stream);
             owner = d2h(d_cnt1);
             glevel = {0};
             L_shard = 1;
         }
-        int32_t iv[7];
-        HIPCHK(hipMemcpyAsync(iv, d_inv, sizeof iv, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(iv, d_inv, 7 * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
+        if (!multi) {
+            if (!d_init_rec) {
+                d_init_rec = dmalloc<uint32_t>(RECW);
+                d_init_fp = dmalloc<ulonglong2>(1);
+            }
+            HIPCHK(hipMemcpyAsync(d_init_rec, d_one, RECW * 4, hipMemcpyDeviceToDevice, stream));
+            HIPCHK(hipMemcpyAsync(d_init_fp, d_fp1, 16, hipMemcpyDeviceToDevice, stream));
+            std::memcpy(init_iv, iv, sizeof init_iv);
+            init_cached = true;
+        }
         const uint64_t zero = 0;
         for (Shard &s : sh) {
             s.level_start = {0};
@@ -1319,11 +1364,9 @@ struct rmc_ctx {
             if (!multi || replicated) s.T_count = 1;
         }
         HIPCHK(hipStreamSynchronize(stream));
-        total_generated = 1;  // TLC counts the initial state as generated
-        total_distinct = 1;
-        depth = 1;
-        inited = true;
-        status = RMC_OK;
+    }
+
+    int init_verdict(const int32_t *iv, uint32_t rw, std::chrono::steady_clock::time_point t0, rmc_level_stats *st) {
         for (uint32_t o = inv_order; o; o >>= 4) {
             const int b = (int)(o & 15u) - 1;
             if (iv[b] != 1) {
@@ -1655,19 +1698,18 @@ struct rmc_ctx {
         h.epoch = ++s.epoch;
         h.stop = CTL_RUN;
         h.batch = (uint32_t)K;
-        HIPCHK(hipMemcpyAsync(s.ctl, &h, sizeof h, hipMemcpyHostToDevice, stream));
+        __atomic_store_n(&s.hloop->done, 0u, __ATOMIC_RELAXED);
+        __atomic_store_n(&s.hloop->stop, (uint32_t)CTL_RUN, __ATOMIC_RELEASE);
+        launch_set_ctl(s.ctl, h, stream);
         uint64_t *offs[2] = {s.cur_off, s.nxt_off};
         std::vector<size_t> mark(K);
-        // Levels go in groups; after each group a snapshot of the control block is copied back
-        // with an event.  Group g + 2 is enqueued only once group g's snapshot says the loop is
-        // still running, so the device always has a group queued and at most two groups of
-        // no-op launches follow the last level.
-        const int GL = 2, ngroups = (K + GL - 1) / GL;
-        while ((int)gev.size() < 3) {
-            hipEvent_t e;
-            HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            gev.push_back(e);
-        }
+        // Levels go in groups of GL.  finish_level mirrors the loop's progress into pinned host
+        // memory (HostLoop: levels done, stop code -- system-scope stores), so nothing but kernels
+        // sits in the stream: an event or a copy between groups would put a hand-off (6-10 us idle)
+        // between levels.  Group g + 2 is enqueued only once group g has finished with the loop
+        // still running, so the device always has a group queued and at most two groups of no-op
+        // launches follow the last level.
+        const int GL = 1, ngroups = (K + GL - 1) / GL;
         auto enqueue_group = [&](int g) {
             for (int i = g * GL; i < std::min(K, (g + 1) * GL); i++) {
                 mark[i] = evrecs.size();
@@ -1676,31 +1718,45 @@ struct rmc_ctx {
                 Q.noff = offs[(i + 1) & 1];
                 Q.ctl = s.ctl;
                 Q.lrec = s.lrec;
+                Q.hloop = s.dloop;
                 Q.p_begin = 0;
                 Q.p_end = DP;  // grids are sized on the bound; the kernels read the level from ctl
                 timed(PH_HASH, [&] { ks.fused(Q, stream); });
                 timed(PH_DEDUP, [&] { ks.wincount(Q, DP, stream); });
                 timed(PH_MAT, [&] { ks.commit(Q, stream); });
             }
-            HIPCHK(hipMemcpyAsync(&s.hsnap[g % 3], s.ctl, sizeof(LevelCtl), hipMemcpyDeviceToHost, stream));
-            HIPCHK(hipEventRecord(gev[g % 3], stream));
+        };
+        // true once group g has finished (or the loop stopped); a stream error ends the wait
+        auto group_done = [&](int g) {
+            const uint32_t need = (uint32_t)std::min(K, (g + 1) * GL);
+            for (uint32_t spin = 0;; spin++) {
+                if (__atomic_load_n(&s.hloop->stop, __ATOMIC_ACQUIRE) != (uint32_t)CTL_RUN) return false;
+                if (__atomic_load_n(&s.hloop->done, __ATOMIC_ACQUIRE) >= need) return true;
+                if ((spin & 255u) == 255u) {
+                    const hipError_t q = hipStreamQuery(stream);
+                    if (q == hipSuccess) {  // drained: the mirror is final
+                        if (__atomic_load_n(&s.hloop->stop, __ATOMIC_ACQUIRE) != (uint32_t)CTL_RUN) return false;
+                        return __atomic_load_n(&s.hloop->done, __ATOMIC_ACQUIRE) >= need;
+                    }
+                    if (q != hipErrorNotReady) HIPCHK(q);
+                }
+            }
         };
         int enq = 0;
         for (; enq < std::min(2, ngroups); enq++) enqueue_group(enq);
         for (; enq < ngroups; enq++) {
-            HIPCHK(hipEventSynchronize(gev[(enq - 2) % 3]));
-            if (s.hsnap[(enq - 2) % 3].stop != CTL_RUN) break;
+            if (!group_done(enq - 2)) break;
             enqueue_group(enq);
         }
         for (int i = enq * GL; i < K; i++) mark[i] = evrecs.size();
-        HIPCHK(hipMemcpyAsync(s.hctl, s.ctl, sizeof(LevelCtl), hipMemcpyDeviceToHost, stream));
-        HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
         HIPCHK(hipGetLastError());
+        *s.hctl = s.hloop->ctl;
         const LevelCtl c = *s.hctl;
         const int D = (int)c.done_levels;
-        if (D > 0 && D <= K) {
-            HIPCHK(hipMemcpyAsync(s.hlrec, s.lrec, sizeof(LevelRec) * D, hipMemcpyDeviceToHost, stream));
+        if (D > 0 && D <= K) std::memcpy(s.hlrec, s.hloop->rec, sizeof(LevelRec) * D);
+        if (c.stop == CTL_ERROR) {  // the erroring level's summary (error keys, winners) for the host path
+            HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
         }
         if (D > K || c.stop == CTL_RUN) throw Fail(RMC_E_STATE, "device level loop did not stop");
@@ -1757,7 +1813,8 @@ struct rmc_ctx {
         s.epoch = c.epoch;
         s.peak_words = std::max(s.peak_words, s.cur_words);
         if (s.T_count != c.T_count) throw Fail(RMC_E_STATE, "device level loop: seen-set count mismatch");
-        flush_trace(s, c.gid_cur + c.cur_n);
+        // a run that ended without an error never reads its trace (no counterexample): no flush
+        if (!(finished && status == RMC_DONE)) flush_trace(s, c.gid_cur + c.cur_n);
         seconds += el;
         if (c.stop == CTL_ERROR) {
             // the level the loop stopped in is intact: report its error as the host path does
@@ -2467,6 +2524,7 @@ struct rmc_ctx {
     void resume(const char *path) {
         if (multi) throw Fail(RMC_E_ARG, "resume: single-GPU runs only");
         if (inited) throw Fail(RMC_E_STATE, "resume: needs a context not yet initialised (rmc_create or rmc_reset)");
+        HIPCHK(hipStreamSynchronize(stream));  // rmc_reset's clears are stream-ordered, the loads below are not
         FILE *f = std::fopen(path, "rb");
         if (!f) throw Fail(RMC_E_ARG, std::string("resume: cannot read ") + path);
         CkptHeader h{};
@@ -2571,7 +2629,7 @@ struct rmc_ctx {
             s.hpar.n = s.hslot.n = 0;
             s.level_start.clear();
         }
-        HIPCHK(hipStreamSynchronize(stream));
+        // (the clears are stream-ordered before the next run's first kernel: no wait here)
         trace.clear();
         inited = finished = false;
         status = RMC_OK;

@@ -54,6 +54,17 @@ struct LevelCtl {
 };
 struct LevelRec { unsigned long long expanded, generated, new_states, words; };
 constexpr int LREC_CAP = 1024;   // levels per batch at most
+// Device-loop mirror in pinned, mapped host memory: finish_level writes each level's record and
+// the control block here, then the level count and (once the loop stops) the stop code with
+// system-scope stores.  The host polls done / stop while the loop runs -- no event or copy in the
+// stream between levels -- and reads the rest once the stream has drained.
+struct HostLoop {
+    uint32_t done;               // levels committed in this batch
+    uint32_t stop;               // CtlStop; CTL_RUN while the loop runs
+    uint32_t pad_[2];
+    LevelCtl ctl;                // the control block as the last finished level left it
+    LevelRec rec[LREC_CAP];
+};
 constexpr uint32_t WTILE = 1024; // parents per tile of the winner-count scan (1024 tiles at most)
 constexpr int SUM_WORDS = 7;     // chunk summary slot of the new states' record words
 
@@ -126,6 +137,7 @@ struct KParams {
     unsigned long long *sum;   // chunk summary {generated, winners, error keys[ERR_NSLOTS], flags, words}
     LevelCtl *ctl;             // device-driven level loop (nullptr: the host drives the chunk)
     LevelRec *lrec;            // statistics of each level the device loop commits
+    HostLoop *hloop;           // device loop: host-mapped mirror of the loop's progress (finish_level)
     // single-state hook outputs
     uint32_t *out_keys;
     uint32_t *out_count;
@@ -154,6 +166,12 @@ constexpr uint32_t LS_SEEN = 0xFFFFFFFFu, LS_ELECT = 0xFFFFFFFEu, LS_WIN = 0xFFF
 // full-slot table -> (full or compact) table
 void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, Seen dst, hipStream_t s);
 void launch_insert_fps(const ulonglong2 *fp, uint64_t n, Seen seen, hipStream_t s);
+// the control block of a device-driven batch, passed by value (no copy-engine hand-off)
+void launch_set_ctl(LevelCtl *dst, const LevelCtl &v, hipStream_t s);
+// Init's level from the cached Init record and fingerprint: record into the ring at word 0, its
+// offset 0, its fingerprint into the seen set
+void launch_init_level(uint32_t *ring, const uint32_t *rec, uint32_t words, uint64_t *off,
+                       const ulonglong2 *fp, Seen seen, hipStream_t s);
 // out[i] = in[i] - sub (offset arrays rebased to a new level start)
 void launch_rebase(const uint64_t *in, uint64_t n, uint64_t sub, uint64_t *out, hipStream_t s);
 

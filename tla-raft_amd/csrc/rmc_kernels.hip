@@ -550,12 +550,78 @@ struct Wave {
     uint32_t inf[MR];
 };
 
+// ---- message-id lookups of the actions, issued before any branch -------------------------------
+// An action that sends a message looks its id up in nat2id; done inside the divergent action
+// branches, every branch the wave takes paid its own round trip.  These compute the same table
+// indices under the same guards as eval_msg / eval_slot, and the loads go out together for the
+// whole wave (one round trip), their values passed in.
+constexpr uint32_t NAT_NONE = 0xFFFFFFFFu;
+
+// the message lane's lookup (round r): ResponseVote's VoteResp, FollowerAccept/RejectEntry's AppendResp
+template <int N, int V, int MR>
+__device__ __forceinline__ uint32_t msg_nat(const KParams &P, const Wave<N, V, MR> &W, int r, int lane) {
+    using Lo = Layout<N, V>;
+    const uint32_t k = (uint32_t)(r * 64 + lane);
+    if (k >= W.nm) return NAT_NONE;
+    const uint32_t m = W.inf[r];
+    const uint32_t s = mi_dst(m), typ = mi_type(m), mt = mi_term(m), src = mi_src(m);
+    const uint32_t ct = nib(W.c[Lo::W_CT], s), role = nib(W.c[Lo::W_ROLE], s);
+    if (mt != ct || role != FOL) return NAT_NONE;
+    if (typ == VREQ) return nat_vresp(P.d, s, src, mt);
+    if (typ != AREQ) return NAT_NONE;
+    const uint32_t ll = nib(W.c[Lo::W_LL], s), lw = W.lds[Lo::W_LOG + s];
+    const uint32_t pli = mi_x1(m), plt = mi_x2(m), ent = mi_ent(m);
+    const bool match = pli <= ll && plt == lw_term(lw, pli);  // LogMatch tla:271-273
+    return match ? nat_aresp(P.d, s, src, mt, pli + ent, 1) : nat_aresp(P.d, s, src, mt, pli, 0);
+}
+
+// the slot lane's lookups: BecomeCandidate's VoteReqs to the N - 1 peers, LeaderAppendEntry's AppendReq
+template <int N, int V, int MR>
+__device__ __forceinline__ void slot_nats(const KParams &P, const Wave<N, V, MR> &W, int lane, uint32_t (&nat)[N - 1]) {
+    using Lo = Layout<N, V>;
+    using S = Spec<N, V, MR>;
+#pragma unroll
+    for (int i = 0; i < N - 1; i++) nat[i] = NAT_NONE;
+    if (lane >= N * S::SLOTS_PER_SERVER) return;
+    const uint32_t s = (uint32_t)lane / S::SLOTS_PER_SERVER, t = (uint32_t)lane % S::SLOTS_PER_SERVER;
+    const uint32_t role = nib(W.c[Lo::W_ROLE], s), ct = nib(W.c[Lo::W_CT], s), ll = nib(W.c[Lo::W_LL], s);
+    const uint32_t lw = W.lds[Lo::W_LOG + s];
+    if (t == 0) {  // BecomeCandidate's guards (eval_slot)
+        if (!((int)(W.c[Lo::W_MISC] & 15u) < P.E) || !(role == FOL || role == CAN)) return;
+        const uint32_t term = ct + 1, llt = lw_term(lw, ll);
+        // nat[i] = the i-th peer's VoteReq: peer i below s, i + 1 from s on (constant indices only)
+#pragma unroll
+        for (int i = 0; i < N - 1; i++) {
+            const uint32_t p = (uint32_t)i < s ? (uint32_t)i : (uint32_t)i + 1u;
+            nat[i] = nat_vreq(P.d, s, p, term, ll, llt);
+        }
+        return;
+    }
+    if (t >= 2 + (uint32_t)V && t < 2 + (uint32_t)V + (N - 1)) {  // LeaderAppendEntry's guards (eval_slot)
+        const uint32_t q = t - 2 - V;
+        const uint32_t dst = q < s ? q : q + 1;
+        if (role != LEA) return;
+        const uint32_t ni = nib(W.lds[Lo::W_NI + s], dst);
+        if (!(ni <= ll + 1)) return;
+        if ((W.c[Lo::W_PEND] >> (s * N + dst)) & 1u) return;
+        const uint32_t pli = ni - 1, plt = lw_term(lw, pli);
+        const uint32_t ent = ni <= ll ? 1u : 0u;
+        const uint32_t eb = ent ? lw_byte(lw, ni) : 0u;
+        nat[0] = nat_areq(P.d, s, dst, ct, pli, plt, ent, eb & 15u, eb >> 4, nib(W.c[Lo::W_CI], s));
+    }
+}
+
+__device__ __forceinline__ uint32_t nat_lookup(const KParams &P, uint32_t nat) {
+    return nat != NAT_NONE ? (uint32_t)P.t.nat2id[nat] : 0u;
+}
+
 // Evaluate the message lane (round r) -> at most one successor.
 // BFV (the tla:420 variant): ob gets the lane's BecomeFollower successor (tla:190-229) -- a second
 // candidate per message; with BFV false ob is not touched.
 template <int N, int V, int MR, bool BFV = false>
 __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> &W, const uint16_t *ids, int r, int lane,
-                         Succ<N, V, MR> &o, Succ<N, V, MR> &ob, uint32_t &assert_key, uint32_t *ainf) {
+                         Succ<N, V, MR> &o, Succ<N, V, MR> &ob, uint32_t &assert_key, uint32_t *ainf, uint32_t pid) {
+    // pid: the id msg_nat looked up for this lane (the only one its action may send)
     using Lo = Layout<N, V>;
     o.key = KEY_NONE;
     o.nadd = 0;
@@ -620,7 +686,7 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
         if (!(vf == VF_NONE || vf == src)) return;
         const uint32_t llt = lw_term(lw, ll), mlli = mi_x1(m), mllt = mi_x2(m);
         if (!(mllt > llt || (mllt == llt && mlli >= ll))) return;
-        const uint32_t g = P.t.nat2id[nat_vresp(P.d, s, src, mt)];
+        const uint32_t g = pid;  // nat2id[nat_vresp(s, src, mt)]
         if (has_id(ids, W.nm, g)) return;
         o.c[Lo::W_VF] = setnib(o.c[Lo::W_VF], s, src);
         o.add[0] = g; o.nadd = 1;
@@ -639,7 +705,7 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
             const uint32_t mn = lc < nl ? lc : nl;
             const uint32_t ci = nib(W.c[Lo::W_CI], s);
             const uint32_t nci = ci > mn ? ci : mn;
-            const uint32_t resp = P.t.nat2id[nat_aresp(P.d, s, src, mt, pli + ent, 1)];
+            const uint32_t resp = pid;  // nat2id[nat_aresp(s, src, mt, pli + ent, TRUE)]
             o.c[Lo::W_CI] = setnib(o.c[Lo::W_CI], s, nci);
             if (truncated || append_new) {
                 // newLog == SubSeq(logs[s], 1, prevLogIndex) \o entries   (tla:291)
@@ -657,7 +723,7 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
             }
             o.key = slot_key(s, FAE, k);
         } else {
-            const uint32_t resp = P.t.nat2id[nat_aresp(P.d, s, src, mt, pli, 0)];
+            const uint32_t resp = pid;  // nat2id[nat_aresp(s, src, mt, pli, FALSE)]
             if (has_id(ids, W.nm, resp)) return;
             o.add[0] = resp; o.nadd = 1;
             ainf[0] = minfo(ARESP, s, src, mt, pli, 0, 0, 0, 0, 0);
@@ -698,7 +764,8 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
 // Evaluate the non-message slot owned by this lane (last round).
 template <int N, int V, int MR>
 __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR> &W, const uint16_t *ids, int lane,
-                          Succ<N, V, MR> &o, uint32_t *ainf) {
+                          Succ<N, V, MR> &o, uint32_t *ainf, const uint32_t (&sid)[N - 1]) {
+    // sid: the ids slot_nats looked up for this lane
     using Lo = Layout<N, V>;
     using S = Spec<N, V, MR>;
     o.key = KEY_NONE;
@@ -731,7 +798,11 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
 #pragma unroll
         for (int p = 0; p < N; p++) {
             if ((uint32_t)p == s) continue;
-            const uint32_t id = P.t.nat2id[nat_vreq(P.d, s, p, term, ll, llt)];
+            // sid[p < s ? p : p - 1] = nat2id[nat_vreq(s, p, term, ll, llt)] (selects: no runtime index)
+            const int ix = p < (int)s ? p : p - 1;
+            uint32_t id = 0;
+#pragma unroll
+            for (int i = 0; i < N - 1; i++) id = i == ix ? sid[i] : id;
             if (!has_id(ids, W.nm, id)) {
 #pragma unroll
                 for (int a = 0; a < S::NADD; a++) o.add[a] = ((uint32_t)a == na) ? id : o.add[a];
@@ -794,7 +865,7 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
         const uint32_t pli = ni - 1, plt = lw_term(lw, pli);
         const uint32_t ent = ni <= ll ? 1u : 0u;
         const uint32_t eb = ent ? lw_byte(lw, ni) : 0u;
-        const uint32_t id = P.t.nat2id[nat_areq(P.d, s, dst, ct, pli, plt, ent, eb & 15u, eb >> 4, ci)];
+        const uint32_t id = sid[0];  // nat2id[nat_areq(s, dst, ct, pli, plt, ent, eb, ci)]
         if (has_id(ids, W.nm, id)) return;  // m \notin msgs
         o.c[Lo::W_PEND] = W.c[Lo::W_PEND] | (1u << pb);
         o.add[0] = id;
@@ -834,16 +905,23 @@ __device__ __forceinline__ void load_core(const uint32_t *ring, uint64_t start, 
 
 // Load a state record into the wave: uniform core, per-lane message ids, LDS copy of
 // the sorted ids and the per-(src,dst) message hash sums.
+// The whole record in one round trip: lane k holds record word k (and 64 + k); the core is read
+// across lanes, each lane's message ids are shuffled to it by load_parent -- no second dependent
+// load for the ids (words past the record's end are read but never used).  k_expand issues this
+// for its next parent while it works on the current one.
+template <int MR, int RECW_MAX>
+__device__ __forceinline__ void fetch_record(const KParams &P, uint64_t start, int lane, uint32_t &rw0, uint32_t &rw1) {
+    rw0 = lane < RECW_MAX ? ring_word(P.front, start, (uint32_t)lane, P.rcap) : 0u;
+    rw1 = (MR > 1 && 64 + lane < RECW_MAX) ? ring_word(P.front, start, 64u + (uint32_t)lane, P.rcap) : 0u;
+}
+
+// load_parent on a record already fetched (fetch_record)
 template <int N, int V, int MR, bool SUMS>
-__device__ __forceinline__ void load_parent(const KParams &P, uint64_t start, int lane, Wave<N, V, MR> &W, uint16_t *ids,
-                            uint64_t *M0, uint64_t *M1, uint32_t *pcore) {
+__device__ __forceinline__ void load_parent_words(const KParams &P, uint64_t start, uint32_t rw0, uint32_t rw1, int lane,
+                                                  Wave<N, V, MR> &W, uint16_t *ids, uint64_t *M0, uint64_t *M1,
+                                                  uint32_t *pcore) {
     using Lo = Layout<N, V>;
     using S = Spec<N, V, MR>;
-    // the whole record in one round trip: lane k holds record word k (and 64 + k); the core is
-    // read across lanes, each lane's message ids are shuffled to it below -- no second dependent
-    // load for the ids (words past the record's end are read but never used)
-    const uint32_t rw0 = lane < S::RECW_MAX ? ring_word(P.front, start, (uint32_t)lane, P.rcap) : 0u;
-    const uint32_t rw1 = (MR > 1 && 64 + lane < S::RECW_MAX) ? ring_word(P.front, start, 64u + (uint32_t)lane, P.rcap) : 0u;
     uint32_t packed[S::CCW];
 #pragma unroll
     for (int k = 0; k < S::CCW; k++) packed[k] = rdlane(rw0, k);
@@ -893,6 +971,15 @@ __device__ __forceinline__ void load_parent(const KParams &P, uint64_t start, in
         if (lane == 0) pcore[Lo::NW + s] = cnt;
     }
     __syncthreads();
+}
+
+template <int N, int V, int MR, bool SUMS>
+__device__ __forceinline__ void load_parent(const KParams &P, uint64_t start, int lane, Wave<N, V, MR> &W, uint16_t *ids,
+                            uint64_t *M0, uint64_t *M1, uint32_t *pcore) {
+    using S = Spec<N, V, MR>;
+    uint32_t rw0, rw1;
+    fetch_record<MR, S::RECW_MAX>(P, start, lane, rw0, rw1);
+    load_parent_words<N, V, MR, SUMS>(P, start, rw0, rw1, lane, W, ids, M0, M1, pcore);
 }
 
 // hash row of the acting server: parent sums + the messages this successor adds
@@ -992,6 +1079,9 @@ __device__ __forceinline__ bool seen_contains(const Seen &S, ulonglong2 f) {
     uint64_t h = t_index(f, S.mask);
     for (;;) {
         const ulonglong2 e = S.T[h];
+        // both words now: one 16-B load per probe (left alone, the compiler loads y only once x
+        // has matched -- a second dependent round trip on every hit and on every collision)
+        asm volatile("" ::"v"(e.x), "v"(e.y));
         if (e.x == 0ull) return false;
         if (e.x == f.x && e.y == f.y) return true;
         h = (h + 1) & S.mask;
@@ -1167,17 +1257,40 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? 4 : ((BFV && N >=
         }
     }
     PHASE_DECL
-    for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
+    // software pipeline over the block's parents: the next parent's record offset goes out at the
+    // top of an iteration and its record once this one's actions are evaluated, so a block's
+    // second and later parents start with their record in registers
+    uint64_t p = P.p_begin + blockIdx.x, nstart = 0;
+    uint32_t nrw0 = 0, nrw1 = 0;
+    if (p < P.p_end) {
+        nstart = rec_start<S::RECW_MAX>(P, p);
+        fetch_record<MR, S::RECW_MAX>(P, nstart, lane, nrw0, nrw1);
+    }
+    for (; p < P.p_end; p += gridDim.x) {
+        const uint64_t start = nstart;
+        const bool more = p + gridDim.x < P.p_end;
+        if (more) nstart = rec_start<S::RECW_MAX>(P, p + gridDim.x);
         Wave<N, V, MR> W;
-        load_parent<N, V, MR, SUMS>(P, rec_start<S::RECW_MAX>(P, p), lane, W, ids, M0, M1, pcore);
+        load_parent_words<N, V, MR, SUMS>(P, start, nrw0, nrw1, lane, W, ids, M0, M1, pcore);
         PHASE(0);
         Succ<N, V, MR> cand[NC];
         uint32_t akey = KEY_NONE;
+        // every id lookup of the actions in one round trip (msg_nat / slot_nats)
+        uint32_t mid[MR], sid[N - 1];
+        {
+            uint32_t snat[N - 1];
+            slot_nats<N, V, MR>(P, W, lane, snat);
+#pragma unroll
+            for (int r = 0; r < MR; r++) mid[r] = nat_lookup(P, msg_nat<N, V, MR>(P, W, r, lane));
+#pragma unroll
+            for (int i = 0; i < N - 1; i++) sid[i] = nat_lookup(P, snat[i]);
+        }
 #pragma unroll
         for (int r = 0; r < MR; r++)
             eval_msg<N, V, MR, BFV>(P, W, ids, r, lane, cand[r], cand[BFV ? MR + 1 + r : r], akey,
-                                    &sAinf[(r * 64 + lane) * S::NADD]);
-        eval_slot<N, V, MR>(P, W, ids, lane, cand[MR], &sAinf[(MR * 64 + lane) * S::NADD]);
+                                    &sAinf[(r * 64 + lane) * S::NADD], mid[r]);
+        eval_slot<N, V, MR>(P, W, ids, lane, cand[MR], &sAinf[(MR * 64 + lane) * S::NADD], sid);
+        if (more) fetch_record<MR, S::RECW_MAX>(P, nstart, lane, nrw0, nrw1);
         PHASE(1);
         // rank of every enabled successor in TLC order
         uint64_t en[NC];
@@ -1570,6 +1683,16 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
             P.wpos[pl] = x;
             P.wposw[pl] = xd;
         }
+        if (ntiles == 1) {  // one tile (small levels): its totals are the chunk's, no arrival round trips
+            if (threadIdx.x == 0) {
+                P.boff[0] = 0u;
+                P.boffw[0] = 0u;
+                P.sum[0] = gt;
+                P.sum[1] = wt;
+                P.sum[SUM_WORDS] = dt;
+            }
+            return;
+        }
         if (threadIdx.x == 0) {
             // write-through (sc1) stores: the last block reads them with sc1 loads, no fences
             __hip_atomic_store(&P.bw[tile], wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1634,14 +1757,21 @@ __device__ void finish_level(const KParams &P) {
     LevelCtl c = *P.ctl;
     if (bad) {  // the host reports the error from this level's buffers
         P.ctl->stop = CTL_ERROR;
+        if (P.hloop) {
+            c.stop = CTL_ERROR;
+            P.hloop->ctl = c;
+            __hip_atomic_store(&P.hloop->stop, (uint32_t)CTL_ERROR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         return;
     }
     if (c.done_levels < (uint32_t)LREC_CAP) {
-        LevelRec &r = P.lrec[c.done_levels];
+        LevelRec r;
         r.expanded = c.cur_n;
         r.generated = G;
         r.new_states = Wn;
         r.words = Ww;
+        P.lrec[c.done_levels] = r;
+        if (P.hloop) P.hloop->rec[c.done_levels] = r;
     }
     c.done_levels++;
     c.gid_cur += c.cur_n;
@@ -1662,6 +1792,11 @@ __device__ void finish_level(const KParams &P) {
              2 * (c.T_count + Gub) > c.T_cap)
         c.stop = CTL_HOST;  // the next level is not known to fit the buffers: the host grows them
     *P.ctl = c;
+    if (P.hloop) {  // the control block only when the loop stops: the host reads it after the drain
+        if (c.stop != CTL_RUN) P.hloop->ctl = c;
+        __hip_atomic_store(&P.hloop->done, c.done_levels, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (c.stop != CTL_RUN) __hip_atomic_store(&P.hloop->stop, c.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // True in the last one-wave block of the commit pass to get here, among the nb blocks that had a
@@ -1712,12 +1847,15 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
         const uint32_t bo = P.boff[pl / WTILE], wp = P.wpos[pl], t = P.cnt[pl];
         const uint32_t bow = P.boffw[pl / WTILE], wpw = P.wposw[pl];
         const uint32_t g0 = lane < MX ? P.lslot[pl * (uint64_t)MX + lane] : LS_SEEN;
+        const uint64_t start = rec_start<S::RECW_MAX>(P, p);  // in bounds for every p of the level
         if (!wc) continue;
-        const uint64_t start = rec_start<S::RECW_MAX>(P, p);
-        // the parent's record in one round trip (as load_parent)
+        // the parent's record in one round trip (as load_parent), and with it the election words
+        // of the first 64 slots (their indices came with the first round trip)
         const uint32_t rw0 = lane < S::RECW_MAX ? ring_word(P.front, start, (uint32_t)lane, P.rcap) : 0u;
         const uint32_t rw1 =
             (MR > 1 && 64 + lane < S::RECW_MAX) ? ring_word(P.front, start, 64u + (uint32_t)lane, P.rcap) : 0u;
+        // (slots past the parent's t successors hold a stale lslot from an earlier chunk: never an index)
+        const unsigned long long L0 = (!P.route && (uint32_t)lane < t && g0 < LS_ELECT) ? P.L[g0] : 0ull;
         uint32_t pc[Lo::NW], ppk[S::CCW];
 #pragma unroll
         for (int k = 0; k < S::CCW; k++) ppk[k] = rdlane(rw0, k);
@@ -1743,7 +1881,7 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
             bool win = false;
             if (r < t) {
                 const uint32_t g = r0 == 0 ? g0 : P.lslot[q];
-                win = P.route ? g == LS_WIN : (g < LS_ELECT && elect_q(P.L[g]) == (uint32_t)q);
+                win = P.route ? g == LS_WIN : (g < LS_ELECT && elect_q(r0 == 0 ? L0 : P.L[g]) == (uint32_t)q);
             }
             const uint64_t m = __ballot(win);
             if (!m) continue;
@@ -1904,6 +2042,26 @@ static inline unsigned grid256(uint64_t n) {
 void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, Seen dst, hipStream_t s) {
     hipLaunchKernelGGL(k_rehash, dim3(grid256(old_cap)), dim3(256), 0, s, Told, old_cap, dst);
 }
+__global__ __launch_bounds__(64) void k_set_ctl(LevelCtl *dst, LevelCtl v) {
+    if (threadIdx.x == 0) *dst = v;
+}
+void launch_set_ctl(LevelCtl *dst, const LevelCtl &v, hipStream_t s) {
+    hipLaunchKernelGGL(k_set_ctl, dim3(1), dim3(64), 0, s, dst, v);
+}
+
+__global__ __launch_bounds__(64) void k_init_level(uint32_t *ring, const uint32_t *rec, uint32_t words,
+                                                   uint64_t *off, const ulonglong2 *fp, Seen seen) {
+    for (uint32_t i = threadIdx.x; i < words; i += 64) ring[i] = rec[i];
+    if (threadIdx.x == 0) {
+        off[0] = 0;
+        seen_insert(seen, fp[0]);
+    }
+}
+void launch_init_level(uint32_t *ring, const uint32_t *rec, uint32_t words, uint64_t *off,
+                       const ulonglong2 *fp, Seen seen, hipStream_t s) {
+    hipLaunchKernelGGL(k_init_level, dim3(1), dim3(64), 0, s, ring, rec, words, off, fp, seen);
+}
+
 void launch_insert_fps(const ulonglong2 *fp, uint64_t n, Seen seen, hipStream_t s) {
     hipLaunchKernelGGL(k_insert, dim3(grid256(n)), dim3(256), 0, s, fp, n, seen);
 }

@@ -10,6 +10,7 @@ no CPU fallback -- ``ModelChecker`` raises if the library or the GPU is missing.
 from __future__ import annotations
 
 import ctypes
+from collections.abc import Sequence as _SeqABC
 import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -313,6 +314,37 @@ class LevelStats:
     new_bytes: int = 0
 
 
+class _LazyLevels(_SeqABC):
+    """Per-level statistics of one run, converted to LevelStats on first access (a run's levels come
+    back from the library as one array; building dozens of Python objects per exhaustion would cost
+    more host time than a small configuration's whole GPU run)."""
+
+    def __init__(self, raw, n: int):
+        self._raw = (_LevelStats * n)()
+        ctypes.memmove(self._raw, raw, ctypes.sizeof(_LevelStats) * n)
+        self._cache: List[Optional[LevelStats]] = [None] * n
+
+    def __len__(self):
+        return len(self._cache)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        if self._cache[i] is None:
+            self._cache[i] = ModelChecker._stats(self._raw[i])
+        return self._cache[i]
+
+    def __eq__(self, other):
+        return list(self) == list(other)
+
+    def __repr__(self):
+        return repr(list(self))
+
+
 @dataclass
 class Result:
     status: str
@@ -362,6 +394,11 @@ class ModelChecker:
     def __exit__(self, *a):
         self.close()
 
+    def _levels_list(self) -> list:
+        if not isinstance(self.levels, list):
+            self.levels = list(self.levels)
+        return self.levels
+
     def _check(self, rc: int) -> int:
         if rc < 0:
             raise RmcError(f"{ERRORS.get(rc, rc)}: {self.lib.rmc_last_error(self.h).decode()}")
@@ -378,7 +415,7 @@ class ModelChecker:
         self._check(self.lib.rmc_init(self.h, ctypes.byref(st)))
         self._inited = True
         ls = self._stats(st)
-        self.levels.append(ls)
+        self._levels_list().append(ls)
         return ls
 
     def reset(self) -> None:
@@ -400,7 +437,7 @@ class ModelChecker:
         st = _LevelStats()
         self._check(self.lib.rmc_step(self.h, ctypes.byref(st)))
         ls = self._stats(st)
-        self.levels.append(ls)
+        self._levels_list().append(ls)
         return ls
 
     def set_timing(self, phases: int) -> None:
@@ -413,17 +450,19 @@ class ModelChecker:
         n = ctypes.c_uint32()
         self._check(self.lib.rmc_steps(self.h, buf, cap, ctypes.byref(n)))
         out = [self._stats(buf[i]) for i in range(n.value)]
-        self.levels.extend(out)
+        self._levels_list().extend(out)
         return out
 
     def run(self) -> Result:
         """Exhaust the state space (or stop at the first error) inside the library."""
         cap = 4096
-        buf = (_LevelStats * cap)()
+        if getattr(self, "_runbuf", None) is None:
+            self._runbuf = (_LevelStats * cap)()  # reused by every run of this checker
         n = ctypes.c_uint32()
-        self._check(self.lib.rmc_run_levels(self.h, buf, cap, ctypes.byref(n), None))
+        self._check(self.lib.rmc_run_levels(self.h, self._runbuf, cap, ctypes.byref(n), None))
         self._inited = True
-        self.levels.extend(self._stats(buf[i]) for i in range(n.value))
+        lazy = _LazyLevels(self._runbuf, n.value)
+        self.levels = lazy if not self.levels else list(self.levels) + list(lazy)
         return self.result()
 
     def result(self) -> Result:
@@ -431,7 +470,8 @@ class ModelChecker:
         self._check(self.lib.rmc_get_result(self.h, ctypes.byref(r)))
         return Result(STATUS_NAMES.get(r.status, str(r.status)), r.depth, r.generated, r.distinct, r.queue,
                       INVARIANT_BY_BIT[r.violated] if r.violated >= 0 else None, r.trace_len, r.seconds,
-                      list(self.levels), r.seen_slots, r.seen_slot_bytes, r.frontier_ring_bytes,
+                      self.levels if isinstance(self.levels, _LazyLevels) else list(self.levels), r.seen_slots,
+                      r.seen_slot_bytes, r.frontier_ring_bytes,
                       r.frontier_peak_bytes)
 
     def trace(self) -> List[Tuple[Optional[Tuple[int, int, int]], dict]]:

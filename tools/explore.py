@@ -36,14 +36,22 @@ print(f"create {time.time() - t0:.2f}s", flush=True)
 ls = mc.init()
 t1 = time.time()
 rows = []
+stopped = ""
 while ls.status == "ok" and time.time() - t1 < a.budget:
-    ls = mc.step()
+    try:
+        ls = mc.step()
+    except raftmc.RmcError as e:  # capacity: report how far one GPU got
+        stopped = str(e)
+        print(f"STOPPED at level {ls.level + 1}: {e}", flush=True)
+        break
     el = time.time() - t1
     ms = " ".join(f"{x:.1f}" for x in ls.kernel_ms)
     print(f"L{ls.level:3d} F={ls.expanded:>11d} G={ls.generated:>12d} N={ls.new_states:>11d} "
           f"tot={ls.total_distinct:>12d} {ls.seconds * 1e3:9.1f}ms [{ms}] el={el:.1f}s "
           f"{ls.total_distinct / el:.3e} ds/s rec={ls.new_bytes / max(1, ls.new_states):.1f}B", flush=True)
     rows.append(ls.__dict__)
+if stopped:
+    sys.exit(0)
 r = mc.result()
 print("RESULT", r.status, "generated", r.generated, "distinct", r.distinct, "depth", r.depth,
       "seconds", round(r.seconds, 3), "seen_slots", r.seen_slots, "x", r.seen_slot_bytes, "B; ring",

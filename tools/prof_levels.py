@@ -56,10 +56,10 @@ def per_level(runs, depth):
 def main(path, depth=37, levels=False):
     rows = [r for r in csv.DictReader(open(path)) if "rmc::k_" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    # every exhaustion starts by fingerprinting Init (k_fp_states): that launch splits the runs
+    # every exhaustion starts with Init's level (k_fp_states the first time, k_init_level after): that launch splits the runs
     runs, cur = [], []
     for r in rows:
-        if "k_fp_states" in r["Kernel_Name"] and cur:
+        if ("k_fp_states" in r["Kernel_Name"] or "k_init_level" in r["Kernel_Name"]) and cur:
             runs.append(cur)
             cur = []
         cur.append(r)
