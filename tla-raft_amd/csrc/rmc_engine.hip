@@ -1703,10 +1703,10 @@ struct rmc_ctx {
         launch_set_ctl(s.ctl, h, stream);
         uint64_t *offs[2] = {s.cur_off, s.nxt_off};
         std::vector<size_t> mark(K);
-        // Levels go in groups of GL.  finish_level mirrors the loop's progress into pinned host
-        // memory (HostLoop: levels done, stop code -- system-scope stores), so nothing but kernels
-        // sits in the stream: an event or a copy between groups would put a hand-off (6-10 us idle)
-        // between levels.  Group g + 2 is enqueued only once group g has finished with the loop
+        // Levels go in groups of GL.  The loop's progress is mirrored into pinned host memory
+        // (HostLoop, system-scope stores): each level's expansion reports the levels done before it
+        // as it starts, finish_level reports the stop -- so nothing but kernels sits in the stream
+        // (an event or a copy between groups would be a hand-off of 6-10 us idle).  Group g + 2 is enqueued only once group g has finished with the loop
         // still running, so the device always has a group queued and at most two groups of no-op
         // launches follow the last level.
         const int GL = 1, ngroups = (K + GL - 1) / GL;

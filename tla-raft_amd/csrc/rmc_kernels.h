@@ -137,7 +137,8 @@ struct KParams {
     unsigned long long *sum;   // chunk summary {generated, winners, error keys[ERR_NSLOTS], flags, words}
     LevelCtl *ctl;             // device-driven level loop (nullptr: the host drives the chunk)
     LevelRec *lrec;            // statistics of each level the device loop commits
-    HostLoop *hloop;           // device loop: host-mapped mirror of the loop's progress (finish_level)
+    HostLoop *hloop;           // device loop: host-mapped mirror of the loop's progress (k_expand, finish_level)
+    uint32_t done_levels;      // device loop: levels of the batch committed before this one (level_args)
     // single-state hook outputs
     uint32_t *out_keys;
     uint32_t *out_count;

@@ -91,6 +91,7 @@ __device__ __forceinline__ bool level_args(KParams &P) {
     if (!P.ctl) return true;
     const LevelCtl *c = P.ctl;
     if (c->stop != CTL_RUN) return false;
+    P.done_levels = c->done_levels;
     P.p_begin = 0;
     P.p_end = c->cur_n;
     P.gid_parent_base = c->gid_cur;
@@ -1240,6 +1241,10 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? 4 : ((BFV && N >=
     __shared__ ulonglong2 sBest[MAXG];
     __shared__ uint32_t sAinf[(MR + 1) * 64 * S::NADD];  // info words of the messages each candidate adds
     if (MODE == M_FUSED && !level_args(P)) return;
+    // device loop: the levels committed so far go to the host as this level starts (the write to
+    // host memory completes in the shadow of the expansion; see finish_level)
+    if (MODE == M_FUSED && P.hloop && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(&P.hloop->done, P.done_levels, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // device-loop grids are sized on a bound of the level: blocks past it leave before the LDS setup
     if (MODE == M_FUSED && P.p_begin + blockIdx.x >= P.p_end) return;
     const int lane = threadIdx.x;
@@ -1260,16 +1265,19 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? 4 : ((BFV && N >=
     // software pipeline over the block's parents: the next parent's record offset goes out at the
     // top of an iteration and its record once this one's actions are evaluated, so a block's
     // second and later parents start with their record in registers
-    uint64_t p = P.p_begin + blockIdx.x, nstart = 0;
+    // (offsets two parents ahead: an offset has a whole iteration to land before its record is fetched)
+    uint64_t p = P.p_begin + blockIdx.x, nstart = 0, nnstart = 0;
     uint32_t nrw0 = 0, nrw1 = 0;
     if (p < P.p_end) {
         nstart = rec_start<S::RECW_MAX>(P, p);
         fetch_record<MR, S::RECW_MAX>(P, nstart, lane, nrw0, nrw1);
+        if (p + gridDim.x < P.p_end) nnstart = rec_start<S::RECW_MAX>(P, p + gridDim.x);
     }
     for (; p < P.p_end; p += gridDim.x) {
         const uint64_t start = nstart;
         const bool more = p + gridDim.x < P.p_end;
-        if (more) nstart = rec_start<S::RECW_MAX>(P, p + gridDim.x);
+        nstart = nnstart;
+        if (p + 2ull * gridDim.x < P.p_end) nnstart = rec_start<S::RECW_MAX>(P, p + 2ull * gridDim.x);
         Wave<N, V, MR> W;
         load_parent_words<N, V, MR, SUMS>(P, start, nrw0, nrw1, lane, W, ids, M0, M1, pcore);
         PHASE(0);
@@ -1571,6 +1579,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? 4 : ((BFV && N >=
             }
         }
         PHASE(5);
+        asm volatile("" ::"v"(nnstart));  // the offset two parents ahead is in by now: keep its load up top
         if (MODE == M_FUSED) continue;
         // SINGLE: every successor, in TLC order
 #pragma unroll
@@ -1792,10 +1801,13 @@ __device__ void finish_level(const KParams &P) {
              2 * (c.T_count + Gub) > c.T_cap)
         c.stop = CTL_HOST;  // the next level is not known to fit the buffers: the host grows them
     *P.ctl = c;
-    if (P.hloop) {  // the control block only when the loop stops: the host reads it after the drain
-        if (c.stop != CTL_RUN) P.hloop->ctl = c;
+    // The loop's stop goes to the host here, with the control block (read after the drain); the
+    // running loop's progress is reported by the next level's expansion as it starts (k_expand):
+    // a write to host memory at the end of this kernel would hold the next launch ~5.6 us.
+    if (P.hloop && c.stop != CTL_RUN) {
+        P.hloop->ctl = c;
         __hip_atomic_store(&P.hloop->done, c.done_levels, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (c.stop != CTL_RUN) __hip_atomic_store(&P.hloop->stop, c.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&P.hloop->stop, c.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1843,12 +1855,17 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
         // every load of the parent that depends on no other load goes out at once: its winner
         // count, offsets, successor count and first 64 election slots (read ahead of knowing
         // whether they are needed; all in bounds)
+        // (commit always reads a ring level: foff is set; in bounds for every p of the level)
+        const uint64_t foffp = P.foff[p];
+        const uint32_t g0 = lane < MX ? P.lslot[pl * (uint64_t)MX + lane] : LS_SEEN;
         const uint32_t wc = P.wcnt[pl];
         const uint32_t bo = P.boff[pl / WTILE], wp = P.wpos[pl], t = P.cnt[pl];
         const uint32_t bow = P.boffw[pl / WTILE], wpw = P.wposw[pl];
-        const uint32_t g0 = lane < MX ? P.lslot[pl * (uint64_t)MX + lane] : LS_SEEN;
-        const uint64_t start = rec_start<S::RECW_MAX>(P, p);  // in bounds for every p of the level
+        // one wait for all of them: otherwise the compiler waits for the counts before it issues
+        // the offset load (or sinks that load behind the branch below) -- a second round trip
+        asm volatile("" ::"v"(foffp), "v"(g0), "v"(wc), "v"(bo), "v"(wp), "v"(t), "v"(bow), "v"(wpw));
         if (!wc) continue;
+        const uint64_t start = ring_wrap(P.fbase + foffp, P.rcap);
         // the parent's record in one round trip (as load_parent), and with it the election words
         // of the first 64 slots (their indices came with the first round trip)
         const uint32_t rw0 = lane < S::RECW_MAX ? ring_word(P.front, start, (uint32_t)lane, P.rcap) : 0u;
@@ -1856,6 +1873,16 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
             (MR > 1 && 64 + lane < S::RECW_MAX) ? ring_word(P.front, start, 64u + (uint32_t)lane, P.rcap) : 0u;
         // (slots past the parent's t successors hold a stale lslot from an earlier chunk: never an index)
         const unsigned long long L0 = (!P.route && (uint32_t)lane < t && g0 < LS_ELECT) ? P.L[g0] : 0ull;
+        // and the staged rows of the first 64 slots that may win (new fingerprints; in a sharded
+        // round the owner's verdict is already known): a speculative read instead of a third round
+        // trip once the election words are in
+        uint4 xa = make_uint4(0u, 0u, 0u, 0u), xb = xa, xc = xa;
+        if ((uint32_t)lane < t && (P.route ? g0 == LS_WIN : g0 < LS_ELECT)) {
+            const uint4 *src = P.score + (pl * (uint64_t)MX + (uint32_t)lane) * (uint64_t)S::SW4;
+            xa = src[0];
+            xb = src[1];
+            if (S::SW4 > 2) xc = src[2];
+        }
         uint32_t pc[Lo::NW], ppk[S::CCW];
 #pragma unroll
         for (int k = 0; k < S::CCW; k++) ppk[k] = rdlane(rw0, k);
@@ -1875,6 +1902,8 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
         const uint64_t wd0 = P.next_wbase + bow + wpw;
         uint32_t done = 0;
         uint64_t done_w = 0;
+        asm volatile("" ::"v"(xa.x), "v"(xa.y), "v"(xa.z), "v"(xa.w), "v"(xb.x), "v"(xb.y), "v"(xb.z), "v"(xb.w),
+                     "v"(xc.x));  // issued with the record, not sunk into the winner branch
         for (uint32_t r0 = 0; r0 < t; r0 += 64) {
             const uint32_t r = r0 + (uint32_t)lane;
             const uint64_t q = pl * (uint64_t)MX + r;
@@ -1891,10 +1920,16 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
 #pragma unroll
             for (int w = 0; w < S::CCW; w++) pk[w] = 0u;
             if (win) {
-                const uint4 *src = P.score + q * (uint64_t)S::SW4;
-                sa = src[0];
-                sb = src[1];
-                if (S::SW4 > 2) sc = src[2];
+                if (r0 == 0) {
+                    sa = xa;
+                    sb = xb;
+                    sc = xc;
+                } else {
+                    const uint4 *src = P.score + q * (uint64_t)S::SW4;
+                    sa = src[0];
+                    sb = src[1];
+                    if (S::SW4 > 2) sc = src[2];
+                }
                 uint32_t c[Lo::NW];
                 unstage_core<N, V>(pc, sa, sb, c);
                 encode_core<N, V>(c, pk);
