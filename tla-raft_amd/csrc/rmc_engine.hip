@@ -1425,6 +1425,10 @@ struct rmc_ctx {
         hoff[F] = s0.cur_words;
         uint32_t *src = s0.R;
         const uint64_t src_cap = s0.rcap, src_wbase = s0.cur_wbase;
+        // A ring already at its budget (the seen set went compact during the replicated levels)
+        // is rebuilt at the budget once the old ring is gone: allocating the new one at the old
+        // one's size first would need the budget twice.
+        const bool was_fixed = s0.ring_fixed;
         uint64_t *src_off = s0.cur_off;
         std::vector<uint32_t *> old_rings;
         for (size_t ti = sh.size(); ti-- > 0;) {  // shard 0 last: its trace entries move in place
@@ -1436,7 +1440,7 @@ struct rmc_ctx {
                 n += hi - lo;
                 words += hoff[hi] - hoff[lo];
             }
-            const uint64_t cap = std::max<uint64_t>(std::max<uint64_t>(words + words / 2, 1ull << 14), &t == &s0 ? s0.rcap : 0);
+            const uint64_t cap = std::max<uint64_t>(words + words / 2, 1ull << 14);
             uint32_t *nr = dmalloc<uint32_t>(cap);
             uint64_t *noff = dmalloc<uint64_t>(std::max<uint64_t>(n + n / 2, 1 << 16));
             uint64_t at = 0, wat = 0;
@@ -1502,6 +1506,8 @@ struct rmc_ctx {
         for (uint32_t *r : old_rings) dfree(r);
         dfree(old_off_);
         old_off_ = nullptr;
+        if (was_fixed)
+            for (Shard &t : sh) fix_ring(t, sh.size());
         replicated = false;
     }
     uint64_t *old_off_ = nullptr;
@@ -1709,7 +1715,11 @@ struct rmc_ctx {
         // (an event or a copy between groups would be a hand-off of 6-10 us idle).  Group g + 2 is enqueued only once group g has finished with the loop
         // still running, so the device always has a group queued and at most two groups of no-op
         // launches follow the last level.
-        const int GL = 1, ngroups = (K + GL - 1) / GL;
+        // GL = 2: the first kernel of every group submitted while the loop runs starts ~5.8 us
+        // late (measured with reports at either end of a level and with a stream query right after
+        // each submission); two levels per group halve that against one, and the no-op tail after
+        // the last level stays at most two groups
+        const int GL = 2, ngroups = (K + GL - 1) / GL;
         auto enqueue_group = [&](int g) {
             for (int i = g * GL; i < std::min(K, (g + 1) * GL); i++) {
                 mark[i] = evrecs.size();

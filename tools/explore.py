@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one configuration level by level on the GPU and print TLC-style progress per level.
 
-usage: explore.py N V E R [--budget SECONDS] [--seeded] [--chunk G] [--seenlog2 K]"""
+usage: explore.py N V E R [--budget SECONDS] [--seeded] [--chunk G] [--seenlog2 K] [--rccl1 [--shard-min K]]"""
 import argparse
 import json
 import os
@@ -25,11 +25,15 @@ ap.add_argument("--json", default="")
 ap.add_argument("--compact-log2", type=int, default=0)
 ap.add_argument("--seen-mem-gb", type=float, default=0)
 ap.add_argument("--frontier-mem-gb", type=float, default=0)
+ap.add_argument("--rccl1", action="store_true", help="the sharded protocol on a one-rank RCCL communicator")
+ap.add_argument("--shard-min", type=int, default=0)
 a = ap.parse_args()
+extra = dict(world_size=1, rank=0, comm_unique_id=raftmc.comm_unique_id()) if a.rccl1 else {}
 cfg = raftmc.ModelConfig(n_servers=a.n, n_vals=a.V, max_election=a.E, max_restart=a.R,
                          spec_variant=raftmc.SPEC_SEEDED if a.seeded else raftmc.SPEC_RAFT,
                          chunk_successors=a.chunk, seen_log2=a.seenlog2, compact_log2=a.compact_log2,
-                         seen_mem_bytes=int(a.seen_mem_gb * 2**30), frontier_mem_bytes=int(a.frontier_mem_gb * 2**30))
+                         seen_mem_bytes=int(a.seen_mem_gb * 2**30), frontier_mem_bytes=int(a.frontier_mem_gb * 2**30),
+                         shard_min_states=a.shard_min, **extra)
 t0 = time.time()
 mc = raftmc.ModelChecker(cfg)
 print(f"create {time.time() - t0:.2f}s", flush=True)
