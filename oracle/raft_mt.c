@@ -180,9 +180,27 @@ static void run_phase(worker_t *W, int T, void *(*fn)(void *)) {
     for (int t = 1; t < T; t++) pthread_join(th[t], NULL);
 }
 
+static int mt_bfs(int n, int V, int E, int R, int threads, uint64_t max_states, uint64_t *lv, uint64_t *lg,
+                  int lcap, uint64_t *distinct, uint64_t *generated, int *depth);
+
 /* Exhaust (n, V, E, R) with `threads` threads; returns 0 done, 1 invariant violated, -1 error.
  * out: distinct, generated, depth. */
 int orc_mt_run(int n, int V, int E, int R, int threads, uint64_t *distinct, uint64_t *generated, int *depth) {
+    return mt_bfs(n, V, E, R, threads, 0, NULL, NULL, 0, distinct, generated, depth);
+}
+
+/* Prefix levels (tests/golden/make_golden_prefix.py --mt): the same BFS, stopped at the first
+ * level boundary where `max_states` distinct states are reached.  Being level-synchronous, every
+ * level it reports is complete: lv[k] = distinct states of level k+1 (k < depth), lg[k] = successors
+ * generated expanding level k+1 (k < depth - 1, or k < depth when the run exhausted).
+ * Returns 0 exhausted, 2 stopped at max_states, 1 invariant violated. */
+int orc_mt_levels(int n, int V, int E, int R, int threads, uint64_t max_states, uint64_t *lv, uint64_t *lg, int lcap,
+                  uint64_t *distinct, uint64_t *generated, int *depth) {
+    return mt_bfs(n, V, E, R, threads, max_states, lv, lg, lcap, distinct, generated, depth);
+}
+
+static int mt_bfs(int n, int V, int E, int R, int threads, uint64_t max_states, uint64_t *lv, uint64_t *lg,
+                  int lcap, uint64_t *distinct, uint64_t *generated, int *depth) {
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
     ocfg_t c = {n, V, E, R, 0, 0, 1u << I_LHACE, 0, 0, 0, 0};
@@ -199,6 +217,7 @@ int orc_mt_run(int n, int V, int E, int R, int threads, uint64_t *distinct, uint
     ar_push(&cur, s0);
     uint64_t dist = 1, gen = 1, seen_n = 1;
     int dep = 1, verdict = 0;
+    if (lcap > 0) lv[0] = 1;
     worker_t *W = (worker_t *)calloc((size_t)threads, sizeof(worker_t));
     lslot_t *lt = NULL;
     uint64_t lt_cap = 0;
@@ -214,7 +233,10 @@ int orc_mt_run(int n, int V, int E, int R, int threads, uint64_t *distinct, uint
         }
         run_phase(W, T, phase_expand);
         uint64_t ncand = 0;
-        for (int t = 0; t < T; t++) { ncand += W[t].ncand; gen += W[t].generated; }
+        uint64_t lgen = 0;
+        for (int t = 0; t < T; t++) { ncand += W[t].ncand; lgen += W[t].generated; }
+        gen += lgen;
+        if (dep - 1 < lcap) lg[dep - 1] = lgen;
         uint64_t need = 1;
         while (need < 2 * ncand + 2) need <<= 1;
         if (need > lt_cap) { free(lt); lt_cap = need; lt = (lslot_t *)malloc(lt_cap * sizeof(lslot_t)); }
@@ -248,8 +270,10 @@ int orc_mt_run(int n, int V, int E, int R, int threads, uint64_t *distinct, uint
         dist += nw;
         ar_free(&cur);
         cur = nxt;
+        if (nw && dep < lcap) lv[dep] = nw;
         if (nw) dep++;
         if (verdict) break;
+        if (max_states && dist >= max_states && cur.n > 0) { verdict = 2; break; }
     }
     for (int t = 0; t < threads; t++) { ar_free(&W[t].cand); ar_free(&W[t].win); free(W[t].ch); free(W[t].ckey); }
     free(W); free(lt); free(seen); free(s0); free(P); ar_free(&cur);

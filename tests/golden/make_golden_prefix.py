@@ -11,8 +11,13 @@ oracle until `max_states` distinct states and keep only the levels it completed:
 The GPU test (tests/test_gpu.py::test_prefix_levels_match_c_oracle) runs the same configuration
 level by level and compares those prefixes exactly.
 
-usage: python tests/golden/make_golden_prefix.py MAX_STATES n V E R [n V E R ...]
+usage: python tests/golden/make_golden_prefix.py [--mt THREADS] MAX_STATES n V E R [n V E R ...]
 writes tests/golden/levels_prefix.json (merged with what is there)
+
+--mt runs oracle/raft_mt.c's level-synchronous BFS (the same restatement, same first-wins
+semantics) on THREADS host threads and stops at the first level boundary past MAX_STATES, so
+every reported level is complete (used for the 5-server configs[3], whose exact canonical form
+costs 120 permutations per successor).
 """
 import ctypes
 import json
@@ -51,13 +56,40 @@ def run_prefix(n, V, E, Rr, max_states):
             "oracle_seconds": round(dt, 1), "source": "c", "invariants": ["Inv"], "check_deadlock": False}
 
 
+def run_prefix_mt(n, V, E, Rr, max_states, threads):
+    lib = ctypes.CDLL(os.path.join(HERE, "..", "..", "oracle", "build", "libraft_mt.so"))
+    lib.orc_mt_levels.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                                       ctypes.POINTER(ctypes.c_uint64), ctypes.c_int,
+                                                       ctypes.POINTER(ctypes.c_uint64),
+                                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]
+    cap = 256
+    d = (ctypes.c_uint64 * cap)()
+    g = (ctypes.c_uint64 * cap)()
+    dist, gen, depth = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+    t = time.time()
+    v = lib.orc_mt_levels(n, V, E, Rr, threads, max_states, d, g, cap, ctypes.byref(dist), ctypes.byref(gen),
+                          ctypes.byref(depth))
+    dt = time.time() - t
+    D = depth.value
+    assert v in (0, 2), f"unexpected verdict {v}"
+    # levels 1..D all complete; levels 1..D-1 expanded (level D too when the run exhausted)
+    levels, gens = list(d[:D]), list(g[:D if v == 0 else D - 1])
+    return {"n": n, "V": V, "E": E, "R": Rr, "max_states": max_states, "stopped_at_distinct": dist.value,
+            "exhausted": v == 0, "levels": levels, "gen_per_level": gens, "oracle_seconds": round(dt, 1),
+            "source": f"c_mt{threads}", "invariants": ["Inv"], "check_deadlock": False}
+
+
 def main():
-    max_states = int(sys.argv[1])
-    a = list(map(int, sys.argv[2:]))
+    args = sys.argv[1:]
+    threads = 0
+    if args and args[0] == "--mt":
+        threads, args = int(args[1]), args[2:]
+    max_states = int(args[0])
+    a = list(map(int, args[1:]))
     cfgs = [tuple(a[i:i + 4]) for i in range(0, len(a), 4)]
     path = os.environ.get("GOLDEN_PREFIX_OUT", os.path.join(HERE, "levels_prefix.json"))
     for (n, V, E, Rr) in cfgs:
-        r = run_prefix(n, V, E, Rr, max_states)
+        r = run_prefix_mt(n, V, E, Rr, max_states, threads) if threads else run_prefix(n, V, E, Rr, max_states)
         out = json.load(open(path)) if os.path.exists(path) else {}
         out[f"n{n}_v{V}_e{E}_r{Rr}"] = r
         with open(path, "w") as f:

@@ -232,6 +232,25 @@ def test_raft_cfg_exhausted_and_prefix_matches_c_oracle():
     assert res.seen_slot_bytes == 8
 
 
+@pytest.mark.skipif("n5_v1_e3_r3" not in PREFIX, reason="no configs[3] prefix fixture")
+def test_configs3_prefix_matches_c_oracle():
+    """configs[3] (5 servers, 1 value, MaxElection 3, MaxRestart 3; Raft.cfg:16-18 with s4, s5 in
+    Servers): the levels the C oracle completes (tests/golden/make_golden_prefix.py --mt, exact
+    canonical forms over all 120 permutations) equal the GPU's level by level -- the signature
+    pre-sort symmetry minimum against the exact orbit count."""
+    g = PREFIX["n5_v1_e3_r3"]
+    for mc in _cache.values():
+        mc.close()
+    _cache.clear()
+    with raftmc.ModelChecker(raftmc.ModelConfig(n_servers=5, n_vals=1, max_election=3, max_restart=3)) as mc:
+        mc.init()
+        while len(mc.levels) < len(g["levels"]) + 1:
+            mc.step()
+        got = [ls.new_states for ls in mc.levels]
+        assert got[:len(g["levels"])] == g["levels"]
+        assert [ls.generated for ls in mc.levels[1:len(g["gen_per_level"]) + 1]] == g["gen_per_level"]
+
+
 @pytest.mark.parametrize("name", sorted(TRACES))
 def test_counterexample_trace_matches_oracle(name):
     g = LEVELS[name]

@@ -229,3 +229,31 @@ def test_multithreaded_cpu_baseline_matches_golden():
                                 ctypes.byref(dep))
             assert rc == 0
             assert (d.value, gen.value, dep.value) == (g["distinct"], g["generated"], g["depth"]), (name, threads)
+
+
+def test_mt_oracle_levels_match_golden_and_prefix():
+    """orc_mt_levels (the --mt prefix generator behind the configs[3] fixture) reports the same
+    per-level distinct/generated counts as the single-threaded oracle's golden levels, and a run
+    stopped at max_states ends on a complete level that is a prefix of them."""
+    import ctypes
+    so = os.path.join(ROOT, "oracle", "build", "libraft_mt.so")
+    if not os.path.exists(so):
+        pytest.skip("oracle/build/libraft_mt.so not built")
+    lib = ctypes.CDLL(so)
+    P64 = ctypes.POINTER(ctypes.c_uint64)
+    lib.orc_mt_levels.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint64, P64, P64, ctypes.c_int, P64, P64,
+                                                       ctypes.POINTER(ctypes.c_int)]
+    levels = json.load(open(os.path.join(GOLDEN, "levels.json")))
+    for name, max_states, threads in (("n3_v1_e2_r3", 0, 4), ("n4_v1_e1_r3", 0, 3), ("n3_v1_e2_r3", 5000, 8)):
+        g = levels[name]
+        d, gen = (ctypes.c_uint64 * 256)(), (ctypes.c_uint64 * 256)()
+        dist, tot, dep = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+        rc = lib.orc_mt_levels(g["n"], g["V"], g["E"], g["R"], threads, max_states, d, gen, 256,
+                               ctypes.byref(dist), ctypes.byref(tot), ctypes.byref(dep))
+        D = dep.value
+        if max_states == 0:
+            assert rc == 0 and D == g["depth"] and list(d[:D]) == g["levels"]
+            assert list(gen[:D]) == g["gen_per_level"]
+        else:
+            assert rc == 2 and D < g["depth"] and sum(d[:D]) == dist.value >= max_states
+            assert list(d[:D]) == g["levels"][:D] and list(gen[:D - 1]) == g["gen_per_level"][:D - 1]

@@ -24,6 +24,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -1650,6 +1651,16 @@ struct rmc_ctx {
     // block that the following kernels read, and stops the loop on an empty level, an error, or a
     // level whose successor bound might not fit the buffers (the host then grows them and
     // carries on).
+    // device-loop submission shape (tuning knobs, read once): levels per group, groups queued ahead,
+    // host spins between stream queries while waiting for a group
+    static int env_int(const char *name, int dflt, int lo, int hi) {
+        const char *v = std::getenv(name);
+        if (!v || !*v) return dflt;
+        return std::max(lo, std::min(hi, std::atoi(v)));
+    }
+    const int dl_group = env_int("RMC_DL_GROUP", 2, 1, 64);
+    const int dl_ahead = env_int("RMC_DL_AHEAD", 2, 1, 64);
+    const uint32_t dl_query_mask = (1u << env_int("RMC_DL_QUERY_LOG2", 8, 0, 30)) - 1u;
     int batch_levels() const { return cfg.device_levels ? (int)cfg.device_levels : LREC_CAP; }
     uint64_t dev_parents() const { return std::min<uint64_t>(chunk_parents, 1ull << 15); }
     bool batch_ok() const {
@@ -1719,7 +1730,7 @@ struct rmc_ctx {
         // late (measured with reports at either end of a level and with a stream query right after
         // each submission); two levels per group halve that against one, and the no-op tail after
         // the last level stays at most two groups
-        const int GL = 2, ngroups = (K + GL - 1) / GL;
+        const int GL = dl_group, ngroups = (K + GL - 1) / GL;
         auto enqueue_group = [&](int g) {
             for (int i = g * GL; i < std::min(K, (g + 1) * GL); i++) {
                 mark[i] = evrecs.size();
@@ -1742,7 +1753,7 @@ struct rmc_ctx {
             for (uint32_t spin = 0;; spin++) {
                 if (__atomic_load_n(&s.hloop->stop, __ATOMIC_ACQUIRE) != (uint32_t)CTL_RUN) return false;
                 if (__atomic_load_n(&s.hloop->done, __ATOMIC_ACQUIRE) >= need) return true;
-                if ((spin & 255u) == 255u) {
+                if ((spin & dl_query_mask) == dl_query_mask) {
                     const hipError_t q = hipStreamQuery(stream);
                     if (q == hipSuccess) {  // drained: the mirror is final
                         if (__atomic_load_n(&s.hloop->stop, __ATOMIC_ACQUIRE) != (uint32_t)CTL_RUN) return false;
@@ -1753,9 +1764,9 @@ struct rmc_ctx {
             }
         };
         int enq = 0;
-        for (; enq < std::min(2, ngroups); enq++) enqueue_group(enq);
+        for (; enq < std::min(dl_ahead, ngroups); enq++) enqueue_group(enq);
         for (; enq < ngroups; enq++) {
-            if (!group_done(enq - 2)) break;
+            if (!group_done(enq - dl_ahead)) break;
             enqueue_group(enq);
         }
         for (int i = enq * GL; i < K; i++) mark[i] = evrecs.size();

@@ -48,6 +48,15 @@ extern "C" int rmc_debug_phases(unsigned long long *out, int reset) {
 #define PHASE_FLUSH do {} while (0)
 #endif
 
+#ifndef RMC_N3_WAVES  // n = 3 expansion (and commit): waves per SIMD the register budget is cut for
+#define RMC_N3_WAVES 4
+#endif
+#ifndef RMC_N3_COMMIT_WAVES
+#define RMC_N3_COMMIT_WAVES 1
+#endif
+#ifndef RMC_GRID_PER_CU  // one-wave blocks per CU in the expansion / commit grids
+#define RMC_GRID_PER_CU 32
+#endif
 #ifndef RMC_WIDE_WAVES
 #define RMC_WIDE_WAVES 2
 #endif
@@ -1215,7 +1224,7 @@ __device__ __forceinline__ void unstage_core(const uint32_t *pc, const uint4 a, 
 // BFV: the BecomeFollower variant (tla:420) -- MR more candidates (one per message lane) and MR * 64
 // more successor slots per parent (MX)
 template <int N, int V, int MR, int MODE, bool BFV = false>
-__global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? 4 : ((BFV && N >= 4) ? 1 : RMC_WIDE_WAVES)) void k_expand(KParams P) {
+__global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((BFV && N >= 4) ? 1 : RMC_WIDE_WAVES)) void k_expand(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
     constexpr bool SUMS = true;
@@ -1843,7 +1852,7 @@ __device__ __forceinline__ bool last_commit_block(uint32_t *tick, uint32_t nb) {
 // at the scanned word offset, its offset in noff), insert its fingerprint, record its parent
 // pointer and slot key.
 template <int N, int V, int MR, bool BFV = false>
-__global__ __launch_bounds__(64) void k_commit(KParams P) {
+__global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) void k_commit(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
     constexpr int MX = S::MAXS + (BFV ? S::MCAP : 0);  // successor slots per parent (k_expand)
@@ -1988,7 +1997,7 @@ __global__ __launch_bounds__(64) void k_commit(KParams P) {
 }
 
 static inline unsigned grid_for(uint64_t n) {
-    const uint64_t cap = 256ull * 32ull;  // 32 one-wave blocks per CU on 256 CUs
+    const uint64_t cap = 256ull * RMC_GRID_PER_CU;  // one-wave blocks per CU (default 32) on 256 CUs
     return (unsigned)(n < cap ? (n ? n : 1) : cap);
 }
 
