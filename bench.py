@@ -42,6 +42,8 @@ WORKLOADS = {
                                              "-deadlock"),
     "c2": dict(n=3, V=1, E=2, R=3, desc="BASELINE configs[1]: Raft.tla, 3 servers, 1 value, MaxElection(=MaxTerm)=2, "
                                          "MaxRestart=3, MaxLogLen=2, SYMMETRY+VIEW, INVARIANT Inv, -deadlock"),
+    "c4": dict(n=5, V=1, E=3, R=3, desc="BASELINE configs[3]: Raft.tla, 5 servers, 1 value, MaxElection(=MaxTerm)=3, "
+                                         "MaxRestart=3, SYMMETRY+VIEW, INVARIANT Inv, -deadlock"),
     "n3v2e2": dict(n=3, V=2, E=2, R=3, desc="Raft.tla, 3 servers, 2 values, MaxElection=2, MaxRestart=3 "
                                              "(18.5M states; between configs[1] and configs[2])"),
 }
@@ -129,6 +131,9 @@ def cpu_baseline(w, budget_s=12.0):
 
 
 SHARDED_TIMEOUT_S = 420  # the multi-GPU Raft.cfg exhaustion (child processes) must finish within this
+SHARDED_TOTAL_S = 480    # ... and both sharded legs (Raft.cfg, then configs[3] as deep as it goes) within this
+C4_BUDGET_S = 120        # levels of configs[3] are started until this much time has passed
+C4_ONE_GPU_LEVELS = 29   # configs[3] on one MI355X: levels 1-29 discovered (2.12 G states), ring full expanding 29
 
 
 def sharded_child(args):
@@ -147,10 +152,14 @@ def sharded_child(args):
     if rank == 0:
         idt = torch.tensor(list(raftmc.comm_unique_id()), dtype=torch.uint8)
     dist.broadcast(idt, 0)
-    w = WORKLOADS["raftcfg"]
+    w = WORKLOADS[args.child_workload]
     cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
                              invariants=("Inv",), check_deadlock=False, device=local, rank=rank, world_size=world,
                              comm_unique_id=bytes(idt.tolist()))
+    if args.child_workload == "c4":
+        c4_child(args, cfg, w, rank, world)
+        dist.destroy_process_group()
+        return
     with raftmc.ModelChecker(cfg) as mc:
         dist.barrier()
         t0 = time.perf_counter()
@@ -176,30 +185,114 @@ def sharded_child(args):
     dist.destroy_process_group()
 
 
-def run_sharded_children(args):
-    """Start this rank's sharded Raft.cfg child (before this process initialises the GPU), wait for it
-    with a time limit, and return rank 0's result (or what went wrong)."""
+def c4_child(args, cfg, w, rank, world):
+    """configs[3] sharded over the N GPUs, level by level, as deep as the node's HBM and the time
+    budget allow (its exhaustion is beyond any node: DESIGN.md section 9).  All ranks agree on
+    every decision: the budget (minimum over ranks), stopping after a level (any rank past the
+    budget), and a capacity failure (the engine raises it on every rank in the same round)."""
+    import torch
+    import torch.distributed as dist
+    import raftmc
+    b = torch.tensor([args.child_budget], dtype=torch.float64)
+    dist.all_reduce(b, op=dist.ReduceOp.MIN)
+    budget = float(b.item())
+    out = {"workload": w["desc"], "n_gpus": world, "one_gpu_levels": C4_ONE_GPU_LEVELS}
+    if budget < 30:
+        out["skipped"] = f"{budget:.0f} s left of the sharded legs' {SHARDED_TOTAL_S} s"
+        if rank == 0:
+            with open(args.sharded_out, "w") as f:
+                json.dump(out, f)
+        return
+    gold = {}
+    gpath = os.path.join(ROOT, "tests", "golden", "levels_prefix.json")
+    if os.path.exists(gpath):
+        gold = json.load(open(gpath)).get("n5_v1_e3_r3", {})
+
+    def report(levels, stop, dt):  # rank 0, after every level: a child killed at its limit still reports
+        k = min(len(levels), len(gold.get("levels", [])))
+        out.update({"parallelism": f"rccl-{world}", "levels_completed": len(levels), "distinct_states": sum(levels),
+                    "last_level_states": levels[-1], "stopped": stop, "seconds": round(dt, 3),
+                    "distinct_per_s": round(sum(levels) / dt, 1) if dt > 0 else None,
+                    "matches_c_oracle_prefix_levels": (levels[:k] == gold["levels"][:k]) if k else None,
+                    "c_oracle_prefix_levels_compared": k})
+        if rank == 0:
+            with open(args.sharded_out + ".tmp", "w") as f:
+                json.dump(out, f)
+            os.replace(args.sharded_out + ".tmp", args.sharded_out)
+
+    levels, stop = [], "exhausted"
+    with raftmc.ModelChecker(cfg) as mc:
+        dist.barrier()
+        t0 = time.perf_counter()
+        levels.append(mc.init().new_states)
+        tl = time.perf_counter()
+        while True:
+            try:
+                ls = mc.step()
+            except raftmc.RmcError as e:  # capacity: every rank raises in the same round
+                stop = str(e)[:200]
+                break
+            if ls.new_states == 0 or ls.status != "ok":
+                stop = "exhausted" if ls.status in ("ok", "done") else ls.status
+                break
+            levels.append(ls.new_states)
+            now = time.perf_counter()
+            # the next level is predicted from this one's time and growth; stop if it would end
+            # past the budget (any rank's view stops all)
+            nxt = (now - tl) * (levels[-1] / max(1, levels[-2]))
+            tl = now
+            report(levels, "in progress (the child's time limit ended the run)", now - t0)
+            past = torch.tensor([1 if now - t0 + nxt > budget else 0], dtype=torch.int32)
+            dist.all_reduce(past, op=dist.ReduceOp.MAX)
+            if int(past.item()):
+                stop = f"time budget ({budget:.0f} s): the next level was predicted past it"
+                break
+        dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    report(levels, stop, float(t.item()))
+
+
+def run_child(args, workload, timeout_s, budget_s=0.0):
+    """Start this rank's sharded child for `workload` (before this process initialises the GPU), wait
+    for it with a time limit, and return rank 0's result (or what went wrong)."""
     import subprocess
     import tempfile
     rank = int(os.environ.get("RANK", "0"))
-    out = os.path.join(tempfile.gettempdir(), f"rmc_sharded_{os.environ.get('MASTER_PORT', '0')}.json")
+    out = os.path.join(tempfile.gettempdir(), f"rmc_sharded_{workload}_{os.environ.get('MASTER_PORT', '0')}.json")
     if rank == 0 and os.path.exists(out):
         os.remove(out)
-    cmd = [sys.executable, os.path.abspath(__file__), "--sharded-child", "--sharded-out", out]
+    cmd = [sys.executable, os.path.abspath(__file__), "--sharded-child", "--sharded-out", out,
+           "--child-workload", workload, "--child-budget", str(budget_s)]
     t0 = time.perf_counter()
     p = subprocess.Popen(cmd, stdout=sys.stderr, stderr=sys.stderr)
     try:
-        rc = p.wait(timeout=SHARDED_TIMEOUT_S)
+        rc = p.wait(timeout=timeout_s)
     except subprocess.TimeoutExpired:
         p.kill()
         p.wait()
-        return {"error": f"timed out after {SHARDED_TIMEOUT_S} s", "wall_s": round(time.perf_counter() - t0, 1)}
+        err = {"error": f"timed out after {timeout_s:.0f} s", "wall_s": round(time.perf_counter() - t0, 1)}
+        if rank == 0 and os.path.exists(out):  # what the child reported before its limit (configs[3])
+            with open(out) as f:
+                err.update(json.load(f))
+        return err if rank == 0 else None
     if rank != 0:
         return None
     if rc != 0 or not os.path.exists(out):
         return {"error": f"child exited with {rc}", "wall_s": round(time.perf_counter() - t0, 1)}
     with open(out) as f:
         return json.load(f)
+
+
+def run_sharded_children(args):
+    """The two sharded legs at N > 1: Raft.cfg exhausted over the N GPUs (configs[2]), then configs[3]
+    as deep as the remaining time allows.  Every rank always starts both children; the configs[3]
+    child agrees on its budget across ranks (the minimum), so no rank is left in a collective."""
+    t0 = time.perf_counter()
+    raft = run_child(args, "raftcfg", SHARDED_TIMEOUT_S)
+    left = SHARDED_TOTAL_S - (time.perf_counter() - t0)
+    c4 = run_child(args, "c4", max(30.0, left), budget_s=min(C4_BUDGET_S, left - 60.0))
+    return raft, c4
 
 
 def main():
@@ -214,13 +307,15 @@ def main():
                     "multi-GPU Raft.cfg exhaustion (N>1)")
     ap.add_argument("--sharded-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--sharded-out", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--child-workload", default="raftcfg", choices=("raftcfg", "c4"), help=argparse.SUPPRESS)
+    ap.add_argument("--child-budget", type=float, default=C4_BUDGET_S, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.sharded_child:
         sharded_child(args)
         return
-    sharded = None
+    sharded = sharded_c4 = None
     if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not args.no_scale:
-        sharded = run_sharded_children(args)
+        sharded, sharded_c4 = run_sharded_children(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -372,6 +467,8 @@ def main():
         line["at_scale"] = at_scale(local, probes_per_s=pk_hbm)
     if rank == 0 and sharded is not None:
         line["at_scale_sharded"] = sharded
+    if rank == 0 and sharded_c4 is not None:
+        line["at_scale_sharded_configs3"] = sharded_c4
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(w)
     if rank == 0:

@@ -1652,7 +1652,7 @@ struct rmc_ctx {
     // level whose successor bound might not fit the buffers (the host then grows them and
     // carries on).
     // device-loop submission shape (tuning knobs, read once): levels per group, groups queued ahead,
-    // host spins between stream queries while waiting for a group
+    // microseconds of waiting for a group between stream queries
     static int env_int(const char *name, int dflt, int lo, int hi) {
         const char *v = std::getenv(name);
         if (!v || !*v) return dflt;
@@ -1660,7 +1660,7 @@ struct rmc_ctx {
     }
     const int dl_group = env_int("RMC_DL_GROUP", 2, 1, 64);
     const int dl_ahead = env_int("RMC_DL_AHEAD", 2, 1, 64);
-    const uint32_t dl_query_mask = (1u << env_int("RMC_DL_QUERY_LOG2", 8, 0, 30)) - 1u;
+    const int dl_query_us = env_int("RMC_DL_QUERY_US", 2000, 0, 1 << 30);
     int batch_levels() const { return cfg.device_levels ? (int)cfg.device_levels : LREC_CAP; }
     uint64_t dev_parents() const { return std::min<uint64_t>(chunk_parents, 1ull << 15); }
     bool batch_ok() const {
@@ -1748,12 +1748,17 @@ struct rmc_ctx {
             }
         };
         // true once group g has finished (or the loop stopped); a stream error ends the wait
+        // The stream is queried only after dl_query_us of waiting (then every dl_query_us): a
+        // hipStreamQuery while the loop runs cost ~2 % of configs[1]'s exhaustion when it was
+        // issued every 256 spins (measured, tools/dl_sweep.sh).
         auto group_done = [&](int g) {
             const uint32_t need = (uint32_t)std::min(K, (g + 1) * GL);
+            auto tq = std::chrono::steady_clock::now() + std::chrono::microseconds(dl_query_us);
             for (uint32_t spin = 0;; spin++) {
                 if (__atomic_load_n(&s.hloop->stop, __ATOMIC_ACQUIRE) != (uint32_t)CTL_RUN) return false;
                 if (__atomic_load_n(&s.hloop->done, __ATOMIC_ACQUIRE) >= need) return true;
-                if ((spin & dl_query_mask) == dl_query_mask) {
+                if ((spin & 255u) == 255u && std::chrono::steady_clock::now() >= tq) {
+                    tq = std::chrono::steady_clock::now() + std::chrono::microseconds(dl_query_us);
                     const hipError_t q = hipStreamQuery(stream);
                     if (q == hipSuccess) {  // drained: the mirror is final
                         if (__atomic_load_n(&s.hloop->stop, __ATOMIC_ACQUIRE) != (uint32_t)CTL_RUN) return false;
