@@ -136,6 +136,21 @@ C4_BUDGET_S = 120        # levels of configs[3] are started until this much time
 C4_ONE_GPU_LEVELS = 29   # configs[3] on one MI355X: levels 1-29 discovered (2.12 G states), ring full expanding 29
 
 
+def xgmi_model(levels, world, shard_min=1 << 20):
+    """SURVEY.md 8(d)'s multi-GPU addition, for the engine's exchange: from
+    the first level of >= shard_min parents on, every successor crosses to its fingerprint's owner
+    as a 24-B item {fp, key} and comes back as a 4-B verdict, and every winner's record (new_bytes)
+    plus a 16-B sidecar goes to the owner of its next-level index; (W-1)/W of it leaves the GPU."""
+    if world < 2:
+        return 0
+    total, on = 0, False
+    for ls in levels:
+        on = on or ls.expanded >= shard_min
+        if on:
+            total += ls.generated * (24 + 4) + ls.new_bytes + 16 * ls.new_states
+    return int(total * (world - 1) / world)
+
+
 def sharded_child(args):
     """One rank of the multi-GPU Raft.cfg exhaustion (configs[2] at N GPUs), run in a child process of
     each bench rank before the bench touches the GPU: the levels are sharded over the N GPUs (RCCL,
@@ -180,6 +195,9 @@ def sharded_child(args):
                "verdict": "Inv holds" if res.status == "done" else res.status,
                "seconds_to_exhaust": round(dt, 3), "distinct_per_s": round(res.distinct / dt, 1),
                "matches_c_oracle_prefix_levels": (got[:len(gold["levels"])] == gold["levels"]) if gold else None}
+        xb = xgmi_model(res.levels, world)
+        out["xgmi_bytes_model"] = xb
+        out["xgmi_GBps_avg"] = round(xb / dt / 1e9, 2)
         with open(args.sharded_out, "w") as f:
             json.dump(out, f)
     dist.destroy_process_group()

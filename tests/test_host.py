@@ -165,3 +165,20 @@ def test_become_follower_variant_spec_recognised():
                                     "--become-follower", src]).decode()
     cfg = raftmc.parse_config(open("/root/reference/Raft.cfg").read(), tla_text=text)
     assert cfg.spec_variant == raftmc.SPEC_BECOME_FOLLOWER
+
+
+def test_bench_xgmi_model():
+    """bench.py's modelled xGMI bytes: nothing below the first sharded level, (W-1)/W
+    of 28 B per successor + the winners' records and sidecars from it on, zero on one GPU."""
+    import importlib.util
+    from types import SimpleNamespace as L
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    levels = [L(expanded=10, generated=50, new_bytes=400, new_states=10),
+              L(expanded=2 ** 20, generated=100, new_bytes=800, new_states=20),
+              L(expanded=100, generated=10, new_bytes=0, new_states=0)]
+    assert bench.xgmi_model(levels, 1) == 0
+    per = 100 * 28 + 800 + 16 * 20 + 10 * 28
+    assert bench.xgmi_model(levels, 2) == per // 2
+    assert bench.xgmi_model(levels, 8) == int(per * 7 / 8)
