@@ -182,10 +182,13 @@ int rmc_reset(void *ctx);
 
 /* Checkpoint / resume between BFS levels (TLC's states/ metadir and -recover, .gitignore:2;
  * SURVEY 8(f) item 4).  rmc_checkpoint writes the seen set, the current level, every state's
- * parent reference and TLC's counters to `path`; single GPU (world_size 1, no virtual shards),
- * after rmc_init and before the run finishes.  rmc_resume loads such a file into a context
- * created with the same configuration and not yet initialised; rmc_step / rmc_run then carry
- * on as if the run had never stopped (same counts, same TLC order, same counterexample). */
+ * parent reference and TLC's counters to `path`, after rmc_init and before the run finishes.
+ * Sharded runs too: a context with virtual shards writes all of them to `path`; an RCCL rank of
+ * a world_size > 1 run writes its own shards to `path` + ".rank<r>" (every rank calls it between
+ * the same two levels).  rmc_resume loads such a file into a context created with the same
+ * configuration and shard layout (world size, rank, virtual shards, chunk size, shard_min) and
+ * not yet initialised; rmc_step / rmc_run then carry on as if the run had never stopped (same
+ * counts, same TLC order, same counterexample). */
 int rmc_checkpoint(void *ctx, const char *path);
 int rmc_resume(void *ctx, const char *path);
 

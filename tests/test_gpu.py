@@ -449,6 +449,87 @@ def test_checkpoint_resume_matches_uninterrupted(name, tmp_path):
     b.close()
 
 
+@pytest.mark.parametrize("mode", ["virtual2", "virtual4", "rccl1"])
+@pytest.mark.parametrize("name,shard_min", [("n3_v1_e2_r3", 1), ("seeded_n3_v2_e2_r3", 40),
+                                            ("deadlock_n3_v1_e1_r3", 1), ("n4_v1_e1_r3", 40)])
+def test_sharded_checkpoint_resume_matches_uninterrupted(name, shard_min, mode, tmp_path):
+    """Checkpoint of a sharded run (virtual shards, or the RCCL transport on a one-rank
+    communicator) after six levels -- sharded from Init, or still replicated / just sharded with
+    shard_min 40 -- resumed in a fresh checker with the same layout: the golden counts, the
+    remaining levels and the counterexample of the uninterrupted run."""
+    g = LEVELS[name]
+    cfg = dict(n_servers=g["n"], n_vals=g["V"], max_election=g["E"], max_restart=g["R"],
+               invariants=tuple(g["invariants"]), check_deadlock=g["check_deadlock"],
+               spec_variant=raftmc.SPEC_SEEDED if g["seeded"] else raftmc.SPEC_RAFT,
+               chunk_successors=3000, shard_min_states=shard_min)
+    if mode.startswith("virtual"):
+        cfg["virtual_shards"] = int(mode[7:])
+    path = str(tmp_path / "run.ckpt")
+
+    def make():
+        extra = dict(world_size=1, rank=0, comm_unique_id=raftmc.comm_unique_id()) if mode == "rccl1" else {}
+        return raftmc.ModelChecker(raftmc.ModelConfig(**cfg, **extra))
+
+    a = make()
+    a.init()
+    k = 0
+    while k < 6 and a.step().status == "ok":
+        k += 1
+    assert k == 6, "the configuration must run past the checkpoint level"
+    a.checkpoint(path)
+    done = len(a.levels)
+    res_a = a.run()
+    b = make()
+    b.resume(path)
+    res_b = b.run()
+    check_levels(g, res_a)
+    for f in ("status", "generated", "distinct", "depth", "queue", "violated", "trace_len"):
+        assert getattr(res_b, f) == getattr(res_a, f), f
+    assert [ls.new_states for ls in res_b.levels] == [ls.new_states for ls in res_a.levels[done:]]
+    assert b.trace() == a.trace()
+    a.close()
+    b.close()
+
+
+def test_sharded_checkpoint_resume_at_scale(tmp_path):
+    """18.5 M states over 2 virtual shards, sharded from the first level of 2^20 states, compact
+    seen-set shards and rings at their budget: checkpointed after 30 levels (sharded by then),
+    resumed in a fresh checker, finished with the C oracle's counts."""
+    g = LEVELS_BIG["n3_v2_e2_r3"]
+    cfg = raftmc.ModelConfig(n_servers=3, n_vals=2, max_election=2, max_restart=3, virtual_shards=2,
+                             compact_log2=20, seen_log2=12, seen_mem_bytes=8 << 25, frontier_mem_bytes=1 << 30)
+    path = str(tmp_path / "big.ckpt")
+    with raftmc.ModelChecker(cfg) as a:
+        a.init()
+        while len(a.levels) < 31:
+            assert a.step().status == "ok"
+        assert max(ls.expanded for ls in a.levels) >= 1 << 20, "the run must be sharded at the checkpoint"
+        a.checkpoint(path)
+        done = len(a.levels)
+    with raftmc.ModelChecker(cfg) as b:
+        b.resume(path)
+        res = b.run()
+    assert (res.status, res.distinct, res.generated, res.depth) == ("done", g["distinct"], g["generated"], g["depth"])
+    assert [ls.new_states for ls in res.levels if ls.new_states] == g["levels"][done:]
+    assert [ls.generated for ls in res.levels] == g["gen_per_level"][done - 1:]
+    assert res.seen_slot_bytes == 8
+
+
+def test_sharded_resume_rejects_another_layout(tmp_path):
+    path = str(tmp_path / "run.ckpt")
+    base = dict(n_servers=3, n_vals=1, max_election=2, max_restart=3, chunk_successors=3000, shard_min_states=1)
+    with raftmc.ModelChecker(raftmc.ModelConfig(**base, virtual_shards=2)) as a:
+        a.init()
+        a.step()
+        a.checkpoint(path)
+    with raftmc.ModelChecker(raftmc.ModelConfig(**base, virtual_shards=4)) as b:
+        with pytest.raises(raftmc.RmcError, match="another shard layout"):
+            b.resume(path)
+    with raftmc.ModelChecker(raftmc.ModelConfig(**base)) as c:
+        with pytest.raises(raftmc.RmcError, match="another shard layout"):
+            c.resume(path)
+
+
 def test_resume_rejects_another_configuration(tmp_path):
     path = str(tmp_path / "run.ckpt")
     with raftmc.ModelChecker(raftmc.ModelConfig(n_servers=3, n_vals=1, max_election=1, max_restart=3)) as a:

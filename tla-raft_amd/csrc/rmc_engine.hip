@@ -2454,19 +2454,31 @@ struct rmc_ctx {
     }
 
     // ---- checkpoint / resume (rmc_checkpoint, rmc_resume) --------------------------------
+    // One file per process: the run's header (configuration, fingerprint scheme, TLC's counters,
+    // and for the sharded protocol W, this process's first shard, the chunk size B that the
+    // block-cyclic layout depends on, replicated / sharded mode and the global level table),
+    // then one section per shard this process holds: its seen-set shard, its part of the current
+    // level (records linearised + offsets) and the parent reference of every state it holds.
+    // An RCCL rank of a W > 1 run writes path + ".rank<r>"; every rank resumes from its own file.
     struct CkptHeader {
         uint64_t magic;
         uint32_t abi, recw;
         int32_t n, v, e, r;
         uint32_t invariants, inv_order;
-        int32_t check_deadlock, spec_variant, no_symmetry, msg_cap, depth, compact;
+        int32_t check_deadlock, spec_variant, no_symmetry, msg_cap, depth, pad0;
         uint64_t scheme;
-        uint64_t total_generated, total_distinct, T_cap, T_count, cur_n, cur_words, n_levels, trace_n;
-        uint32_t epoch, pad;
+        uint64_t total_generated, total_distinct;
+        int32_t W, first_shard, nshards, replicated, L_shard, pad1;
+        uint64_t chunk_parents, shard_min, n_glevel;
         double seconds;
         uint64_t check;  // checksum of every field above
     };
-    static constexpr uint64_t CKPT_MAGIC = 0x3250434b434d52ull;  // "RMCKCP2"
+    struct CkptShard {
+        int32_t id, compact;
+        uint32_t epoch, pad;
+        uint64_t T_cap, T_count, cur_n, cur_words, n_levels, trace_n;
+    };
+    static constexpr uint64_t CKPT_MAGIC = 0x3350434b434d52ull;  // "RMCKCP3"
 
     CkptHeader ckpt_header() const {
         CkptHeader h{};
@@ -2479,13 +2491,23 @@ struct rmc_ctx {
         h.check_deadlock = cfg.check_deadlock; h.spec_variant = cfg.spec_variant;
         h.no_symmetry = cfg.no_symmetry; h.msg_cap = ks.MCAP;
         h.scheme = scheme_hash;
+        h.W = multi ? W : 0;
+        h.first_shard = multi ? sh[0].id : 0;
+        h.nshards = (int32_t)sh.size();
+        h.chunk_parents = multi ? chunk_parents : 0;
+        h.shard_min = multi ? shard_min : 0;
         return h;
     }
-    static uint64_t header_check(const CkptHeader &h) {
+    template <class T>
+    static uint64_t fnv(const T &h, size_t bytes) {
         const unsigned char *b = reinterpret_cast<const unsigned char *>(&h);
         uint64_t x = 0xcbf29ce484222325ull;
-        for (size_t i = 0; i < offsetof(CkptHeader, check); i++) x = (x ^ b[i]) * 0x100000001b3ull;
+        for (size_t i = 0; i < bytes; i++) x = (x ^ b[i]) * 0x100000001b3ull;
         return x;
+    }
+    static uint64_t header_check(const CkptHeader &h) { return fnv(h, offsetof(CkptHeader, check)); }
+    std::string ckpt_path(const char *path) const {
+        return (rccl && W > 1) ? std::string(path) + ".rank" + std::to_string(rank) : std::string(path);
     }
 
     // device <-> file in bounded pieces through one host buffer
@@ -2500,43 +2522,58 @@ struct rmc_ctx {
 
     // Written to path + ".tmp", flushed to disk, then renamed over path: the previous checkpoint
     // survives until the new one is complete.
-    void checkpoint(const char *path) {
-        if (multi) throw Fail(RMC_E_ARG, "checkpoint: single-GPU runs only");
+    void checkpoint(const char *path_arg) {
         if (!inited || finished) throw Fail(RMC_E_STATE, "checkpoint: between levels of a started, unfinished run");
-        Shard &s = sh[0];
         HIPCHK(hipStreamSynchronize(stream));
         sync_trace();
+        const std::string path = ckpt_path(path_arg);
         CkptHeader h = ckpt_header();
         h.depth = depth;
-        h.compact = s.Tc ? 1 : 0;
         h.total_generated = total_generated; h.total_distinct = total_distinct;
-        h.T_cap = s.T_cap; h.T_count = s.T_count; h.cur_n = s.cur_n; h.cur_words = s.cur_words;
-        h.n_levels = s.level_start.size();
-        h.trace_n = s.level_start.back() + s.cur_n;  // every state found so far has a global id below
-        h.epoch = s.epoch;
+        h.replicated = replicated ? 1 : 0;
+        h.L_shard = L_shard;
+        h.n_glevel = (multi && !replicated) ? glevel.size() : 0;
         h.seconds = seconds;
         h.check = header_check(h);
-        if (s.tflushed != h.trace_n) throw Fail(RMC_E_STATE, "checkpoint: trace not flushed");
-        const std::string tmp = std::string(path) + ".tmp";
+        std::vector<CkptShard> sc(sh.size());
+        for (size_t i = 0; i < sh.size(); i++) {
+            const Shard &t = sh[i];
+            CkptShard &c = sc[i];
+            c.id = t.id;
+            c.compact = t.Tc ? 1 : 0;
+            c.epoch = t.epoch;
+            c.T_cap = t.T_cap; c.T_count = t.T_count; c.cur_n = t.cur_n; c.cur_words = t.cur_words;
+            c.n_levels = t.level_start.size();
+            c.trace_n = t.level_start.back() + t.cur_n;  // every state the shard holds has a local gid below
+            if (t.tflushed != c.trace_n) throw Fail(RMC_E_STATE, "checkpoint: trace not flushed");
+        }
+        const std::string tmp = path + ".tmp";
         FILE *f = std::fopen(tmp.c_str(), "wb");
         if (!f) throw Fail(RMC_E_ARG, std::string("checkpoint: cannot write ") + tmp);
         bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 &&
-                  std::fwrite(s.level_start.data(), 8, s.level_start.size(), f) == s.level_start.size();
+                  std::fwrite(glevel.data(), 8, h.n_glevel, f) == h.n_glevel;
         auto out = [&](void *dev, char *host, size_t k) {
             HIPCHK(hipMemcpy(host, dev, k, hipMemcpyDeviceToHost));
             ok = ok && std::fwrite(host, 1, k, f) == k;
         };
-        if (s.Tc) stream_bytes(s.Tc, h.T_cap * 8, out);
-        else stream_bytes(s.T, h.T_cap * 16, out);
-        // the current level, linearised
-        uint32_t *lin = dmalloc<uint32_t>(std::max<uint64_t>(h.cur_words, 1));
-        ring_copy_out(s, s.cur_wbase, h.cur_words, lin);
-        HIPCHK(hipStreamSynchronize(stream));
-        stream_bytes(lin, h.cur_words * 4, out);
-        dfree(lin);
-        stream_bytes(s.cur_off, h.cur_n * 8, out);
-        s.hpar.for_range(0, h.trace_n, [&](const uint64_t *p, uint64_t k) { ok = ok && std::fwrite(p, 8, k, f) == k; });
-        s.hslot.for_range(0, h.trace_n, [&](const uint16_t *p, uint64_t k) { ok = ok && std::fwrite(p, 2, k, f) == k; });
+        for (size_t i = 0; ok && i < sh.size(); i++) {
+            Shard &t = sh[i];
+            const CkptShard &c = sc[i];
+            const uint64_t chk = fnv(c, sizeof c);
+            ok = std::fwrite(&c, sizeof c, 1, f) == 1 && std::fwrite(&chk, 8, 1, f) == 1 &&
+                 std::fwrite(t.level_start.data(), 8, c.n_levels, f) == c.n_levels;
+            if (t.Tc) stream_bytes(t.Tc, c.T_cap * 8, out);
+            else stream_bytes(t.T, c.T_cap * 16, out);
+            // the shard's part of the current level, linearised
+            uint32_t *lin = dmalloc<uint32_t>(std::max<uint64_t>(c.cur_words, 1));
+            ring_copy_out(t, t.cur_wbase, c.cur_words, lin);
+            HIPCHK(hipStreamSynchronize(stream));
+            stream_bytes(lin, c.cur_words * 4, out);
+            dfree(lin);
+            stream_bytes(t.cur_off, c.cur_n * 8, out);
+            t.hpar.for_range(0, c.trace_n, [&](const uint64_t *p, uint64_t k) { ok = ok && std::fwrite(p, 8, k, f) == k; });
+            t.hslot.for_range(0, c.trace_n, [&](const uint16_t *p, uint64_t k) { ok = ok && std::fwrite(p, 2, k, f) == k; });
+        }
         ok = std::fflush(f) == 0 && ok;
         ok = ok && fsync(fileno(f)) == 0;
         ok = (std::fclose(f) == 0) && ok;
@@ -2544,89 +2581,115 @@ struct rmc_ctx {
             std::remove(tmp.c_str());
             throw Fail(RMC_E_ARG, std::string("checkpoint: short write to ") + tmp);
         }
-        if (std::rename(tmp.c_str(), path) != 0) throw Fail(RMC_E_ARG, std::string("checkpoint: cannot rename to ") + path);
+        if (std::rename(tmp.c_str(), path.c_str()) != 0)
+            throw Fail(RMC_E_ARG, std::string("checkpoint: cannot rename to ") + path);
     }
 
-    void resume(const char *path) {
-        if (multi) throw Fail(RMC_E_ARG, "resume: single-GPU runs only");
+    void resume(const char *path_arg) {
         if (inited) throw Fail(RMC_E_STATE, "resume: needs a context not yet initialised (rmc_create or rmc_reset)");
         HIPCHK(hipStreamSynchronize(stream));  // rmc_reset's clears are stream-ordered, the loads below are not
-        FILE *f = std::fopen(path, "rb");
+        const std::string path = ckpt_path(path_arg);
+        FILE *f = std::fopen(path.c_str(), "rb");
         if (!f) throw Fail(RMC_E_ARG, std::string("resume: cannot read ") + path);
+        auto fail = [&](const char *what) {
+            std::fclose(f);
+            throw Fail(RMC_E_ARG, std::string("resume: ") + path + what);
+        };
         CkptHeader h{};
         const CkptHeader want = ckpt_header();
         bool ok = std::fread(&h, sizeof h, 1, f) == 1;
         if (!ok || h.magic != CKPT_MAGIC || h.abi != want.abi || h.recw != want.recw || h.n != want.n ||
             h.v != want.v || h.e != want.e || h.r != want.r || h.invariants != want.invariants ||
             h.inv_order != want.inv_order || h.check_deadlock != want.check_deadlock ||
-            h.spec_variant != want.spec_variant || h.no_symmetry != want.no_symmetry || h.msg_cap != want.msg_cap) {
-            std::fclose(f);
-            throw Fail(RMC_E_ARG, std::string("resume: ") + path + " is not a checkpoint of this configuration");
-        }
-        if (h.scheme != want.scheme) {
-            std::fclose(f);
-            throw Fail(RMC_E_ARG, std::string("resume: ") + path + " was written with another fingerprint scheme");
-        }
+            h.spec_variant != want.spec_variant || h.no_symmetry != want.no_symmetry || h.msg_cap != want.msg_cap)
+            fail(" is not a checkpoint of this configuration");
+        if (h.scheme != want.scheme) fail(" was written with another fingerprint scheme");
+        if (h.W != want.W || h.first_shard != want.first_shard || h.nshards != want.nshards ||
+            h.chunk_parents != want.chunk_parents || h.shard_min != want.shard_min)
+            fail(" was written with another shard layout (world size, rank, virtual shards, chunk size or shard_min)");
         // the header's own consistency, before anything is allocated from it
-        if (h.check != header_check(h) || h.n_levels == 0 || h.n_levels > 100000 ||
-            (!h.compact && (h.T_cap & (h.T_cap - 1)) != 0) || h.T_cap == 0 ||
-            h.T_count >= h.T_cap || h.T_count > h.trace_n || h.cur_words > h.cur_n * (uint64_t)RECW ||
-            h.cur_words < h.cur_n * (uint64_t)ks.CCW) {
-            std::fclose(f);
-            throw Fail(RMC_E_ARG, std::string("resume: ") + path + " has an inconsistent header");
-        }
-        std::vector<uint64_t> ls(h.n_levels);
-        ok = std::fread(ls.data(), 8, ls.size(), f) == ls.size();
-        for (size_t i = 1; ok && i < ls.size(); i++) ok = ls[i] > ls[i - 1];
-        if (!ok || ls.back() + h.cur_n != h.trace_n) {
-            std::fclose(f);
-            throw Fail(RMC_E_ARG, std::string("resume: ") + path + " has an inconsistent level table");
-        }
-        Shard &s = sh[0];
-        dfree(s.T);
-        dfree(s.Tc);
-        if (h.compact) {
-            s.Tc = dmalloc<unsigned long long>(h.T_cap);
-            s.ring_fixed = false;  // re-derived below
-        } else {
-            s.T = dmalloc<ulonglong2>(h.T_cap);
-        }
-        s.T_cap = h.T_cap;
-        s.cur_wbase = 0;
-        s.cur_words = 0;
-        s.nxt_words = 0;
-        ensure_ring(s, h.cur_words + 1, 0);
-        ensure_off(s.cur_off, s.cur_off_cap, 0, std::max<uint64_t>(h.cur_n, 1));
+        if (h.check != header_check(h) || h.n_glevel > 100000 || (h.replicated && h.n_glevel) ||
+            (multi && !h.replicated && (h.n_glevel == 0 || h.L_shard <= 0)))
+            fail(" has an inconsistent header");
+        std::vector<uint64_t> gl(h.n_glevel);
+        ok = std::fread(gl.data(), 8, gl.size(), f) == gl.size();
+        for (size_t i = 1; ok && i < gl.size(); i++) ok = gl[i] > gl[i - 1];
+        if (!ok) fail(" has an inconsistent global level table");
+        std::vector<CkptShard> sc(sh.size());
+        std::vector<std::vector<uint64_t>> lss(sh.size());
         auto in = [&](void *dev, char *host, size_t k) {
             ok = ok && std::fread(host, 1, k, f) == k;
             if (ok) HIPCHK(hipMemcpy(dev, host, k, hipMemcpyHostToDevice));
         };
-        if (s.Tc) stream_bytes(s.Tc, h.T_cap * 8, in);
-        else stream_bytes(s.T, h.T_cap * 16, in);
-        stream_bytes(s.R, h.cur_words * 4, in);
-        stream_bytes(s.cur_off, h.cur_n * 8, in);
-        s.hpar.reserve_to(h.trace_n);
-        s.hslot.reserve_to(h.trace_n);
-        for (uint64_t i = 0; ok && i < h.trace_n;) {
-            const uint64_t k = std::min<uint64_t>(h.trace_n - i, HostArr<uint64_t>::B - i % HostArr<uint64_t>::B);
-            ok = std::fread(s.hpar.blk[i / HostArr<uint64_t>::B].p + i % HostArr<uint64_t>::B, 8, k, f) == k;
-            i += k;
-        }
-        for (uint64_t i = 0; ok && i < h.trace_n;) {
-            const uint64_t k = std::min<uint64_t>(h.trace_n - i, HostArr<uint16_t>::B - i % HostArr<uint16_t>::B);
-            ok = std::fread(s.hslot.blk[i / HostArr<uint16_t>::B].p + i % HostArr<uint16_t>::B, 2, k, f) == k;
-            i += k;
+        for (size_t i = 0; i < sh.size(); i++) {
+            Shard &s = sh[i];
+            CkptShard &c = sc[i];
+            uint64_t chk = 0;
+            ok = std::fread(&c, sizeof c, 1, f) == 1 && std::fread(&chk, 8, 1, f) == 1;
+            if (!ok || chk != fnv(c, sizeof c) || c.id != s.id || c.n_levels == 0 || c.n_levels > 100000 ||
+                (!c.compact && (c.T_cap & (c.T_cap - 1)) != 0) || c.T_cap == 0 || c.T_count >= c.T_cap ||
+                c.T_count > h.total_distinct || (!multi && c.T_count > c.trace_n) || c.cur_words > c.cur_n * (uint64_t)RECW || c.cur_words < c.cur_n * (uint64_t)ks.CCW)
+                fail(" has an inconsistent shard header");
+            std::vector<uint64_t> &ls = lss[i];
+            ls.resize(c.n_levels);
+            ok = std::fread(ls.data(), 8, ls.size(), f) == ls.size();
+            // (a shard may hold no state of a small sharded level: non-decreasing there)
+            for (size_t j = 1; ok && j < ls.size(); j++) ok = multi ? ls[j] >= ls[j - 1] : ls[j] > ls[j - 1];
+            if (!ok || ls.back() + c.cur_n != c.trace_n) fail(" has an inconsistent level table");
+            dfree(s.T);
+            dfree(s.Tc);
+            if (c.compact) {
+                s.Tc = dmalloc<unsigned long long>(c.T_cap);
+                s.ring_fixed = false;  // re-derived below
+            } else {
+                s.T = dmalloc<ulonglong2>(c.T_cap);
+            }
+            s.T_cap = c.T_cap;
+            s.cur_wbase = 0;
+            s.cur_words = 0;
+            s.nxt_words = 0;
+            ensure_ring(s, c.cur_words + 1, 0);
+            ensure_off(s.cur_off, s.cur_off_cap, 0, std::max<uint64_t>(c.cur_n, 1));
+            if (s.Tc) stream_bytes(s.Tc, c.T_cap * 8, in);
+            else stream_bytes(s.T, c.T_cap * 16, in);
+            stream_bytes(s.R, c.cur_words * 4, in);
+            stream_bytes(s.cur_off, c.cur_n * 8, in);
+            s.hpar.reserve_to(c.trace_n);
+            s.hslot.reserve_to(c.trace_n);
+            for (uint64_t j = 0; ok && j < c.trace_n;) {
+                const uint64_t k = std::min<uint64_t>(c.trace_n - j, HostArr<uint64_t>::B - j % HostArr<uint64_t>::B);
+                ok = std::fread(s.hpar.blk[j / HostArr<uint64_t>::B].p + j % HostArr<uint64_t>::B, 8, k, f) == k;
+                j += k;
+            }
+            for (uint64_t j = 0; ok && j < c.trace_n;) {
+                const uint64_t k = std::min<uint64_t>(c.trace_n - j, HostArr<uint16_t>::B - j % HostArr<uint16_t>::B);
+                ok = std::fread(s.hslot.blk[j / HostArr<uint16_t>::B].p + j % HostArr<uint16_t>::B, 2, k, f) == k;
+                j += k;
+            }
+            if (!ok) fail(" is truncated");
         }
         std::fclose(f);
-        if (!ok) throw Fail(RMC_E_ARG, std::string("resume: ") + path + " is truncated");
-        s.hpar.n = s.hslot.n = h.trace_n;
-        s.tflushed = h.trace_n;
-        s.level_start = ls;
-        s.cur_n = h.cur_n;
-        s.cur_words = h.cur_words;
-        s.T_count = h.T_count;
-        s.epoch = std::max(s.epoch, h.epoch);
-        if (s.Tc) fix_ring(s, 1);  // a compact seen set means a large run: the ring goes to its budget
+        for (size_t i = 0; i < sh.size(); i++) {
+            Shard &s = sh[i];
+            const CkptShard &c = sc[i];
+            s.hpar.n = s.hslot.n = c.trace_n;
+            s.tflushed = s.tdev = c.trace_n;
+            s.level_start = lss[i];
+            s.cur_n = c.cur_n;
+            s.nxt_n = 0;
+            s.cur_words = c.cur_words;
+            s.T_count = c.T_count;
+            s.epoch = std::max(s.epoch, c.epoch);
+        }
+        // a compact seen set means a large run: the rings go to their budget (shared by the
+        // shards of this process, as enter_sharded leaves them)
+        for (Shard &s : sh)
+            if (s.Tc) fix_ring(s, sh.size());
+        if (multi) {
+            replicated = h.replicated != 0;
+            glevel = gl;
+            L_shard = h.L_shard;
+        }
         total_generated = h.total_generated;
         total_distinct = h.total_distinct;
         depth = h.depth;
@@ -2637,7 +2700,7 @@ struct rmc_ctx {
         err_ref = 0;
         err_last_slot = KEY_NONE;
         inited = true;
-        finished = s.cur_n == 0;
+        finished = sh[0].cur_n == 0 && (replicated || !multi);
         if (finished) { status = RMC_DONE; queue_at_end = 0; }
     }
 

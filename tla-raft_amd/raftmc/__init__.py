@@ -425,7 +425,8 @@ class ModelChecker:
         self._inited = False
 
     def checkpoint(self, path: str) -> None:
-        """Write the run so far (seen set, current level, parent references, counters) to path."""
+        """Write the run so far (seen set, current level, parent references, counters) to path (an RCCL
+        rank of a world_size > 1 run: path + ".rank<r>"; virtual shards: all in path)."""
         self._check(self.lib.rmc_checkpoint(self.h, os.fsencode(path)))
 
     def resume(self, path: str) -> None:
