@@ -161,7 +161,8 @@ def sharded_child(args):
     import raftmc
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    port = int(os.environ.get("MASTER_PORT", "29500")) + 17
+    # a port of its own per child (the Raft.cfg child's store may still hold its port when the next starts)
+    port = int(os.environ.get("MASTER_PORT", "29500")) + (17 if args.child_workload == "raftcfg" else 19)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     idt = torch.zeros(128, dtype=torch.uint8)
     if rank == 0:
