@@ -133,7 +133,7 @@ def cpu_baseline(w, budget_s=12.0):
 SHARDED_TIMEOUT_S = 420  # the multi-GPU Raft.cfg exhaustion (child processes) must finish within this
 SHARDED_TOTAL_S = 480    # ... and both sharded legs (Raft.cfg, then configs[3] as deep as it goes) within this
 C4_BUDGET_S = 120        # levels of configs[3] are started until this much time has passed
-C4_ONE_GPU_LEVELS = 29   # configs[3] on one MI355X: levels 1-29 discovered (2.12 G states), ring full expanding 29
+C4_ONE_GPU_LEVELS = 30   # configs[3] on one MI355X, single-GPU path, 48 GB seen set / 200 GB ring: levels 1-30
 
 
 def xgmi_model(levels, world, shard_min=1 << 20):
@@ -173,6 +173,10 @@ def sharded_child(args):
                              invariants=("Inv",), check_deadlock=False, device=local, rank=rank, world_size=world,
                              comm_unique_id=bytes(idt.tolist()))
     if args.child_workload == "c4":
+        # per GPU: a 48 GB seen-set shard (6.4 G compact slots) and a 160 GB frontier ring, ~80 GB
+        # left for the rounds' buffers; the default gives the seen set half of HBM, far more than
+        # this configuration's levels fill before the ring does
+        cfg.seen_mem_bytes, cfg.frontier_mem_bytes = 48 << 30, 160 << 30
         c4_child(args, cfg, w, rank, world)
         dist.destroy_process_group()
         return

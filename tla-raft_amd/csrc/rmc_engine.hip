@@ -2151,8 +2151,8 @@ struct rmc_ctx {
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
                 if (!s.np) continue;
-                grow_outbox(s, wwords[li], wnum[li]);
                 guard(li, [&] {
+                    grow_outbox(s, wwords[li], wnum[li]);
                     if (wwords[li] >= s.rcap) ensure_ring(s, wwords[li], 0);  // P.rcap also bounds the outbox
                     timed(PH_MAT, [&] { ks.commit(round_params(s, gbase), stream); });
                 });
