@@ -782,12 +782,15 @@ struct rmc_ctx {
 
         // successor slots per chunk: dense for the sharded path, sparse (parents x maxsucc) for
         // the fused single-GPU path, whose staging holds SW4 * 16 + 36 bytes per slot
-        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (multi ? (virt ? (1ull << 23) : (1ull << 26)) : (1ull << 26));
+        // (an RCCL rank's rounds take 2^27 slots, ~2 M parents: each round pays a dozen host round
+        // trips and collectives, so fewer, larger rounds; the one-GPU fused path keeps 2^26, whose
+        // per-chunk cost is a few launches)
+        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (multi ? (virt ? (1ull << 23) : (1ull << 27)) : (1ull << 26));
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 30)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^30");
         chunk_parents = Gcap / ks.maxsucc;
         shard_min = multi ? (cfg.shard_min_states ? cfg.shard_min_states : (1ull << 20)) : 0;
-        chunk_parents = std::min<uint64_t>(chunk_parents, (uint64_t)WTILE * 1024);  // winner-count tiles
+        chunk_parents = std::min<uint64_t>(chunk_parents, (uint64_t)WTILE * WTILES_MAX);  // winner-count tiles
         Lcap_max = next_pow2(2 * Gcap);
 
         sh.resize(virt ? W : 1);
@@ -829,11 +832,11 @@ struct rmc_ctx {
         s.ctick = dmalloc<uint32_t>(33 * 32);
         HIPCHK(hipMemsetAsync(s.ctick, 0, 33 * 32 * 4, stream));
         HIPCHK(hipMemsetAsync(s.wacc, 0, (chunk_parents + 1) * 4, stream));
-        s.bw = dmalloc<uint32_t>(1024);
-        s.bg = dmalloc<uint32_t>(1024);
-        s.boff = dmalloc<uint32_t>(1024);
-        s.bww = dmalloc<uint32_t>(1024);
-        s.boffw = dmalloc<uint32_t>(1024);
+        s.bw = dmalloc<uint32_t>(WTILES_MAX);
+        s.bg = dmalloc<uint32_t>(WTILES_MAX);
+        s.boff = dmalloc<uint32_t>(WTILES_MAX);
+        s.bww = dmalloc<uint32_t>(WTILES_MAX);
+        s.boffw = dmalloc<uint32_t>(WTILES_MAX);
         s.tickets = dmalloc<uint32_t>(4);
         HIPCHK(hipMemsetAsync(s.tickets, 0, 16, stream));
         s.ctl = dmalloc<LevelCtl>(1);

@@ -65,7 +65,8 @@ struct HostLoop {
     LevelCtl ctl;                // the control block as the last finished level left it
     LevelRec rec[LREC_CAP];
 };
-constexpr uint32_t WTILE = 1024; // parents per tile of the winner-count scan (1024 tiles at most)
+constexpr uint32_t WTILE = 1024; // parents per tile of the winner-count scan
+constexpr uint32_t WTILES_MAX = 2048; // tiles per chunk (the last block scans two per thread)
 constexpr int SUM_WORDS = 7;     // chunk summary slot of the new states' record words
 
 // In device-loop mode the host sizes every grid on a bound of the level's parents (p_end -

@@ -1731,20 +1731,29 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
     }
     __syncthreads();
     if (!flag) return;
-    // tile offsets (ntiles <= 1024 = blockDim.x) and the chunk totals
-    uint32_t wsum = 0, gsum = 0, dsum = 0, wtot, gtot, dtot;
+    // tile offsets (ntiles <= WTILES_MAX: thread i takes tiles 2i and 2i + 1) and the chunk totals
+    static_assert(WTILES_MAX == 2 * 1024, "two tiles per thread of the 1024-thread block");
+    uint32_t wv[2] = {0u, 0u}, gv[2] = {0u, 0u}, dv[2] = {0u, 0u}, wtot, gtot, dtot;
     const uint32_t i = threadIdx.x;
-    if (i < ntiles) {
-        wsum = __hip_atomic_load(&P.bw[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        gsum = __hip_atomic_load(&P.bg[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        dsum = __hip_atomic_load(&P.bww[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const uint32_t tl = 2 * i + (uint32_t)k;
+        if (tl < ntiles) {
+            wv[k] = __hip_atomic_load(&P.bw[tl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gv[k] = __hip_atomic_load(&P.bg[tl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            dv[k] = __hip_atomic_load(&P.bww[tl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
-    const uint32_t o = block_excl_scan(wsum, ws, &wtot);
-    (void)block_excl_scan(gsum, ws, &gtot);
-    const uint32_t od = block_excl_scan(dsum, ws, &dtot);
-    if (i < ntiles) {
-        P.boff[i] = o;
-        P.boffw[i] = od;
+    const uint32_t o = block_excl_scan(wv[0] + wv[1], ws, &wtot);
+    (void)block_excl_scan(gv[0] + gv[1], ws, &gtot);
+    const uint32_t od = block_excl_scan(dv[0] + dv[1], ws, &dtot);
+    if (2 * i < ntiles) {
+        P.boff[2 * i] = o;
+        P.boffw[2 * i] = od;
+    }
+    if (2 * i + 1 < ntiles) {
+        P.boff[2 * i + 1] = o + wv[0];
+        P.boffw[2 * i + 1] = od + dv[0];
     }
     if (i == 0) {
         P.sum[0] = gtot;
