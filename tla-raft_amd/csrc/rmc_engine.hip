@@ -782,10 +782,10 @@ struct rmc_ctx {
 
         // successor slots per chunk: dense for the sharded path, sparse (parents x maxsucc) for
         // the fused single-GPU path, whose staging holds SW4 * 16 + 36 bytes per slot
-        // (an RCCL rank's rounds take 2^27 slots, ~2 M parents: each round pays a dozen host round
-        // trips and collectives, so fewer, larger rounds; the one-GPU fused path keeps 2^26, whose
-        // per-chunk cost is a few launches)
-        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (multi ? (virt ? (1ull << 23) : (1ull << 27)) : (1ull << 26));
+        // 2^27 slots (~2 M parents for 3 servers, 2 values): fewer, larger chunks -- an RCCL rank's
+        // round pays a dozen host round trips and collectives (one-rank Raft.cfg 66.8 -> 60.6 s
+        // against 2^26), a one-GPU chunk a few launches and its tail (Raft.cfg 55.0 -> 52.7 s)
+        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (virt ? (1ull << 23) : (1ull << 27));
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 30)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^30");
         chunk_parents = Gcap / ks.maxsucc;
