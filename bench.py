@@ -487,6 +487,7 @@ def main():
         "survey_roofline": survey_roofline(res.levels, S, elapsed / args.steps, pk_hbm),
     }
     if rank == 0 and world == 1 and not args.no_scale:
+        mc.close()  # the at-scale run gets the whole device (this checker's chunk buffers are ~12 GB)
         line["at_scale"] = at_scale(local, probes_per_s=pk_hbm)
     if rank == 0 and sharded is not None:
         line["at_scale_sharded"] = sharded

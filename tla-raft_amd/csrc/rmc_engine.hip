@@ -782,9 +782,11 @@ struct rmc_ctx {
 
         // successor slots per chunk: dense for the sharded path, sparse (parents x maxsucc) for
         // the fused single-GPU path, whose staging holds SW4 * 16 + 36 bytes per slot
-        // 2^27 slots (~2 M parents for 3 servers, 2 values): fewer, larger chunks -- an RCCL rank's
+        // Fewer, larger chunks: 2^27 slots (~2 M parents for 3 servers and 2 values).  An RCCL rank's
         // round pays a dozen host round trips and collectives (one-rank Raft.cfg 66.8 -> 60.6 s
-        // against 2^26), a one-GPU chunk a few launches and its tail (Raft.cfg 55.0 -> 52.7 s)
+        // against 2^26), a one-GPU chunk a few launches and their tails (Raft.cfg 55.0 s at 2^26,
+        // 52.7 at 2^27, 51.7 at 2^28).  The chunk buffers are allocated at create (~12 GB at
+        // 2^27 for n = 3), so 2^28 would cost every checker ~25 GB: chunk_successors opts in.
         Gcap = cfg.chunk_successors ? cfg.chunk_successors : (virt ? (1ull << 23) : (1ull << 27));
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 30)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^30");

@@ -66,7 +66,7 @@ struct HostLoop {
     LevelRec rec[LREC_CAP];
 };
 constexpr uint32_t WTILE = 1024; // parents per tile of the winner-count scan
-constexpr uint32_t WTILES_MAX = 2048; // tiles per chunk (the last block scans two per thread)
+constexpr uint32_t WTILES_MAX = 4096; // tiles per chunk (the last block scans four per thread)
 constexpr int SUM_WORDS = 7;     // chunk summary slot of the new states' record words
 
 // In device-loop mode the host sizes every grid on a bound of the level's parents (p_end -

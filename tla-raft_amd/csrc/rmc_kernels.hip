@@ -1731,29 +1731,37 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
     }
     __syncthreads();
     if (!flag) return;
-    // tile offsets (ntiles <= WTILES_MAX: thread i takes tiles 2i and 2i + 1) and the chunk totals
-    static_assert(WTILES_MAX == 2 * 1024, "two tiles per thread of the 1024-thread block");
-    uint32_t wv[2] = {0u, 0u}, gv[2] = {0u, 0u}, dv[2] = {0u, 0u}, wtot, gtot, dtot;
+    // tile offsets (ntiles <= WTILES_MAX: thread i takes tiles TPT i .. TPT i + TPT - 1) and the
+    // chunk totals
+    constexpr uint32_t TPT = WTILES_MAX / 1024;
+    static_assert(TPT * 1024 == WTILES_MAX, "whole tiles per thread of the 1024-thread block");
+    uint32_t wv[TPT], gv[TPT], dv[TPT], wtot, gtot, dtot, ws_ = 0, gs_ = 0, ds_ = 0;
     const uint32_t i = threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const uint32_t tl = 2 * i + (uint32_t)k;
+    for (uint32_t k = 0; k < TPT; k++) {
+        const uint32_t tl = TPT * i + k;
+        wv[k] = gv[k] = dv[k] = 0u;
         if (tl < ntiles) {
             wv[k] = __hip_atomic_load(&P.bw[tl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             gv[k] = __hip_atomic_load(&P.bg[tl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             dv[k] = __hip_atomic_load(&P.bww[tl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        ws_ += wv[k];
+        gs_ += gv[k];
+        ds_ += dv[k];
     }
-    const uint32_t o = block_excl_scan(wv[0] + wv[1], ws, &wtot);
-    (void)block_excl_scan(gv[0] + gv[1], ws, &gtot);
-    const uint32_t od = block_excl_scan(dv[0] + dv[1], ws, &dtot);
-    if (2 * i < ntiles) {
-        P.boff[2 * i] = o;
-        P.boffw[2 * i] = od;
-    }
-    if (2 * i + 1 < ntiles) {
-        P.boff[2 * i + 1] = o + wv[0];
-        P.boffw[2 * i + 1] = od + dv[0];
+    uint32_t o = block_excl_scan(ws_, ws, &wtot);
+    (void)block_excl_scan(gs_, ws, &gtot);
+    uint32_t od = block_excl_scan(ds_, ws, &dtot);
+#pragma unroll
+    for (uint32_t k = 0; k < TPT; k++) {
+        const uint32_t tl = TPT * i + k;
+        if (tl < ntiles) {
+            P.boff[tl] = o;
+            P.boffw[tl] = od;
+        }
+        o += wv[k];
+        od += dv[k];
     }
     if (i == 0) {
         P.sum[0] = gtot;
