@@ -357,6 +357,7 @@ struct Shard {
     ulonglong2 *LXY = nullptr;  // fused path: fingerprint of each election slot (tagged)
     uint32_t epoch = 0;
     uint32_t lxy_epoch0 = 0;    // epoch of the last LXY clear (16-bit tags repeat after 65535 epochs)
+    uint64_t gslots = 0, lcap = 0;  // successor slots of fp / lslot / score, election slots of L / LXY
     // fused single-shard level: sparse successor staging (slot q = chunk parent * maxsucc + rank)
     uint4 *score = nullptr;
     uint32_t *wcnt = nullptr, *wacc = nullptr, *pnm = nullptr, *wposw = nullptr, *ctick = nullptr;
@@ -782,12 +783,13 @@ struct rmc_ctx {
 
         // successor slots per chunk: dense for the sharded path, sparse (parents x maxsucc) for
         // the fused single-GPU path, whose staging holds SW4 * 16 + 36 bytes per slot
-        // Fewer, larger chunks: 2^27 slots (~2 M parents for 3 servers and 2 values).  An RCCL rank's
-        // round pays a dozen host round trips and collectives (one-rank Raft.cfg 66.8 -> 60.6 s
-        // against 2^26), a one-GPU chunk a few launches and their tails (Raft.cfg 55.0 s at 2^26,
-        // 52.7 at 2^27, 51.7 at 2^28).  The chunk buffers are allocated at create (~12 GB at
-        // 2^27 for n = 3), so 2^28 would cost every checker ~25 GB: chunk_successors opts in.
-        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (virt ? (1ull << 23) : (1ull << 27));
+        // Fewer, larger chunks.  An RCCL rank's round (2^27 slots, ~2 M parents for 3 servers and 2
+        // values) pays a dozen host round trips and collectives (one-rank Raft.cfg 66.8 -> 60.6 s
+        // against 2^26); a one-GPU chunk (2^28 slots, ~4 M parents) a few launches and their tails
+        // (Raft.cfg 55.0 s at 2^26, 52.7 at 2^27, 51.7 at 2^28).  On one GPU the slot buffers grow
+        // on demand (ensure_chunk), so a small run does not pay for them; an RCCL rank allocates
+        // them at create, its budgets may be explicit (bench's configs[3] leg).
+        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (virt ? (1ull << 23) : multi ? (1ull << 27) : (1ull << 28));
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 30)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^30");
         chunk_parents = Gcap / ks.maxsucc;
@@ -811,22 +813,47 @@ struct rmc_ctx {
         HIPCHK(hipStreamSynchronize(stream));
     }
 
+    // Successor-slot buffers (fingerprints, election slots, staging) and the election table for
+    // at least `slots` successor slots (powers of two, at most Gcap / Lcap_max).  A checker whose
+    // levels all run in the device loop keeps them small; the first larger chunk grows them, and
+    // so does the move of the seen set / ring to their budgets (migrate_compact, fix_ring) -- so
+    // that those budgets are taken from what the full chunk buffers leave.
+    void ensure_chunk(Shard &s, uint64_t slots) {
+        slots = std::min<uint64_t>(std::max<uint64_t>(slots, 1), Gcap);
+        if (slots <= s.gslots) return;
+        const uint64_t g = std::min<uint64_t>(std::max<uint64_t>(next_pow2(slots), 2 * s.gslots), Gcap);
+        const uint64_t lc = std::min<uint64_t>(next_pow2(2 * g), Lcap_max);
+        HIPCHK(hipStreamSynchronize(stream));
+        dfree(s.fp); dfree(s.lslot); dfree(s.score);
+        s.fp = nullptr; s.lslot = nullptr; s.score = nullptr;
+        s.fp = dmalloc<ulonglong2>(g);
+        s.lslot = dmalloc<uint32_t>(g);
+        s.score = dmalloc<uint4>(g * (uint64_t)sw4());
+        s.gslots = g;
+        if (lc > s.lcap) {
+            dfree(s.L); dfree(s.LXY);
+            s.L = nullptr; s.LXY = nullptr;
+            s.L = dmalloc<unsigned long long>(lc);
+            // an all-ones election word is older than every epoch's (elect_key)
+            HIPCHK(hipMemsetAsync(s.L, 0xFF, lc * 8, stream));
+            s.LXY = dmalloc<ulonglong2>(lc);
+            HIPCHK(hipMemsetAsync(s.LXY, 0, lc * 16, stream));
+            s.lcap = lc;
+            s.lxy_epoch0 = s.epoch;
+        }
+    }
+
     void alloc_shard(Shard &s, int id) {
         s.id = id;
         s.hpar.pool = pool_par.get();
         s.hslot.pool = pool_slot.get();
         HIPCHK(hipEventCreateWithFlags(&s.tev, hipEventDisableTiming));
         s.cnt = dmalloc<uint32_t>(chunk_parents + 1);
-        s.fp = dmalloc<ulonglong2>(Gcap);
-        s.lslot = dmalloc<uint32_t>(Gcap);
         s.wpos = dmalloc<uint32_t>(Gcap + 1);
         HIPCHK(hipMemsetAsync(s.cnt, 0, (chunk_parents + 1) * 4, stream));
-        s.L = dmalloc<unsigned long long>(Lcap_max);
-        // an all-ones election word is older than every epoch's (elect_key)
-        HIPCHK(hipMemsetAsync(s.L, 0xFF, Lcap_max * 8, stream));
-        s.LXY = dmalloc<ulonglong2>(Lcap_max);
-        HIPCHK(hipMemsetAsync(s.LXY, 0, Lcap_max * 16, stream));
-        s.score = dmalloc<uint4>(Gcap * (uint64_t)sw4());
+        // the successor-slot buffers: at their full size on the sharded path, on one GPU sized for
+        // the device loop's levels and grown on demand (ensure_chunk)
+        ensure_chunk(s, multi ? Gcap : dev_parents() * (uint64_t)ks.maxsucc);
         s.wcnt = dmalloc<uint32_t>(chunk_parents + 1);
         s.wacc = dmalloc<uint32_t>(chunk_parents + 1);
         s.pnm = dmalloc<uint32_t>(chunk_parents + 1);
@@ -1049,6 +1076,7 @@ struct rmc_ctx {
 
     void migrate_compact(Shard &s, uint64_t need) {
         const uint64_t local = sh.size();
+        ensure_chunk(s, Gcap);  // the budget below is what the full chunk buffers leave
         HIPCHK(hipStreamSynchronize(stream));
         const uint64_t budget = cfg.seen_mem_bytes ? cfg.seen_mem_bytes : free_device_bytes() / 2 / local;
         const uint64_t slots = budget / 8 / 64 * 64;
@@ -1069,6 +1097,7 @@ struct rmc_ctx {
     // The frontier ring at its budget: rmc_config.frontier_mem_bytes (which may be smaller than the
     // ring so far, down to the live frontier), else 70 % of the free device memory.
     void fix_ring(Shard &s, uint64_t local) {
+        ensure_chunk(s, Gcap);  // the budget below is what the full chunk buffers leave
         const uint64_t live = s.cur_words + s.nxt_words;
         uint64_t words;
         if (cfg.frontier_mem_bytes) {
@@ -1536,7 +1565,7 @@ struct rmc_ctx {
     // `ahead` epochs could reuse a tag still in LXY, clear it (all tags are nonzero).
     void renew_election_tags(Shard &s, uint32_t ahead) {
         if (!s.LXY || s.epoch + ahead - s.lxy_epoch0 < 0xFFFFu) return;
-        HIPCHK(hipMemsetAsync(s.LXY, 0, Lcap_max * 16, stream));
+        HIPCHK(hipMemsetAsync(s.LXY, 0, s.lcap * 16, stream));
         s.lxy_epoch0 = s.epoch;
     }
 
@@ -1579,7 +1608,8 @@ struct rmc_ctx {
                 grow_trace(s, Gub);
                 grow_seen(s, s.T_count + Gub);
             }
-            const uint64_t Lcap = std::min(next_pow2(2 * Gub), Lcap_max);
+            ensure_chunk(s, Gub);
+            const uint64_t Lcap = std::min(next_pow2(2 * Gub), s.lcap);
             renew_election_tags(s, 1);
             ++s.epoch;
             trace_restart(s);
@@ -1705,7 +1735,8 @@ struct rmc_ctx {
         h.cur_n = s.cur_n;
         h.gid_cur = gid0;
         h.T_count = s.T_count;
-        h.Lmask = std::min(next_pow2(2 * s.cur_n * MS), Lcap_max) - 1;
+        ensure_chunk(s, DP * MS);
+        h.Lmask = std::min(next_pow2(2 * s.cur_n * MS), s.lcap) - 1;
         h.cur_wbase = s.cur_wbase;
         h.cur_words = s.cur_words;
         h.off_cap = std::min(s.cur_off_cap, s.nxt_off_cap);
@@ -1714,7 +1745,7 @@ struct rmc_ctx {
         h.trace_cap = s.trace_cap;
         h.T_cap = s.Tc ? (uint64_t)((double)s.T_cap * 1.8) : s.T_cap;  // compact: load <= 0.9
         h.chunk_parents = replicated ? std::min<uint64_t>(DP, shard_min - 1) : DP;  // stop before sharding starts
-        h.Lcap_max = Lcap_max;
+        h.Lcap_max = s.lcap;
         h.level = (uint32_t)L0;
         renew_election_tags(s, K + 1);
         h.epoch = ++s.epoch;
