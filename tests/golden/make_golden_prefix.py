@@ -11,13 +11,17 @@ oracle until `max_states` distinct states and keep only the levels it completed:
 The GPU test (tests/test_gpu.py::test_prefix_levels_match_c_oracle) runs the same configuration
 level by level and compares those prefixes exactly.
 
-usage: python tests/golden/make_golden_prefix.py [--mt THREADS] MAX_STATES n V E R [n V E R ...]
+usage: python tests/golden/make_golden_prefix.py [--mt THREADS | --lean THREADS SEEN_SLOTS] MAX_STATES n V E R [...]
 writes tests/golden/levels_prefix.json (merged with what is there)
 
 --mt runs oracle/raft_mt.c's level-synchronous BFS (the same restatement, same first-wins
 semantics) on THREADS host threads and stops at the first level boundary past MAX_STATES, so
 every reported level is complete (used for the 5-server configs[3], whose exact canonical form
 costs 120 permutations per successor).
+
+--lean runs oracle/raft_prefix.c (same semantics, packed records, seen set of SEEN_SLOTS 16-B slots
+sized once, winners regenerated instead of stored) for Raft.cfg's deep prefix: 35 levels, 984 M
+states, in ~55 GB; it must reproduce the levels already recorded, and adds max |msgs| per level.
 """
 import ctypes
 import json
@@ -79,17 +83,55 @@ def run_prefix_mt(n, V, E, Rr, max_states, threads):
             "source": f"c_mt{threads}", "invariants": ["Inv"], "check_deadlock": False}
 
 
+def run_prefix_lean(n, V, E, Rr, max_states, threads, seen_slots):
+    """oracle/raft_prefix.c: the same level-synchronous first-wins BFS with packed records, a seen set
+    sized once (seen_slots x 16 B) and no stored candidates, for prefixes of ~10^9 states in the
+    build container's memory.  Also records each level's largest |msgs|."""
+    lib = ctypes.CDLL(os.path.join(HERE, "..", "..", "oracle", "build", "libraft_prefix.so"))
+    P64 = ctypes.POINTER(ctypes.c_uint64)
+    lib.orc_prefix_levels.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint64, ctypes.c_uint64, P64, P64,
+                                                           ctypes.POINTER(ctypes.c_int), ctypes.c_int, P64, P64,
+                                                           ctypes.POINTER(ctypes.c_int)]
+    cap = 256
+    d, g, m = (ctypes.c_uint64 * cap)(), (ctypes.c_uint64 * cap)(), (ctypes.c_int * cap)()
+    dist, gen, depth = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+    t = time.time()
+    v = lib.orc_prefix_levels(n, V, E, Rr, threads, max_states, seen_slots, d, g, m, cap, ctypes.byref(dist),
+                              ctypes.byref(gen), ctypes.byref(depth))
+    dt = time.time() - t
+    D = depth.value
+    assert v in (0, 2), f"unexpected verdict {v}"
+    return {"n": n, "V": V, "E": E, "R": Rr, "max_states": max_states, "stopped_at_distinct": dist.value,
+            "exhausted": v == 0, "levels": list(d[:D]), "gen_per_level": list(g[:D if v == 0 else D - 1]),
+            "max_msgs_per_level": list(m[:D]), "max_msgs_seen": max(m[:D]), "oracle_seconds": round(dt, 1),
+            "source": f"c_lean{threads}", "invariants": ["Inv"], "check_deadlock": False}
+
+
 def main():
     args = sys.argv[1:]
-    threads = 0
+    threads = lean = 0
     if args and args[0] == "--mt":
         threads, args = int(args[1]), args[2:]
+    elif args and args[0] == "--lean":  # --lean THREADS SEEN_SLOTS
+        threads, lean, args = int(args[1]), int(args[2]), args[3:]
     max_states = int(args[0])
     a = list(map(int, args[1:]))
     cfgs = [tuple(a[i:i + 4]) for i in range(0, len(a), 4)]
     path = os.environ.get("GOLDEN_PREFIX_OUT", os.path.join(HERE, "levels_prefix.json"))
     for (n, V, E, Rr) in cfgs:
-        r = run_prefix_mt(n, V, E, Rr, max_states, threads) if threads else run_prefix(n, V, E, Rr, max_states)
+        if lean:
+            r = run_prefix_lean(n, V, E, Rr, max_states, threads, lean)
+            old = (json.load(open(path)) if os.path.exists(path) else {}).get(f"n{n}_v{V}_e{E}_r{Rr}")
+            if old:  # the lean run must reproduce the prefix already recorded
+                k = min(len(old["levels"]), len(r["levels"]))
+                assert r["levels"][:k] == old["levels"][:k], "lean prefix disagrees with the recorded one"
+                k = min(len(old["gen_per_level"]), len(r["gen_per_level"]))
+                assert r["gen_per_level"][:k] == old["gen_per_level"][:k], "lean generated counts disagree"
+                r["previous_source"] = old["source"]
+        elif threads:
+            r = run_prefix_mt(n, V, E, Rr, max_states, threads)
+        else:
+            r = run_prefix(n, V, E, Rr, max_states)
         out = json.load(open(path)) if os.path.exists(path) else {}
         out[f"n{n}_v{V}_e{E}_r{Rr}"] = r
         with open(path, "w") as f:

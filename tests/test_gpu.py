@@ -4,6 +4,7 @@ Bit-exact bar: identical successor lists (TLC order, keys and concrete states), 
 symmetry classes, identical invariant values, identical per-level distinct/generated
 counts, depth, verdict and counterexample traces (tests/golden/, from oracle/)."""
 import dataclasses
+import gzip
 import json
 import os
 
@@ -85,6 +86,68 @@ def test_invariants_match_oracle(name):
                 except R.EvalError:
                     exp = None
                 assert mc.eval_invariant(sc["state"], nm) == exp, nm
+
+
+# Deep states (tests/golden/make_golden_deep.py): guided walks from Init to depth 60-86 -- Raft.cfg
+# states with up to 41 messages, configs[3] up to 63 -- plus synthetic states past them, up to the
+# layout's message cap (64 at 3 servers; 122-126 at 4-5 servers: the second message round, MR = 2).
+with gzip.open(os.path.join(GOLDEN, "successors_deep.json.gz"), "rt") as _f:
+    DEEP = json.load(_f)
+INV_NAMES = ["Inv", "NoSplitVote", "RaftCanCommt", "FollowerCanCommit", "CommitAll", "NoAllCommit",
+             "ExistLeaderAndCandidate"]
+
+
+@pytest.mark.parametrize("name", sorted(DEEP))
+def test_deep_successors_match_oracle(name):
+    """Successor lists (TLC order, keys and concrete states) of message-heavy states, and the Assert
+    (tla:185) exactly where both oracles raise it."""
+    g = DEEP[name]
+    mc = checker(g["n"], g["V"], g["E"], g["R"])
+    n_assert = 0
+    for it in g["items"]:
+        if it["assert_fails"]:
+            with pytest.raises(AssertionError, match="split brain"):
+                mc.successors(it["state"])
+            n_assert += 1
+            continue
+        got = mc.successors(it["state"])
+        exp = it["successors"]
+        assert [list(k) for k, _, _ in got] == [e["key"] for e in exp], it["nmsgs"]
+        for (k, st, _), e in zip(got, exp):
+            assert st == e["state"], (k, it["nmsgs"])
+    assert n_assert == g["coverage"]["assert_states"]
+
+
+@pytest.mark.parametrize("name", sorted(DEEP))
+def test_deep_fingerprint_classes_match_oracle(name):
+    """The 128-bit symmetry fingerprint induces the oracles' exact canonical partition on every
+    successor of the deep states (and a permuted copy has its state's fingerprint)."""
+    g = DEEP[name]
+    mc = checker(g["n"], g["V"], g["E"], g["R"])
+    fp_of_canon, canon_of_fp = {}, {}
+    for it in g["items"]:
+        if it["assert_fails"]:
+            continue
+        assert mc.fingerprint(it["state"]) == mc.fingerprint(it["permuted"])
+        for (k, st, fp), e in zip(mc.successors(it["state"]), it["successors"]):
+            assert mc.fingerprint(st) == fp
+            assert fp_of_canon.setdefault(e["canon"], fp) == fp
+            assert canon_of_fp.setdefault(fp, e["canon"]) == e["canon"]
+    assert len(fp_of_canon) == len({e["canon"] for it in g["items"] for e in it.get("successors", [])})
+
+
+@pytest.mark.parametrize("name", sorted(DEEP))
+def test_deep_invariants_match_oracle(name):
+    """Every invariant (tla:434-499; None = TLC evaluation error) on the deep states and their first
+    successors, as both oracles evaluate them."""
+    g = DEEP[name]
+    mc = checker(g["n"], g["V"], g["E"], g["R"])
+    for it in g["items"]:
+        if it["assert_fails"]:
+            continue
+        for tag, vals in it["invariants"].items():
+            st = it["state"] if tag == "state" else it["successors"][int(tag[4:])]["state"]
+            assert [mc.eval_invariant(st, nm) for nm in INV_NAMES] == vals, (tag, it["nmsgs"])
 
 
 def _no_all_commit_state(msgs):

@@ -257,3 +257,41 @@ def test_mt_oracle_levels_match_golden_and_prefix():
         else:
             assert rc == 2 and D < g["depth"] and sum(d[:D]) == dist.value >= max_states
             assert list(d[:D]) == g["levels"][:D] and list(gen[:D - 1]) == g["gen_per_level"][:D - 1]
+
+
+def test_deep_fixture_coverage_and_python_recheck():
+    """successors_deep.json.gz (tests/golden/make_golden_deep.py) covers the message-heavy states
+    the BFS prefixes cannot reach -- Raft.cfg states with more than 30 messages, and 4/5-server
+    states past 64 (the kernels' second message round) -- and every 7th item's successors, classes
+    and invariants still come out of the Python restatement unchanged."""
+    import gzip
+    with gzip.open(os.path.join(GOLDEN, "successors_deep.json.gz"), "rt") as f:
+        deep = json.load(f)
+    cov = {k: v["coverage"] for k, v in deep.items()}
+    assert cov["raftcfg_n3_v2_e3_r3"]["states_over_30_msgs"] >= 50
+    assert cov["raftcfg_n3_v2_e3_r3"]["max_msgs"] >= 40 and cov["raftcfg_n3_v2_e3_r3"]["max_depth"] >= 60
+    assert cov["c4_n5_v1_e3_r3"]["max_msgs"] >= 60
+    assert cov["c4_n5_v1_e3_r3"]["synthetic_states_over_64_msgs"] >= 10
+    names = ["Inv", "NoSplitVote", "RaftCanCommt", "FollowerCanCommit", "CommitAll", "NoAllCommit",
+             "ExistLeaderAndCandidate"]
+    for g in deep.values():
+        cfg = R.Config(n=g["n"], V=g["V"], max_election=g["E"], max_restart=g["R"])
+        canon = {}
+        for it in g["items"][::7]:
+            st = R.state_from_json(it["state"])
+            if it["assert_fails"]:
+                with pytest.raises(R.AssertionFailure):
+                    R.successors(cfg, st)
+                continue
+            succ = R.successors(cfg, st)
+            assert [list(k) for k, _ in succ] == [e["key"] for e in it["successors"]]
+            assert [R.state_to_json(t) for _, t in succ] == [e["state"] for e in it["successors"]]
+            for (_, t), e in zip(succ, it["successors"]):
+                c = R.canonical(cfg, t)
+                assert canon.setdefault(c, e["canon"]) == e["canon"]
+            for nm, v in zip(names, it["invariants"]["state"]):
+                try:
+                    got = R.INV_FUNCS[nm](cfg, st)
+                except R.EvalError:
+                    got = None
+                assert got == v, nm

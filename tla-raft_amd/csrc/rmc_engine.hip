@@ -37,6 +37,7 @@
 
 #include "rmc.h"
 #include "rmc_kernels.h"
+#include "rmc_plan.h"
 #include "rmc_spec.h"
 
 #ifdef RMC_WITH_RCCL
@@ -446,7 +447,7 @@ struct rmc_ctx {
     unsigned long long *d_err1 = nullptr;
     uint32_t *d_flags1 = nullptr;
     unsigned long long *d_red = nullptr, *h_red = nullptr;  // collective scratch (RED_CAP values)
-    static constexpr int RED_CAP = 16 * 64;
+    static constexpr int RED_CAP = 64 * (2 * 64 + 8) + (2 * 64 + 8);  // a W x K gathered count matrix + one row
 
     // progress
     bool inited = false, finished = false;
@@ -719,6 +720,20 @@ struct rmc_ctx {
             throw Fail(RMC_E_ARG, "no compiled kernels for n_servers=" + std::to_string(N) + " n_vals=" +
                                       std::to_string(V) + " msg_cap=" + std::to_string(cap));
         RECW = ks.RECW_MAX;
+        // the sharded election key is (parent's global index << 10) | rank (k_route_place): every
+        // parent's successors must fit the 10-bit rank (BecomeFollower at 5 servers: ~306)
+        if (multi && ks.maxsucc > 1024)
+            throw Fail(RMC_E_ARG, "sharded runs need at most 1024 successor slots per state");
+        if (const char *fi = std::getenv("RMC_FAULT_INJECT")) {  // tests: "site,shard,round[,level]"
+            long long r = -1;
+            int lv = -1;
+            if (std::sscanf(fi, "%d,%d,%lld,%d", &fi_site, &fi_shard, &r, &lv) >= 3) {
+                fi_round = r;
+                fi_level = lv;
+            } else {
+                fi_site = 0;
+            }
+        }
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
             throw Fail(RMC_E_DEVICE, "no HIP device: the model checker runs only on the GPU");
@@ -774,12 +789,13 @@ struct rmc_ctx {
         d_seeds = dmalloc<uint64_t>(seeds.size());
         HIPCHK(hipMemcpy(d_seeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
         // fingerprint scheme identity (checkpoints): seeds, message hashes, record codec, slot hash
-        scheme_hash = 0x5eed5c4e3e000005ull;  // 4: signature-coset minimum for n >= 4; 5: positional slot keys
+        scheme_hash = 0x5eed5c4e3e000006ull;  // 4: signature-coset minimum for n >= 4; 5: positional slot keys; 6: codec of (N, V)
         auto mixin = [&](uint64_t v) { scheme_hash = mix64(scheme_hash ^ (v + 0x9e3779b97f4a7c15ull)); };
         for (uint64_t s : seeds) mixin(s);
         for (const ulonglong2 &g : U.gmsg) { mixin(g.x); mixin(g.y); }
         mixin((uint64_t)ks.CCW);
-        mixin((uint64_t)Codec<3, 2>::BITS);
+        mixin((uint64_t)codec_bits(N, V));  // the instance's packed layout (field widths below)
+        for (int w : {bits_for(N), bits_for(V + 1), bits_for(V + 2), bits_for(V - 1)}) mixin((uint64_t)w);
 
         // successor slots per chunk: dense for the sharded path, sparse (parents x maxsucc) for
         // the fused single-GPU path, whose staging holds SW4 * 16 + 36 bytes per slot
@@ -1219,53 +1235,77 @@ struct rmc_ctx {
 #endif
     }
 
-    // counts: c_out[local d][s] = c_in[local s][d]
-    void exchange_counts(const std::vector<std::vector<uint64_t>> &in, std::vector<std::vector<uint64_t>> &out) {
-        out.assign(sh.size(), std::vector<uint64_t>(W, 0));
+    // Every shard's row of K values on every rank: rows[li] = sh[li]'s row in, the W x K matrix
+    // (row t = shard t) out.  One ncclAllGather through RCCL; virtual shards are all local.
+    std::vector<uint64_t> gather_rows(const std::vector<std::vector<uint64_t>> &rows, int K) {
+        std::vector<uint64_t> M((size_t)W * K, 0);
         if (!rccl) {
-            for (int s = 0; s < W && s < (int)in.size(); s++)
-                for (int d = 0; d < (int)sh.size(); d++) out[d][s] = in[s][d];
-            return;
+            for (size_t li = 0; li < sh.size(); li++)
+                std::copy(rows[li].begin(), rows[li].end(), M.begin() + (size_t)sh[li].id * K);
+            return M;
         }
 #ifdef RMC_WITH_RCCL
-        for (int d = 0; d < W; d++) h_red[d] = in[0][d];
-        HIPCHK(hipMemcpyAsync(d_red, h_red, W * 8, hipMemcpyHostToDevice, stream));
-        if (ncclAllToAll(d_red, d_red + 64, 1, ncclUint64, comm, stream) != ncclSuccess)
-            throw Fail(RMC_E_COMM, "ncclAllToAll failed");
-        HIPCHK(hipMemcpyAsync(h_red, d_red + 64, W * 8, hipMemcpyDeviceToHost, stream));
+        if ((size_t)W * K + K > (size_t)RED_CAP) throw Fail(RMC_E_ARG, "gather_rows: matrix exceeds the collective scratch");
+        for (int k = 0; k < K; k++) h_red[k] = rows[0][k];
+        HIPCHK(hipMemcpyAsync(d_red, h_red, K * 8, hipMemcpyHostToDevice, stream));
+        if (ncclAllGather(d_red, d_red + K, K, ncclUint64, comm, stream) != ncclSuccess)
+            throw Fail(RMC_E_COMM, "ncclAllGather failed");
+        HIPCHK(hipMemcpyAsync(h_red + K, d_red + K, (size_t)W * K * 8, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
-        for (int s = 0; s < W; s++) out[0][s] = h_red[s];
+        std::copy(h_red + K, h_red + K + (size_t)W * K, M.begin());
 #endif
+        return M;
     }
 
-    // alltoallv of fixed-size items: send[local s] segment d (cnt scnt[s][d] at soff[s][d]) ->
-    // recv[local d] segment s (at roff[d][s]).
-    void exchange_items(const std::vector<const void *> &send, const std::vector<std::vector<uint64_t>> &scnt,
-                        const std::vector<std::vector<uint64_t>> &soff, const std::vector<void *> &recv,
-                        const std::vector<std::vector<uint64_t>> &roff, size_t elem) {
+    // One or more all-to-all-v payloads of fixed-size items, by the plans of rmc_plan.h
+    // (plans[li] = sh[li]'s; P[k] the k-th payload): virtual shards copy every transfer on the
+    // device, an RCCL rank posts one send and one receive per peer and payload, all in one group.
+    struct Payload {
+        const std::vector<XPlan> *plans;
+        std::vector<const void *> send;
+        std::vector<void *> recv;
+        size_t elem;
+    };
+    void exchange(const std::vector<Payload> &P) {
         if (!rccl) {
-            for (int s = 0; s < W; s++)
-                for (int d = 0; d < W; d++) {
-                    const uint64_t n = scnt[s][d];
-                    if (!n) continue;
-                    HIPCHK(hipMemcpyAsync((char *)recv[d] + roff[d][s] * elem, (const char *)send[s] + soff[s][d] * elem,
-                                          n * elem, hipMemcpyDeviceToDevice, stream));
-                }
+            for (const Payload &p : P)
+                for (const Xfer &x : transfers(*p.plans))
+                    HIPCHK(hipMemcpyAsync((char *)p.recv[x.to] + x.dst_off * p.elem,
+                                          (const char *)p.send[x.from] + x.src_off * p.elem, x.n * p.elem,
+                                          hipMemcpyDeviceToDevice, stream));
             return;
         }
 #ifdef RMC_WITH_RCCL
-        // recv counts are the transposed send counts, known to the caller through roff
         if (ncclGroupStart() != ncclSuccess) throw Fail(RMC_E_COMM, "ncclGroupStart failed");
-        for (int peer = 0; peer < W; peer++) {
-            const uint64_t ns = scnt[0][peer];
-            const uint64_t nr = roff[0][peer + 1] - roff[0][peer];
-            if (ns && ncclSend((const char *)send[0] + soff[0][peer] * elem, ns * elem, ncclUint8, peer, comm, stream) != ncclSuccess)
-                throw Fail(RMC_E_COMM, "ncclSend failed");
-            if (nr && ncclRecv((char *)recv[0] + roff[0][peer] * elem, nr * elem, ncclUint8, peer, comm, stream) != ncclSuccess)
-                throw Fail(RMC_E_COMM, "ncclRecv failed");
+        for (const Payload &p : P) {
+            const XPlan &x = (*p.plans)[0];
+            for (int peer = 0; peer < W; peer++) {
+                const uint64_t ns = x.send_cnt[peer], nr = x.recv_cnt[peer];
+                if (ns && ncclSend((const char *)p.send[0] + x.send_off[peer] * p.elem, ns * p.elem, ncclUint8, peer,
+                                   comm, stream) != ncclSuccess)
+                    throw Fail(RMC_E_COMM, "ncclSend failed");
+                if (nr && ncclRecv((char *)p.recv[0] + x.recv_off[peer] * p.elem, nr * p.elem, ncclUint8, peer, comm,
+                                   stream) != ncclSuccess)
+                    throw Fail(RMC_E_COMM, "ncclRecv failed");
+            }
         }
         if (ncclGroupEnd() != ncclSuccess) throw Fail(RMC_E_COMM, "ncclGroupEnd failed");
 #endif
+    }
+
+    // Fault injection (tests only, RMC_FAULT_INJECT="site,shard,round[,level]"): the allocation at
+    // `site` of the sharded round fails on that shard, as a full device would make it fail.  Sites:
+    // 1 send buffer, 2 receive buffer, 3 owner (seen set / election table), 4 outbox, 5 regrouped
+    // winners, 6 winner inbox, 7 next-level append (ring, offsets, trace, scan scratch),
+    // 8 entering the sharded layout.  Every shard must then stop with RMC_E_MEMORY in the same round.
+    int fi_site = 0, fi_shard = -1, fi_level = -1;
+    int64_t fi_round = -1;
+    void inject(int site, int shard, uint64_t round, int level) const {
+        if (site == fi_site && shard == fi_shard && (int64_t)round == fi_round && (fi_level < 0 || level == fi_level))
+            throw Fail(RMC_E_MEMORY, "injected allocation failure (RMC_FAULT_INJECT site " + std::to_string(site) + ")");
+    }
+    bool injecting(int site, int shard, uint64_t round, int level) const {
+        return site == fi_site && shard == fi_shard && (int64_t)round == fi_round && (fi_level < 0 || level == fi_level);
     }
 
     // successors of one record already in d_one: keys + records in d_out
@@ -1437,7 +1477,18 @@ struct rmc_ctx {
         rmc_level_stats local;
         if (!st) st = &local;
         std::memset(st, 0, sizeof *st);
-        if (replicated && sh[0].cur_n >= shard_min) enter_sharded();
+        if (replicated && sh[0].cur_n >= shard_min) {
+            // a failure here is this rank's alone: it is held and agreed at the sharded level's
+            // first collective, so no rank waits in it for a peer that already left
+            try {
+                inject(8, sh[0].id, 0, (int)sh[0].level_start.size());
+                enter_sharded();
+            } catch (const Fail &e) {
+                pending_fail = e.code;
+                pending_msg = e.msg;
+                replicated = false;
+            }
+        }
         return (!multi || replicated) ? step_single(st) : step_sharded(st);
     }
 
@@ -1546,6 +1597,8 @@ struct rmc_ctx {
         replicated = false;
     }
     uint64_t *old_off_ = nullptr;
+    int pending_fail = 0;  // a failure entering the sharded layout, agreed at the next level's start
+    std::string pending_msg;
 
     // First error in TLC order among the error slots: smaller (parent, slot) first; on a
     // tie the Assert wins (its sub-action's batch is discarded).
@@ -2061,18 +2114,19 @@ struct rmc_ctx {
         uint64_t Fg = 0;
         for (Shard &s : sh) { Fg += s.cur_n; s.nxt_n = 0; s.nxt_words = 0; }
         allreduce(&Fg, 1, false);
+        {
+            uint64_t pend = (uint64_t)(-pending_fail);
+            allreduce(&pend, 1, true);
+            if (pend) {
+                const std::string m = pending_fail ? pending_msg : "another rank failed entering the sharded layout";
+                pending_fail = 0;
+                throw Fail(-(int)pend, m);
+            }
+        }
         st->expanded = Fg;
         const uint64_t gbase = glevel[L - 1], rounds = (Fg + B * W - 1) / (B * W);
         const size_t NL = sh.size();
         uint64_t level_gen = 0, level_new = 0, level_words = 0;
-        using VV = std::vector<std::vector<uint64_t>>;
-        auto prefix = [](const std::vector<uint64_t> &c) {
-            std::vector<uint64_t> o(c.size() + 1, 0);
-            for (size_t i = 0; i < c.size(); i++) o[i + 1] = o[i] + c[i];
-            return o;
-        };
-        std::vector<const void *> sp(NL);
-        std::vector<void *> rp(NL);
         // A shard that runs out of seen-set or ring room, or meets a state past msg_cap, must not
         // leave the others waiting in a collective: it records the failure, skips its own kernels
         // and keeps exchanging; the round's table (and a last check at the round's end) carries the
@@ -2092,40 +2146,91 @@ struct rmc_ctx {
             if (!worst) return;
             throw Fail(-(int)worst, fail_msg.empty() ? std::string("another shard failed (see its rank's error)") : fail_msg);
         };
+        // failure agreement: a shard that fails (allocation, capacity) records it and keeps taking
+        // part in every exchange; the next gathered matrix / all-reduce carries the failure to every
+        // rank and all of them raise it together (agree).  Receive buffers grow before their payload
+        // moves, decided from the gathered counts and capacities the same way on every rank, followed
+        // by one extra all-reduce only in the rounds where some shard grows.
+        auto col_max = [&](const std::vector<uint64_t> &M, int K, int col) {
+            uint64_t m = 0;
+            for (int t = 0; t < W; t++) m = std::max(m, M[(size_t)t * K + col]);
+            return m;
+        };
+        auto local_worst = [&] {
+            uint64_t m = 0;
+            for (size_t li = 0; li < NL; li++) m = std::max(m, (uint64_t)(-fail[li]));
+            return m;
+        };
+        auto agree_now = [&] {  // one all-reduce of the worst failure
+            uint64_t worst = local_worst();
+            allreduce(&worst, 1, true);
+            agree(worst);
+        };
+        std::vector<uint64_t> hoff_buf;  // piece boundaries read back in one copy per round
         for (uint64_t c = 0; c < rounds; c++) {
             // (1) expand the round's block: fingerprints, staged rows; successors per owner
-            VV scnt(NL, std::vector<uint64_t>(W, 0)), rcnt, soff(NL), roff(NL);
-            for (Shard &s : sh) {
+            for (size_t li = 0; li < NL; li++) {
+                Shard &s = sh[li];
                 s.p0 = c * B;
                 s.np = s.cur_n > s.p0 ? std::min<uint64_t>(B, s.cur_n - s.p0) : 0;
                 s.gblk = (c * (uint64_t)W + (uint64_t)s.id) * B;
                 HIPCHK(hipMemsetAsync(s.ocnt, 0, 64 * 4, stream));
                 HIPCHK(hipMemsetAsync(s.sum + 9, 0, 8, stream));
-                if (!s.np) continue;
+                if (!s.np || fail[li]) continue;
                 timed(PH_HASH, [&] { ks.fused(round_params(s, gbase), stream); });
                 launch_route_count(s.fp, s.cnt, s.np, (uint32_t)MS, (uint32_t)W, s.ocnt, stream);
             }
+            // gathered row per shard: its successors per owner, its receive capacity, its failure
+            const int K1 = W + 2;
+            std::vector<std::vector<uint64_t>> rows(NL, std::vector<uint64_t>(K1, 0));
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
                 HIPCHK(hipMemcpyAsync(s.hsum, s.ocnt, 64 * 4, hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
                 const uint32_t *hc = reinterpret_cast<const uint32_t *>(s.hsum);
-                for (int d = 0; d < W; d++) scnt[li][d] = hc[d];
-                soff[li] = prefix(scnt[li]);
-                s.G = soff[li][W];
+                s.G = 0;
+                for (int d = 0; d < W; d++) { rows[li][d] = hc[d]; s.G += hc[d]; }
+                guard(li, [&] {
+                    inject(1, s.id, c, L);
+                    if (s.G) grow_plain(s.xs, s.xs_cap, s.G);
+                });
+                rows[li][W] = injecting(2, s.id, c, L) ? 0 : s.xr_cap;  // site 2 forces this shard to grow
+                rows[li][W + 1] = (uint64_t)(-fail[li]);
             }
             collect_times(st);
-            exchange_counts(scnt, rcnt);
+            std::vector<uint64_t> M = gather_rows(rows, K1);
+            agree(col_max(M, K1, W + 1));
+            {
+                std::vector<uint64_t> need(W, 0), cap(W, 0);
+                for (int o = 0; o < W; o++) {
+                    for (int t = 0; t < W; t++) need[o] += M[(size_t)t * K1 + o];
+                    cap[o] = M[(size_t)o * K1 + W];
+                }
+                if (!must_grow(need, cap).empty()) {
+                    for (size_t li = 0; li < NL; li++) {
+                        const int id = sh[li].id;
+                        if (need[id] + 1 > cap[id])
+                            guard(li, [&] {
+                                inject(2, id, c, L);
+                                grow_recv(sh[li], need[id]);
+                            });
+                    }
+                    agree_now();
+                }
+            }
+            std::vector<XPlan> xp(NL), xb(NL);
+            for (size_t li = 0; li < NL; li++) {
+                xp[li] = make_plan(M.data(), W, K1, sh[li].id);
+                xb[li] = reverse_plan(xp[li]);
+            }
             SDBG("0");
             // (2) successors to their owners: owner-grouped items, cursors preset to the groups
+            Payload items{&xp, std::vector<const void *>(NL), std::vector<void *>(NL), sizeof(XItem)};
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
-                roff[li] = prefix(rcnt[li]);
-                grow_recv(s, roff[li][W]);
                 if (s.G) {
-                    grow_plain(s.xs, s.xs_cap, s.G);
                     uint32_t *hc = reinterpret_cast<uint32_t *>(s.hsum);
-                    for (int d = 0; d < W; d++) hc[d] = (uint32_t)soff[li][d];
+                    for (int d = 0; d < W; d++) hc[d] = (uint32_t)xp[li].send_off[d];
                     HIPCHK(hipMemcpyAsync(s.ocnt, hc, W * 4, hipMemcpyHostToDevice, stream));
                     timed(PH_XCHG, [&] {
                         launch_route_place(s.fp, s.cnt, s.np, (uint32_t)MS, (uint32_t)W, s.ocnt, s.gblk, s.xs, s.perm,
@@ -2133,20 +2238,22 @@ struct rmc_ctx {
                     });
                     HIPCHK(hipStreamSynchronize(stream));  // hsum is reused below
                 }
-                sp[li] = s.xs;
-                rp[li] = s.xr;
+                items.send[li] = s.xs;
+                items.recv[li] = s.xr;
             }
             SDBG("1");
-            timed(PH_XCHG, [&] { exchange_items(sp, scnt, soff, rp, roff, sizeof(XItem)); });
+            timed(PH_XCHG, [&] { exchange({items}); });
             SDBG("2");
             // (3) owners: seen-set probe, smallest key per new fingerprint, verdicts, seen-set insert
+            Payload verdicts{&xb, std::vector<const void *>(NL), std::vector<void *>(NL), 4};
             for (size_t li = 0; li < NL; li++) {
                 Shard &o = sh[li];
-                const uint64_t R = roff[li][W];
-                sp[li] = o.rflag;
-                rp[li] = o.sflag;
+                const uint64_t R = xp[li].recv_total;
+                verdicts.send[li] = o.rflag;
+                verdicts.recv[li] = o.sflag;
                 if (!R) continue;
                 guard(li, [&] {
+                    inject(3, o.id, c, L);
                     grow_seen(o, o.T_count + R);
                     const uint64_t cap = owner_table(o, R);
                     timed(PH_DEDUP, [&] {
@@ -2154,13 +2261,16 @@ struct rmc_ctx {
                         launch_owner_flags(o.xr, R, o.rslot, o.OK, o.seen(), o.rflag, o.sum + 9, stream);
                     });
                 });
+                // a failed owner answers "no winner" everywhere (the round is abandoned at the next agreement)
+                if (fail[li]) HIPCHK(hipMemsetAsync(o.rflag, 0, R * 4, stream));
             }
             SDBG("3");
-            timed(PH_XCHG, [&] { exchange_items(sp, rcnt, roff, rp, soff, 4); });
+            timed(PH_XCHG, [&] { exchange({verdicts}); });
             SDBG("4");
             // (4) sources: verdicts on the slots, winners per parent and their words
-            for (Shard &s : sh) {
-                if (!s.np) continue;
+            for (size_t li = 0; li < NL; li++) {
+                Shard &s = sh[li];
+                if (!s.np || fail[li]) continue;
                 timed(PH_DEDUP, [&] {
                     launch_scatter_win(s.perm, s.sflag, s.G, s.score, (uint32_t)sw4(), s.pnm, (uint32_t)MS, s.lslot,
                                        s.wacc, stream);
@@ -2175,7 +2285,7 @@ struct rmc_ctx {
                 HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 10 * 8, hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
                 ins[li] = s.hsum[9];
-                if (s.np) {
+                if (s.np && !fail[li]) {
                     tab[TAB * s.id + 0] = s.hsum[0];
                     wnum[li] = s.hsum[1];
                     wwords[li] = s.hsum[SUM_WORDS];
@@ -2188,6 +2298,7 @@ struct rmc_ctx {
                 Shard &s = sh[li];
                 if (!s.np) continue;
                 guard(li, [&] {
+                    inject(4, s.id, c, L);
                     grow_outbox(s, wwords[li], wnum[li]);
                     if (wwords[li] >= s.rcap) ensure_ring(s, wwords[li], 0);  // P.rcap also bounds the outbox
                     timed(PH_MAT, [&] { ks.commit(round_params(s, gbase), stream); });
@@ -2196,7 +2307,7 @@ struct rmc_ctx {
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
                 s.T_count += ins[li];
-                if (!s.np) continue;
+                if (!s.np || fail[li]) continue;
                 HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
                 HIPCHK(hipGetLastError());
@@ -2205,7 +2316,6 @@ struct rmc_ctx {
                     fail_msg = "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages";
                 }
                 uint64_t *row = &tab[TAB * s.id];
-                row[6] = (uint64_t)(-fail[li]);
                 row[1] = wnum[li];
                 row[2] = wwords[li];
                 row[3] = ins[li];
@@ -2239,97 +2349,146 @@ struct rmc_ctx {
                 return status;
             }
             SDBG("8");
-            // (7) winners to the shards owning their global next-level indices
+            // (7) winners to the shards owning their global next-level indices (rmc_plan.h route_pieces)
             std::vector<uint64_t> A(W + 1, level_new);
             for (int t = 0; t < W; t++) A[t + 1] = A[t] + tab[TAB * t + 1];
-            VV pc(NL, std::vector<uint64_t>(W, 0)), pw(NL, std::vector<uint64_t>(W, 0)), pco(NL), pwo(NL), rpc, rpw;
-            std::vector<const void *> sps(NL), spw(NL);
-            std::vector<void *> rps(NL), rpw_(NL);
+            std::vector<std::vector<Piece>> pcs(NL);
+            std::vector<PieceLayout> lay(NL);
+            std::vector<std::vector<uint64_t>> pw0(NL), pw1(NL);  // word range of each piece
+            {
+                // every piece boundary of every local shard in one copy back (pinned scratch)
+                size_t nb = 0;
+                for (size_t li = 0; li < NL; li++) {
+                    const Shard &s = sh[li];
+                    pcs[li] = route_pieces(A[s.id], A[s.id + 1] - A[s.id], B, W);
+                    nb += pcs[li].size();
+                }
+                if (nb > (size_t)RED_CAP) throw Fail(RMC_E_ARG, "too many winner pieces in a round");
+                size_t k = 0;
+                for (size_t li = 0; li < NL; li++)
+                    for (const Piece &pe : pcs[li])
+                        HIPCHK(hipMemcpyAsync(h_red + k++, sh[li].ooff + pe.i0, 8, hipMemcpyDeviceToHost, stream));
+                if (nb) HIPCHK(hipStreamSynchronize(stream));
+                k = 0;
+                for (size_t li = 0; li < NL; li++) {
+                    const uint64_t w = A[sh[li].id + 1] - A[sh[li].id];
+                    pw0[li].resize(pcs[li].size());
+                    pw1[li].resize(pcs[li].size());
+                    for (size_t q = 0; q < pcs[li].size(); q++) pw0[li][q] = h_red[k++];
+                    for (size_t q = 0; q < pcs[li].size(); q++)
+                        pw1[li][q] = pcs[li][q].i1 < w ? pw0[li][q + 1] : wwords[li];
+                }
+            }
+            const int K2 = 2 * W + 3;
+            std::vector<std::vector<uint64_t>> rows2(NL, std::vector<uint64_t>(K2, 0));
+            std::vector<std::vector<uint64_t>> wlay(NL, std::vector<uint64_t>(W, 0));  // word offsets per destination
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
-                const uint64_t x0 = A[s.id], w = A[s.id + 1] - x0;
-                pco[li].assign(W, 0);
-                pwo[li].assign(W, 0);
-                sps[li] = s.oside;
-                spw[li] = s.ob;
-                if (!w) continue;
-                struct Piece { int d; uint64_t i0, i1, w0, w1; };
-                std::vector<Piece> pcs;
-                std::vector<int> seen_d(W, 0);
-                bool repeat = false;
-                for (uint64_t x = x0; x < x0 + w;) {
-                    const uint64_t b = x / B, y = std::min(x0 + w, (b + 1) * B);
-                    const int d = (int)(b % (uint64_t)W);
-                    repeat |= seen_d[d]++ > 0;
-                    pcs.push_back({d, x - x0, y - x0, 0, 0});
-                    x = y;
-                }
-                for (Piece &pe : pcs) {
-                    pe.w0 = d2h(s.ooff + pe.i0);
-                    pe.w1 = pe.i1 < w ? d2h(s.ooff + pe.i1) : wwords[li];
-                    pc[li][pe.d] += pe.i1 - pe.i0;
-                    pw[li][pe.d] += pe.w1 - pe.w0;
-                }
-                if (!repeat) {
-                    for (const Piece &pe : pcs) { pco[li][pe.d] = pe.i0; pwo[li][pe.d] = pe.w0; }
-                } else {
+                const uint64_t w = A[s.id + 1] - A[s.id];
+                lay[li] = piece_layout(pcs[li], W);
+                std::vector<uint64_t> pwc(W, 0);
+                for (size_t q = 0; q < pcs[li].size(); q++) pwc[pcs[li][q].d] += pw1[li][q] - pw0[li][q];
+                if (w && !lay[li].regroup) {
+                    for (size_t q = 0; q < pcs[li].size(); q++) wlay[li][pcs[li][q].d] = pw0[li][q];
+                } else if (w) {
                     // a destination owns several of the pieces: group them (in order) by destination
-                    grow_inbox(s, wwords[li], w);  // the inbox holds the grouped copy until the exchange
-                    uint64_t at = 0, wat = 0;
-                    for (int d = 0; d < W; d++) {
-                        pco[li][d] = at;
-                        pwo[li][d] = wat;
-                        for (const Piece &pe : pcs) {
-                            if (pe.d != d) continue;
-                            HIPCHK(hipMemcpyAsync(s.iside + at, s.oside + pe.i0, (pe.i1 - pe.i0) * 16,
-                                                  hipMemcpyDeviceToDevice, stream));
-                            HIPCHK(hipMemcpyAsync(s.ib + wat, s.ob + pe.w0, (pe.w1 - pe.w0) * 4, hipMemcpyDeviceToDevice,
-                                                  stream));
-                            at += pe.i1 - pe.i0;
-                            wat += pe.w1 - pe.w0;
-                        }
-                    }
-                    // the grouped copy goes out of the outbox buffers (the inbox is refilled below)
-                    HIPCHK(hipMemcpyAsync(s.oside, s.iside, w * 16, hipMemcpyDeviceToDevice, stream));
-                    HIPCHK(hipMemcpyAsync(s.ob, s.ib, wwords[li] * 4, hipMemcpyDeviceToDevice, stream));
-                    HIPCHK(hipStreamSynchronize(stream));
+                    uint64_t wat = 0;
+                    for (int d = 0; d < W; d++) { wlay[li][d] = wat; wat += pwc[d]; }
+                    guard(li, [&] {
+                        inject(5, s.id, c, L);
+                        grow_inbox(s, wwords[li], w);  // the inbox holds the grouped copy until the exchange
+                        uint64_t at = 0;
+                        wat = 0;
+                        for (int d = 0; d < W; d++)
+                            for (size_t q = 0; q < pcs[li].size(); q++) {
+                                const Piece &pe = pcs[li][q];
+                                if (pe.d != d) continue;
+                                HIPCHK(hipMemcpyAsync(s.iside + at, s.oside + pe.i0, (pe.i1 - pe.i0) * 16,
+                                                      hipMemcpyDeviceToDevice, stream));
+                                HIPCHK(hipMemcpyAsync(s.ib + wat, s.ob + pw0[li][q], (pw1[li][q] - pw0[li][q]) * 4,
+                                                      hipMemcpyDeviceToDevice, stream));
+                                at += pe.i1 - pe.i0;
+                                wat += pw1[li][q] - pw0[li][q];
+                            }
+                        // the grouped copy goes out of the outbox buffers (the inbox is refilled below)
+                        HIPCHK(hipMemcpyAsync(s.oside, s.iside, w * 16, hipMemcpyDeviceToDevice, stream));
+                        HIPCHK(hipMemcpyAsync(s.ob, s.ib, wwords[li] * 4, hipMemcpyDeviceToDevice, stream));
+                        HIPCHK(hipStreamSynchronize(stream));
+                    });
                 }
+                for (int d = 0; d < W; d++) {
+                    rows2[li][d] = lay[li].cnt[d];
+                    rows2[li][W + d] = pwc[d];
+                }
+                const bool force = injecting(6, s.id, c, L);  // site 6 forces this shard's inbox to grow
+                rows2[li][2 * W] = force ? 0 : s.is_cap;
+                rows2[li][2 * W + 1] = force ? 0 : s.ib_cap;
+                rows2[li][2 * W + 2] = (uint64_t)(-fail[li]);
             }
             SDBG("9");
-            exchange_counts(pc, rpc);
-            exchange_counts(pw, rpw);
-            VV rro(NL), rrw(NL);
-            for (size_t li = 0; li < NL; li++) {
-                Shard &o = sh[li];
-                rro[li] = prefix(rpc[li]);
-                rrw[li] = prefix(rpw[li]);
-                grow_inbox(o, rrw[li][W], rro[li][W]);
-                rps[li] = o.iside;
-                rpw_[li] = o.ib;
+            std::vector<uint64_t> M2 = gather_rows(rows2, K2);
+            agree(col_max(M2, K2, 2 * W + 2));
+            {
+                std::vector<uint64_t> need_n(W, 0), need_w(W, 0), cap_n(W, 0), cap_w(W, 0);
+                for (int o = 0; o < W; o++) {
+                    for (int t = 0; t < W; t++) {
+                        need_n[o] += M2[(size_t)t * K2 + o];
+                        need_w[o] += M2[(size_t)t * K2 + W + o];
+                    }
+                    cap_n[o] = M2[(size_t)o * K2 + 2 * W];
+                    cap_w[o] = M2[(size_t)o * K2 + 2 * W + 1];
+                }
+                if (!must_grow(need_n, cap_n).empty() || !must_grow(need_w, cap_w).empty()) {
+                    for (size_t li = 0; li < NL; li++) {
+                        const int id = sh[li].id;
+                        if (need_n[id] + 1 > cap_n[id] || need_w[id] + 1 > cap_w[id])
+                            guard(li, [&] {
+                                inject(6, id, c, L);
+                                grow_inbox(sh[li], need_w[id], need_n[id]);
+                            });
+                    }
+                    agree_now();
+                }
             }
-            timed(PH_XCHG, [&] {
-                exchange_items(sps, pc, pco, rps, rro, 16);
-                exchange_items(spw, pw, pwo, rpw_, rrw, 4);
-            });
+            std::vector<XPlan> xs_(NL), xw_(NL);
+            Payload sides{&xs_, std::vector<const void *>(NL), std::vector<void *>(NL), 16};
+            Payload words_{&xw_, std::vector<const void *>(NL), std::vector<void *>(NL), 4};
+            for (size_t li = 0; li < NL; li++) {
+                Shard &s = sh[li];
+                xs_[li] = make_plan(M2.data(), W, K2, s.id);
+                xw_[li] = make_plan(M2.data() + W, W, K2, s.id);
+                for (int d = 0; d < W; d++) {  // the send layout: pieces in place, or regrouped
+                    xs_[li].send_off[d] = lay[li].off[d];
+                    xw_[li].send_off[d] = wlay[li][d];
+                }
+                sides.send[li] = s.oside;
+                words_.send[li] = s.ob;
+                sides.recv[li] = s.iside;
+                words_.recv[li] = s.ib;
+            }
+            timed(PH_XCHG, [&] { exchange({sides, words_}); });
             SDBG("10");
             // (8) owners append what they received, in source order, to the next level
             for (size_t li = 0; li < NL; li++) {
                 Shard &o = sh[li];
-                const uint64_t n = rro[li][W], words = rrw[li][W];
+                const uint64_t n = xs_[li].recv_total, words = xw_[li].recv_total;
                 if (!n) continue;
                 uint64_t consumed = 0;
                 if (o.ring_fixed) {
                     const uint64_t done = std::min(o.cur_n, (c + 1) * B);
                     consumed = done < o.cur_n ? d2h(o.cur_off + done) : o.cur_words;
                 }
-                guard(li, [&] { ensure_ring(o, words, consumed); });
+                guard(li, [&] {
+                    inject(7, o.id, c, L);
+                    ensure_ring(o, words, consumed);
+                    ensure_off(o.nxt_off, o.nxt_off_cap, o.nxt_n, o.nxt_n + n);
+                    grow_trace(o, n);
+                    ensure_tmp(o, n + 1);
+                });
                 if (fail[li]) continue;
-                ensure_off(o.nxt_off, o.nxt_off_cap, o.nxt_n, o.nxt_n + n);
                 const uint64_t gid = o.level_start[L - 1] + o.cur_n + o.nxt_n;  // local gid of the first
-                grow_trace(o, n);
                 trace_restart(o);
                 trace_fence(o);
-                ensure_tmp(o, n + 1);
                 timed(PH_OTHER, [&] {
                     ring_copy_in(o, ring_wrap(o.nbase() + o.nxt_words, o.rcap), o.ib, words);
                     launch_side_sizes(o.iside, n, o.isz, stream);
@@ -2343,12 +2502,9 @@ struct rmc_ctx {
                 o.nxt_words += words;
             }
             SDBG("11");
-            {
-                uint64_t worst = 0;
-                for (size_t li = 0; li < NL; li++) worst = std::max(worst, (uint64_t)(-fail[li]));
-                allreduce(&worst, 1, true);
-                agree(worst);
-            }
+            // an append failure rides on the next round's gathered matrix; after the level's last
+            // round it is agreed here
+            if (c + 1 == rounds) agree_now();
             for (int t = 0; t < W; t++) {
                 level_gen += tab[TAB * t + 0];
                 level_new += tab[TAB * t + 1];
@@ -2514,7 +2670,7 @@ struct rmc_ctx {
         uint32_t epoch, pad;
         uint64_t T_cap, T_count, cur_n, cur_words, n_levels, trace_n;
     };
-    static constexpr uint64_t CKPT_MAGIC = 0x3350434b434d52ull;  // "RMCKCP3"
+    static constexpr uint64_t CKPT_MAGIC = 0x3450434b434d52ull;  // "RMCKCP4": data checksums
 
     CkptHeader ckpt_header() const {
         CkptHeader h{};
@@ -2542,6 +2698,22 @@ struct rmc_ctx {
         return x;
     }
     static uint64_t header_check(const CkptHeader &h) { return fnv(h, offsetof(CkptHeader, check)); }
+    // checksum of a shard's data sections (seen set, ring words, offsets, trace), 8 bytes at a time:
+    // fast enough for a 150 GB checkpoint, and a corrupt or mismatched section fails resume
+    struct DataSum {
+        uint64_t h = 0x6a09e667f3bcc909ull;
+        void add(const void *p, size_t k) {
+            const unsigned char *b = static_cast<const unsigned char *>(p);
+            size_t i = 0;
+            for (; i + 8 <= k; i += 8) {
+                uint64_t w;
+                std::memcpy(&w, b + i, 8);
+                h = (h ^ w) * 0x9e3779b97f4a7c15ull;
+                h ^= h >> 29;
+            }
+            for (; i < k; i++) h = (h ^ b[i]) * 0x100000001b3ull;
+        }
+    };
     std::string ckpt_path(const char *path) const {
         return (rccl && W > 1) ? std::string(path) + ".rank" + std::to_string(rank) : std::string(path);
     }
@@ -2588,14 +2760,17 @@ struct rmc_ctx {
         if (!f) throw Fail(RMC_E_ARG, std::string("checkpoint: cannot write ") + tmp);
         bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 &&
                   std::fwrite(glevel.data(), 8, h.n_glevel, f) == h.n_glevel;
+        DataSum sum;
         auto out = [&](void *dev, char *host, size_t k) {
             HIPCHK(hipMemcpy(host, dev, k, hipMemcpyDeviceToHost));
+            sum.add(host, k);
             ok = ok && std::fwrite(host, 1, k, f) == k;
         };
         for (size_t i = 0; ok && i < sh.size(); i++) {
             Shard &t = sh[i];
             const CkptShard &c = sc[i];
             const uint64_t chk = fnv(c, sizeof c);
+            sum = DataSum{};
             ok = std::fwrite(&c, sizeof c, 1, f) == 1 && std::fwrite(&chk, 8, 1, f) == 1 &&
                  std::fwrite(t.level_start.data(), 8, c.n_levels, f) == c.n_levels;
             if (t.Tc) stream_bytes(t.Tc, c.T_cap * 8, out);
@@ -2607,8 +2782,15 @@ struct rmc_ctx {
             stream_bytes(lin, c.cur_words * 4, out);
             dfree(lin);
             stream_bytes(t.cur_off, c.cur_n * 8, out);
-            t.hpar.for_range(0, c.trace_n, [&](const uint64_t *p, uint64_t k) { ok = ok && std::fwrite(p, 8, k, f) == k; });
-            t.hslot.for_range(0, c.trace_n, [&](const uint16_t *p, uint64_t k) { ok = ok && std::fwrite(p, 2, k, f) == k; });
+            t.hpar.for_range(0, c.trace_n, [&](const uint64_t *p, uint64_t k) {
+                sum.add(p, k * 8);
+                ok = ok && std::fwrite(p, 8, k, f) == k;
+            });
+            t.hslot.for_range(0, c.trace_n, [&](const uint16_t *p, uint64_t k) {
+                sum.add(p, k * 2);
+                ok = ok && std::fwrite(p, 2, k, f) == k;
+            });
+            ok = ok && std::fwrite(&sum.h, 8, 1, f) == 1;
         }
         ok = std::fflush(f) == 0 && ok;
         ok = ok && fsync(fileno(f)) == 0;
@@ -2653,9 +2835,32 @@ struct rmc_ctx {
         if (!ok) fail(" has an inconsistent global level table");
         std::vector<CkptShard> sc(sh.size());
         std::vector<std::vector<uint64_t>> lss(sh.size());
+        DataSum sum;
         auto in = [&](void *dev, char *host, size_t k) {
             ok = ok && std::fread(host, 1, k, f) == k;
-            if (ok) HIPCHK(hipMemcpy(dev, host, k, hipMemcpyHostToDevice));
+            if (ok) {
+                sum.add(host, k);
+                HIPCHK(hipMemcpy(dev, host, k, hipMemcpyHostToDevice));
+            }
+        };
+        // the current level's offsets, checked before they reach the device: level-relative, from 0,
+        // increasing by one record (CCW..RECW words) at a time, the last record ending at cur_words
+        // -- the kernels' ring arithmetic assumes it (ring_wrap takes x < 2 cap)
+        uint64_t off_prev = 0, off_i = 0, off_words = 0;
+        bool off_ok = true;
+        auto in_off = [&](void *dev, char *host, size_t k) {
+            ok = ok && std::fread(host, 1, k, f) == k;
+            if (!ok) return;
+            sum.add(host, k);
+            const uint64_t *o = reinterpret_cast<const uint64_t *>(host);
+            for (size_t j = 0; j < k / 8; j++, off_i++) {
+                const uint64_t x = o[j];
+                if (off_i == 0) off_ok = off_ok && x == 0;
+                else off_ok = off_ok && x >= off_prev + (uint64_t)ks.CCW && x <= off_prev + (uint64_t)RECW;
+                off_ok = off_ok && x < off_words;
+                off_prev = x;
+            }
+            if (off_ok) HIPCHK(hipMemcpy(dev, host, k, hipMemcpyHostToDevice));
         };
         for (size_t i = 0; i < sh.size(); i++) {
             Shard &s = sh[i];
@@ -2686,10 +2891,17 @@ struct rmc_ctx {
             s.nxt_words = 0;
             ensure_ring(s, c.cur_words + 1, 0);
             ensure_off(s.cur_off, s.cur_off_cap, 0, std::max<uint64_t>(c.cur_n, 1));
+            sum = DataSum{};
             if (s.Tc) stream_bytes(s.Tc, c.T_cap * 8, in);
             else stream_bytes(s.T, c.T_cap * 16, in);
             stream_bytes(s.R, c.cur_words * 4, in);
-            stream_bytes(s.cur_off, c.cur_n * 8, in);
+            off_prev = off_i = 0;
+            off_words = c.cur_words;
+            off_ok = true;
+            stream_bytes(s.cur_off, c.cur_n * 8, in_off);
+            if (ok && (!off_ok || (c.cur_n && (c.cur_words - off_prev < (uint64_t)ks.CCW ||
+                                               c.cur_words - off_prev > (uint64_t)RECW))))
+                fail(" has inconsistent frontier offsets");
             s.hpar.reserve_to(c.trace_n);
             s.hslot.reserve_to(c.trace_n);
             for (uint64_t j = 0; ok && j < c.trace_n;) {
@@ -2702,7 +2914,12 @@ struct rmc_ctx {
                 ok = std::fread(s.hslot.blk[j / HostArr<uint16_t>::B].p + j % HostArr<uint16_t>::B, 2, k, f) == k;
                 j += k;
             }
+            s.hpar.for_range(0, c.trace_n, [&](const uint64_t *p, uint64_t k) { sum.add(p, k * 8); });
+            s.hslot.for_range(0, c.trace_n, [&](const uint16_t *p, uint64_t k) { sum.add(p, k * 2); });
+            uint64_t want_sum = 0;
+            ok = ok && std::fread(&want_sum, 8, 1, f) == 1;
             if (!ok) fail(" is truncated");
+            if (want_sum != sum.h) fail(" has a corrupt data section (checksum mismatch)");
         }
         std::fclose(f);
         for (size_t i = 0; i < sh.size(); i++) {

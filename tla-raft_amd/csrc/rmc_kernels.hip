@@ -2153,7 +2153,7 @@ __global__ __launch_bounds__(256) void k_route_count(const ulonglong2 *__restric
 
 // Source: every successor to its owner's segment of the send buffer (cursor[o] = the segment's
 // next free item, preset to its start): {fingerprint, global key = (parent's global index in the
-// level << 8) | rank among its successors} -- the key orders the level's successors as TLC
+// level << 10) | rank among its successors (< 1024, checked at create)} -- the key orders the level's successors as TLC
 // generates them -- and perm[item] = its slot q, for the owner's verdict to come back to.
 __global__ __launch_bounds__(256) void k_route_place(const ulonglong2 *__restrict__ fp, const uint32_t *__restrict__ cnt,
                                                      uint64_t np, uint32_t maxsucc, uint32_t W, uint32_t *__restrict__ cursor,
@@ -2177,7 +2177,7 @@ __global__ __launch_bounds__(256) void k_route_place(const ulonglong2 *__restric
             const ulonglong2 f = fp[q];
             const uint32_t o = fp_owner(f, W);
             const uint32_t pos = base[o] + atomicAdd(&h[o], 1u);
-            items[pos] = XItem{f.x, f.y, ((g0 + pl) << 8) | r};
+            items[pos] = XItem{f.x, f.y, ((g0 + pl) << 10) | r};
             perm[pos] = (uint32_t)q;
         }
         __syncthreads();

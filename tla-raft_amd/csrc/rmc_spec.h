@@ -63,6 +63,12 @@ RMC_HD uint32_t setnib(uint32_t w, int i, uint32_t v) { return (w & ~(15u << (4 
 // u16 message ids (TLC order), padded to a whole word: CCW + ceil(|msgs| / 2) words.
 constexpr int bits_for(int maxval) { return maxval <= 0 ? 0 : 1 + bits_for(maxval >> 1); }
 
+// bits of the packed core of (N, V) -- Codec<N, V>::BITS, for the host at run time
+constexpr int codec_bits(int N, int V) {
+    return N * (bits_for(N) + 3 + 2 + 2 * bits_for(V + 1)) + N * V * (3 + bits_for(V - 1)) +
+           N * N * (bits_for(V + 1) + bits_for(V + 2)) + N * N + 3 + 4 + V + 8;
+}
+
 template <int N, int V>
 struct Codec {
     static constexpr int B_VF = bits_for(N);                  // 0 = None, k + 1 = server k
@@ -75,6 +81,7 @@ struct Codec {
     static constexpr int BITS = N * (B_VF + B_CT + B_RO + 2 * B_IX) + N * V * B_ENT + N * N * (B_IX + B_NI) +
                                 N * N + 3 + 4 + V + 8;
     static constexpr int CCW = (BITS + 31) / 32;              // packed core words
+    static_assert(BITS == codec_bits(N, V), "codec_bits must follow the field widths above");
 };
 
 RMC_HD void bits_put(uint32_t *w, int pos, uint32_t v, int b) {
