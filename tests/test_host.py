@@ -152,6 +152,53 @@ def test_launcher_reports_cfg_errors(tmp_path):
     assert r.returncode == 151 and "VIEW" in r.stdout
 
 
+def _locations(tla_path):
+    out = subprocess.check_output([LAUNCHER, "-print-locations", str(tla_path)], text=True)
+    return {ln.split()[0]: tuple(map(int, ln.split()[1:])) for ln in out.splitlines()}
+
+
+def test_action_locations_rules(tmp_path):
+    """The trace header's range (raftmc.cpp action_locations): from the first token after "==" to the
+    last token before the next column-1 line, skipping blank lines, comment-only lines and a trailing
+    line comment."""
+    spec = ("---- MODULE M ----\n"
+            "Restart(s) ==\n"
+            "  /\\ role[s] = Leader   \\* trailing comment\n"
+            "  /\\ UNCHANGED x\n"
+            "  \\* /\\ Print(x, TRUE)\n"
+            "\n"
+            "ClientReq(s) == /\\ y' = 1\n"
+            "====\n")
+    (tmp_path / "M.tla").write_text(spec)
+    loc = _locations(tmp_path / "M.tla")
+    assert loc["Restart"] == (3, 3, 4, 16)
+    assert loc["ClientReq"] == (7, 17, 7, 25)
+    assert loc["BecomeLeader"] == (0, 0, 0, 0)  # absent: the launcher falls back to <Action(s)>
+
+
+def test_action_locations_on_reference_spec():
+    """The ranges on the verbatim Raft.tla (skipped where the reference is absent, as on the GPU box).
+    Hand-checked against the text: BecomeCandidate's body runs from tla:108 col 3 to the UNCHANGED
+    conjunct ending tla:130 col 79; BecomeLeader's ends at tla:172, not at the commented-out Print on
+    tla:173; BecomeFollower is the three-line disjunction tla:229-231."""
+    src = "/root/reference/Raft.tla"
+    if not os.path.exists(src):
+        pytest.skip("reference Raft.tla not present")
+    loc = _locations(src)
+    assert loc["BecomeCandidate"] == (108, 3, 130, 79)
+    assert loc["BecomeLeader"][:3] == (158, 3, 172)
+    assert loc["UpdateTerm"][:3] == (176, 3, 188)
+    assert loc["ResponseVote"][:3] == (133, 3, 155)
+    assert loc["Restart"][:3] == (410, 3, 414)
+    assert loc["BecomeFollower"] == (229, 3, 231, 24)
+    lines = open(src).read().split("\n")
+    for name, (l0, c0, l1, c1) in loc.items():
+        assert l0 > 1 and lines[l0 - 2].startswith(name + "(s) ==") or lines[l0 - 1].startswith(name), name
+        assert lines[l0 - 1][c0 - 1] in "/\\", name          # every body is a conjunction / disjunction list
+        last = lines[l1 - 1].split("\\*")[0].rstrip()
+        assert len(last) == c1 and last.lstrip(), name         # ends on the last code column of its line
+
+
 def test_become_follower_variant_spec_recognised():
     """tools/make_variant_spec.py --become-follower on Raft.tla (skipped where the reference is absent, as on
     the GPU box): the launcher's parser maps the text to RMC_SPEC_BECOME_FOLLOWER."""

@@ -7,6 +7,7 @@
 // the counterexample) so that parsers of raft.log keep working.  GPU-specific lines
 // are printed after TLC's block.  Exit codes follow TLC's (0 ok, 11 deadlock,
 // 12 safety violation, 14 Assert, 75 evaluation error, 150/151 spec/config errors).
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -89,14 +90,22 @@ std::vector<Loc> action_locations(const std::string &tla, const std::vector<std:
             Loc L;
             L.l0 = (int)li + 1;
             L.c0 = (int)col + 1;
-            // body ends at the last non-blank line before the next column-1 line
+            // body ends at the last token before the next column-1 line: blank lines, comment-only
+            // lines (tla:173 "\* /\ Print(...)" after BecomeLeader's last conjunct) and a line's
+            // trailing "\*" comment are not part of the expression
+            auto code_end = [&](size_t k) -> long {  // last code column (0-based) of line k, -1 if none
+                const std::string &s = lines[k];
+                size_t cut = s.find("\\*");
+                long e = (long)std::min(cut, s.size()) - 1;
+                while (e >= 0 && isspace((unsigned char)s[e])) e--;
+                return e;
+            };
             size_t j = li + 1;
             while (j < lines.size() && (lines[j].empty() || isspace((unsigned char)lines[j][0]))) j++;
             size_t e = j - 1;
-            while (e > li && lines[e].find_first_not_of(" \t") == std::string::npos) e--;
-            size_t endc = lines[e].find_last_not_of(" \t");
+            while (e > li && code_end(e) < 0) e--;
             L.l1 = (int)e + 1;
-            L.c1 = (int)endc + 1;
+            L.c1 = (int)code_end(e) + 1;
             locs[a] = L;
             break;
         }
@@ -212,6 +221,8 @@ int usage(const char *msg) {
 int main(int argc, char **argv) {
     std::string tla_path, cfg_path;
     int check_deadlock = 1, device = -1, msgcap = 0, seenlog2 = 0, workers = 1;
+    bool print_locations = false;       // print each action's source range and exit (no GPU needed)
+    double progress_s = 60.0;           // TLC reports Progress once a minute (and at the end)
     double ckpt_minutes = 30.0;         // TLC -checkpoint: minutes between checkpoints (0 = never)
     std::string metadir, recover_dir;   // TLC -metadir / -recover: where checkpoints go / come from
     for (int i = 1; i < argc; i++) {
@@ -229,6 +240,8 @@ int main(int argc, char **argv) {
         else if (a == "-checkpoint") ckpt_minutes = std::atof(need("-checkpoint"));
         else if (a == "-metadir") metadir = need("-metadir");
         else if (a == "-recover") recover_dir = need("-recover");
+        else if (a == "-progress") progress_s = std::atof(need("-progress"));
+        else if (a == "-print-locations") print_locations = true;
         else if (a.size() > 4 && a.compare(a.size() - 4, 4, ".tla") == 0) tla_path = a;
         else if (a[0] != '-' && tla_path.empty()) tla_path = a + ".tla";
         else return usage(("unsupported option " + a).c_str());
@@ -240,6 +253,15 @@ int main(int argc, char **argv) {
     if (!read_file(tla_path, &tla)) {
         if (!skip_spec) { std::fprintf(stderr, "Error: cannot read %s\n", tla_path.c_str()); return 150; }
         tla.clear();
+    }
+    if (print_locations) {
+        // the "<Action line L, col C to line L', col C' of module M>" ranges the trace headers use
+        std::vector<std::string> names(kActionNames, kActionNames + 13);
+        names.insert(names.end(), kBfNames, kBfNames + 3);
+        std::vector<Loc> locs = action_locations(tla, names);
+        for (size_t a = 0; a < names.size(); a++)
+            std::printf("%s %d %d %d %d\n", names[a].c_str(), locs[a].l0, locs[a].c0, locs[a].l1, locs[a].c1);
+        return 0;
     }
     if (!read_file(cfg_path, &cfgtxt)) { std::fprintf(stderr, "Error: cannot read %s\n", cfg_path.c_str()); return 151; }
     rmc::ParsedModel pm;
@@ -292,21 +314,33 @@ int main(int argc, char **argv) {
     auto last_ckpt = std::chrono::steady_clock::now();
     double gpu_seconds = 0;
     std::vector<rmc_level_stats> lv(65);
+    // TLC prints Progress at start, then once per reporting interval, then at the end of the search
+    auto progress = [&](const rmc_level_stats &q) {
+        const double el = std::max(1e-9, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        std::printf("Progress(%d) at %s: %llu states generated (%.0f s/min), %llu distinct states found (%.0f ds/min), "
+                    "%llu states left on queue.\n",
+                    q.level + 1, now_str().c_str(), (unsigned long long)q.total_generated,
+                    q.total_generated / el * 60.0, (unsigned long long)q.total_distinct,
+                    q.total_distinct / el * 60.0, (unsigned long long)q.queue);
+        std::fflush(stdout);
+    };
+    auto last_progress = std::chrono::steady_clock::now();
+    bool reported = false, have_last = false;
+    rmc_level_stats last{};
     while (rc == RMC_OK) {
         uint32_t nl = 0;
         rc = rmc_steps(ctx, lv.data(), (uint32_t)lv.size(), &nl);
         if (rc < 0) break;
-        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        for (uint32_t i = 0; i < nl; i++) {
-            const rmc_level_stats &q = lv[i];
-            gpu_seconds += q.seconds;
-            std::printf("Progress(%d) at %s: %llu states generated (%.0f s/min), %llu distinct states found (%.0f ds/min), "
-                        "%llu states left on queue.\n",
-                        q.level + 1, now_str().c_str(), (unsigned long long)q.total_generated,
-                        q.total_generated / el * 60.0, (unsigned long long)q.total_distinct,
-                        q.total_distinct / el * 60.0, (unsigned long long)q.queue);
+        for (uint32_t i = 0; i < nl; i++) gpu_seconds += lv[i].seconds;
+        if (nl == 0) continue;
+        last = lv[nl - 1];
+        have_last = true;
+        const auto now = std::chrono::steady_clock::now();
+        if (!reported || std::chrono::duration<double>(now - last_progress).count() >= progress_s) {
+            progress(last);
+            reported = true;
+            last_progress = now;
         }
-        std::fflush(stdout);
         const double since = std::chrono::duration<double>(std::chrono::steady_clock::now() - last_ckpt).count();
         if (rc == RMC_OK && ckpt_minutes > 0 && since >= ckpt_minutes * 60.0) {
             // TLC -checkpoint: the run so far, between two levels (rmc_checkpoint)
@@ -325,6 +359,7 @@ int main(int argc, char **argv) {
         rmc_destroy(ctx);
         return 75;
     }
+    if (have_last) progress(last);  // the closing report
     rmc_result res;
     rmc_get_result(ctx, &res);
     int exit_code = 0;

@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""At-scale counters of the expansion and commit kernels, per BFS level (tools/pmc_scale.sh output).
+
+tools/pmc_scale.sh runs tools/explore.py (default 3 servers / 2 values / MaxElection 2: 18.5 M states,
+levels of up to 1.5 M parents, a compact seen set of ~140 GB -- far beyond the 256 MB Infinity Cache,
+so FETCH_SIZE / WRITE_SIZE are HBM traffic) once per counter pass.  Every level is one dispatch of
+each kernel, so dispatch k (in dispatch order) is level k + 1, and the explore log of the same pass
+gives that level's parents F, successors G, new states N, average record bytes S and the HIP-event
+duration of each kernel.  Per level this prints and records:
+
+  alg_bytes    bench.py alg_bytes() -- the algorithmic bytes of the kernel
+  hbm_bytes    2 * 1024 * FETCH_SIZE + 1024 * WRITE_SIZE (MI355X_MICROARCH.md rocprofv3 section; the
+               x2 is the guide's gfx950 correction for wide streaming reads, an upper bound for the
+               8-16 B random accesses that dominate here -- both readings are reported)
+  ratio        hbm_bytes / alg_bytes (traffic well above 1 = whole lines moved for a few useful bytes)
+  valu_frac    SQ_INSTS_VALU / duration against 256 CUs x 4 SIMDs x 2.4 GHz / 2 wave64 issues per s
+  alg_GBps     alg_bytes / duration, hbm_GBps = hbm_bytes / duration (peak 8 TB/s)
+
+usage: pmc_scale_report.py gpurun_out/pmcs out.json [--min-parents 500000]"""
+import argparse
+import collections
+import csv
+import json
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import HBM_PEAK_GBS, VALU_PEAK, alg_bytes  # noqa: E402
+
+LEVEL = re.compile(r"^L\s*(\d+) F=\s*(\d+) G=\s*(\d+) N=\s*(\d+) tot=\s*\d+\s+[\d.]+ms \[([^\]]*)\].*rec=([\d.]+)B")
+KERNELS = {"expand": ("k_expand", 1, "expand_hash"), "commit": ("k_commit", 3, "materialize")}
+
+
+def levels_of(log):
+    out = []
+    for ln in open(log):
+        m = LEVEL.match(ln)
+        if m:
+            lv, F, G, N, ph, rec = m.groups()
+            out.append(dict(level=int(lv), F=int(F), G=int(G), N=int(N), ms=[float(x) for x in ph.split()],
+                            rec=float(rec)))
+    return out
+
+
+def per_dispatch(csvf, kname):
+    vals = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in csv.DictReader(open(csvf)):
+        if kname in r["Kernel_Name"]:
+            vals[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    return [vals[k] for k in sorted(vals)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("out")
+    ap.add_argument("--min-parents", type=int, default=500000)
+    ap.add_argument("--n", type=int, default=3)
+    a = ap.parse_args()
+    report = {"workload": "tools/explore.py 3 2 2 3 (n3 V2 E2: 18.5 M states, 51 levels; compact seen set beyond the "
+                          "Infinity Cache)", "hbm_peak_GBps": HBM_PEAK_GBS, "valu_peak_insts_per_s": VALU_PEAK,
+              "note": "one dispatch per level per kernel; durations are the explore run's HIP events of the same pass",
+              "kernels": {}}
+    swb = 48 if a.n >= 4 else 32
+    for key, (kname, ph, phase) in KERNELS.items():
+        rows, tot = [], collections.Counter()
+        fetch = per_dispatch(os.path.join(a.root, "fetch", "run_counter_collection.csv"), kname)
+        write = per_dispatch(os.path.join(a.root, "write", "run_counter_collection.csv"), kname)
+        sq = per_dispatch(os.path.join(a.root, "sqa", "run_counter_collection.csv"), kname)
+        lv_f = levels_of(os.path.join(a.root, "fetch.log"))
+        if not (len(fetch) == len(write) == len(sq) == len(lv_f)):
+            sys.exit(f"{kname}: dispatches {len(fetch)}/{len(write)}/{len(sq)} vs {len(lv_f)} levels")
+        for i, L in enumerate(lv_f):
+            if L["F"] < a.min_parents:
+                continue
+            ms = L["ms"][ph]
+            alg = alg_bytes(phase, L["F"], L["G"], L["N"], L["rec"], 0, 8, swb)
+            rd, wr = 1024 * fetch[i]["FETCH_SIZE"], 1024 * write[i]["WRITE_SIZE"]
+            hbm = 2 * rd + wr
+            valu = sq[i]["SQ_INSTS_VALU"]
+            rows.append({"level": L["level"], "parents": L["F"], "successors": L["G"], "new": L["N"], "ms": ms,
+                         "alg_bytes": round(alg), "hbm_bytes": round(hbm), "hbm_bytes_fetch_x1": round(rd + wr),
+                         "ratio": round(hbm / alg, 3), "ratio_fetch_x1": round((rd + wr) / alg, 3),
+                         "alg_GBps": round(alg / ms / 1e6, 1), "hbm_GBps": round(hbm / ms / 1e6, 1),
+                         "valu_insts": round(valu), "valu_per_successor": round(valu / max(1, L["G"]), 1),
+                         "valu_frac": round(valu / (ms / 1e3) / VALU_PEAK, 4)})
+            for k, v in (("alg", alg), ("hbm", hbm), ("hbm1", rd + wr), ("ms", ms), ("valu", valu), ("G", L["G"])):
+                tot[k] += v
+        agg = {"levels": len(rows), "alg_bytes": round(tot["alg"]), "hbm_bytes": round(tot["hbm"]),
+               "ratio": round(tot["hbm"] / tot["alg"], 3), "ratio_fetch_x1": round(tot["hbm1"] / tot["alg"], 3),
+               "alg_GBps": round(tot["alg"] / tot["ms"] / 1e6, 1), "hbm_GBps": round(tot["hbm"] / tot["ms"] / 1e6, 1),
+               "alg_frac": round(tot["alg"] / tot["ms"] / 1e6 / HBM_PEAK_GBS, 5),
+               "hbm_frac": round(tot["hbm"] / tot["ms"] / 1e6 / HBM_PEAK_GBS, 5),
+               "valu_frac": round(tot["valu"] / (tot["ms"] / 1e3) / VALU_PEAK, 4),
+               "valu_per_successor": round(tot["valu"] / max(1, tot["G"]), 1)}
+        report["kernels"][key] = {"kernel": kname, "levels_with_parents_ge": a.min_parents, "aggregate": agg,
+                                  "per_level": rows}
+        print(f"{key}: {agg}")
+    with open(a.out, "w") as f:
+        json.dump(report, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
