@@ -279,7 +279,8 @@ RAFT_CFG_TOTALS = dict(distinct=10946499503, generated=56936653204, depth=72)
 def test_raft_cfg_exhausted_and_prefix_matches_c_oracle():
     """configs[0]/[2]: Raft.cfg as shipped (3 servers, 2 values, MaxElection 3, MaxRestart 3) exhausted
     on one GPU -- the large-run storage (compact seen set, frontier ring, host trace) end to end.  The
-    first 30 levels (211M states) equal the C oracle's level by level, distinct and generated."""
+    first 34 levels (743.6 M states, 2.47 G generated; oracle/raft_prefix.c) equal the C oracle's level
+    by level, distinct and generated."""
     g = PREFIX["n3_v2_e3_r3"]
     for mc in _cache.values():  # the run takes most of the device's memory
         mc.close()
