@@ -1666,16 +1666,20 @@ struct rmc_ctx {
             renew_election_tags(s, 1);
             ++s.epoch;
             trace_restart(s);
+            // chunks of many parents probe and elect in a pass of their own, a lane per successor
+            const bool split = split_min && np_ >= split_min;
             auto params = [&] {
                 KParams Q = chunk_params(s);
                 Q.p_begin = p0; Q.p_end = p1; Q.next_base = s.nxt_n; Q.next_wbase = s.nxt_words;
                 Q.gid_next_base = gid_nxt; Q.gid_parent_base = gid_cur;
                 Q.Lmask = Lcap - 1;
                 Q.epoch = s.epoch;
+                Q.split = split ? 1 : 0;
                 return Q;
             };
             // expand + fingerprint + seen-set probe + staging, one evaluation per parent
             timed(PH_HASH, [&] { ks.fused(params(), stream); });
+            if (split) timed(PH_OTHER, [&] { ks.probe(params(), np_, stream); });
             timed(PH_DEDUP, [&] { ks.wincount(params(), np_, stream); });
             if (!small) {
                 HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
@@ -1746,6 +1750,9 @@ struct rmc_ctx {
         if (!v || !*v) return dflt;
         return std::max(lo, std::min(hi, std::atoi(v)));
     }
+    // parents per host-driven chunk from which the seen-set probe and election run as their own
+    // pass (k_probe; 0 = always fused into the expansion)
+    const uint64_t split_min = (uint64_t)env_int("RMC_SPLIT_MIN", 1 << 16, 0, 1 << 30);
     const int dl_group = env_int("RMC_DL_GROUP", 2, 1, 64);
     const int dl_ahead = env_int("RMC_DL_AHEAD", 2, 1, 64);
     const int dl_query_us = env_int("RMC_DL_QUERY_US", 2000, 0, 1 << 30);

@@ -113,6 +113,10 @@ struct KParams {
     // xside[i] = {parent global id lo, hi, slot key, record words} instead of par / pslot
     int route;
     uint4 *xside;
+    // split probe (host-driven chunks of many parents): expand writes each successor's fingerprint and
+    // its extra record words (lslot = e) and k_probe gives every successor a lane of its own for the
+    // seen-set probe and the election
+    int split;
     // fused single-shard level: expand (+hash, +seen-set probe, +election, +staging) -> wincount
     // -> commit.  Successor slot q = (p - p_begin) * maxsucc + rank is sparse and increases in
     // TLC order; it indexes fp, lslot and score (the staged successor: its acting server's row,
@@ -149,6 +153,7 @@ struct KernelSet {
     int N, V, MR, MCAP, CCW, RECW_MAX, maxsucc;
     void (*single)(const KParams &, hipStream_t);           // all successors of front[0] -> next, fp, out_keys
     void (*fused)(const KParams &, hipStream_t);            // expand + hash + probe + election + staging
+    void (*probe)(const KParams &, uint64_t np, hipStream_t);     // split probe: seen set + election per successor
     void (*wincount)(const KParams &, uint64_t np, hipStream_t);  // winners per parent + their scan, successors generated
     void (*commit)(const KParams &, hipStream_t);           // winners -> next level, seen set, trace, invariants;
                                                             // chunk summary (and the device loop's next level)

@@ -57,6 +57,9 @@ extern "C" int rmc_debug_phases(unsigned long long *out, int reset) {
 #ifndef RMC_GRID_PER_CU  // one-wave blocks per CU in the expansion / commit grids
 #define RMC_GRID_PER_CU 32
 #endif
+#ifndef RMC_COMMIT_EARLY  // k_commit: the seen-set insert's first CAS overlaps the record writes
+#define RMC_COMMIT_EARLY 1
+#endif
 #ifndef RMC_WIDE_WAVES
 #define RMC_WIDE_WAVES 2
 #endif
@@ -1115,6 +1118,34 @@ __device__ __forceinline__ void seen_insert(const Seen &S, ulonglong2 f) {
     }
 }
 
+// An insert split in two: the first slot's CAS goes out as soon as the fingerprint is known and its
+// result is taken only once the caller's other work is issued (k_commit: the state's record, trace
+// entry and invariants), so the round trip overlaps that work instead of preceding it.
+__device__ __forceinline__ uint64_t seen_insert_begin(const Seen &S, ulonglong2 f, unsigned long long *prev) {
+    if (S.Tc) {
+        const uint64_t h = t_home_c(f, S.cap);
+        *prev = atomicCAS(&S.Tc[h], 0ull, (unsigned long long)f.x);
+        return h;
+    }
+    const uint64_t h = t_index(f, S.mask);
+    *prev = atomicCAS((unsigned long long *)&S.T[h].x, 0ull, (unsigned long long)f.x);
+    return h;
+}
+__device__ __forceinline__ void seen_insert_end(const Seen &S, ulonglong2 f, uint64_t h, unsigned long long prev) {
+    if (S.Tc) {
+        while (prev != 0ull) {
+            h = (h + 1 == S.cap) ? 0 : h + 1;
+            prev = atomicCAS(&S.Tc[h], 0ull, (unsigned long long)f.x);
+        }
+        return;
+    }
+    while (prev != 0ull) {
+        h = (h + 1) & S.mask;
+        prev = atomicCAS((unsigned long long *)&S.T[h].x, 0ull, (unsigned long long)f.x);
+    }
+    S.T[h].y = f.y;
+}
+
 __device__ __forceinline__ uint64_t l_index(const ulonglong2 f, uint64_t mask) {
     return (f.x ^ (f.x >> 31) ^ (f.y >> 7)) & mask;
 }
@@ -1457,12 +1488,16 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
                     const uint64_t q = pl * (uint64_t)MX + lo;
                     P.fp[q] = f;
                     if (P.route) return;  // sharded round: the fingerprint's owner probes and elects
+                    const uint32_t e = ((uint32_t)sNa[lo] + (W.nm & 1u) + 1u) >> 1;
+                    if (P.split) {  // k_probe probes and elects, a lane per successor
+                        P.lslot[q] = e;
+                        return;
+                    }
                     // the election slot's first word goes out with the seen-set probe: one
                     // round trip fewer for a new fingerprint
                     const uint64_t g0 = l_index(f, P.Lmask);
                     const unsigned long long v0 =
                         __hip_atomic_load(&P.LXY[g0].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t e = ((uint32_t)sNa[lo] + (W.nm & 1u) + 1u) >> 1;
                     P.lslot[q] = seen_contains(P.seen, f)
                                      ? LS_SEEN
                                      : elect_slot<MX>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g0, v0);
@@ -1605,6 +1640,45 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
         if (lane == 0) *P.out_count = total;
     }
     PHASE_FLUSH;
+}
+
+// Split probe of a host-driven chunk: the expansion (P.split) wrote every successor's fingerprint
+// fp[q] and its extra record words e in lslot[q]; here each successor gets a lane of its own for the
+// seen-set probe and the election (elect_slot, the same protocol as the fused pass), so a wave keeps
+// 64 independent probe chains in flight instead of the ~5 of one parent.  A wave takes 64
+// consecutive parents: their successor counts are scanned across the wave and successor i of the
+// group goes to lane i % 64 of round i / 64 (its parent found by a binary search over the scan).
+template <int MX>
+__global__ __launch_bounds__(256) void k_probe(KParams P) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t np = P.p_end - P.p_begin;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t g0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; g0 < np;
+         g0 += nwaves * 64) {
+        const uint64_t pl = g0 + (uint64_t)lane;
+        const uint32_t t = pl < np ? P.cnt[pl] : 0u;
+        uint32_t tot;
+        const uint32_t ex = wave_excl_scan(t, lane, &tot);
+        for (uint32_t b0 = 0; b0 < tot; b0 += 64) {
+            const uint32_t i = b0 + (uint32_t)lane;
+            // the last lane j with ex[j] <= i: ex[j + 1] = ex[j] + t[j] > i, so t[j] > 0
+            int j = 0;
+#pragma unroll
+            for (int st = 32; st; st >>= 1) {
+                const uint32_t v = (uint32_t)__shfl(ex, j + st, 64);
+                j = v <= i ? j + st : j;
+            }
+            const uint32_t exj = (uint32_t)__shfl(ex, j, 64);
+            if (i >= tot) continue;
+            const uint64_t q = (g0 + (uint64_t)j) * (uint64_t)MX + (i - exj);
+            const ulonglong2 f = P.fp[q];
+            const uint32_t e = P.lslot[q];
+            const uint64_t g = l_index(f, P.Lmask);
+            const unsigned long long v0 = __hip_atomic_load(&P.LXY[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            P.lslot[q] = seen_contains(P.seen, f) ? LS_SEEN
+                                                  : elect_slot<MX>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g, v0);
+        }
+    }
 }
 
 // fingerprints of whole states (Init, test hooks): one wave per state
@@ -1903,11 +1977,17 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
         // round the owner's verdict is already known): a speculative read instead of a third round
         // trip once the election words are in
         uint4 xa = make_uint4(0u, 0u, 0u, 0u), xb = xa, xc = xa;
+#if RMC_COMMIT_EARLY
+        ulonglong2 xf = make_ulonglong2(0ull, 0ull);  // and their fingerprints (the seen-set insert)
+#endif
         if ((uint32_t)lane < t && (P.route ? g0 == LS_WIN : g0 < LS_ELECT)) {
             const uint4 *src = P.score + (pl * (uint64_t)MX + (uint32_t)lane) * (uint64_t)S::SW4;
             xa = src[0];
             xb = src[1];
             if (S::SW4 > 2) xc = src[2];
+#if RMC_COMMIT_EARLY
+            if (!P.route) xf = P.fp[pl * (uint64_t)MX + (uint32_t)lane];
+#endif
         }
         uint32_t pc[Lo::NW], ppk[S::CCW];
 #pragma unroll
@@ -1943,6 +2023,11 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
             uint32_t pk[S::CCW];
             uint4 sa = make_uint4(0u, 0u, 0u, 0u), sb = sa, sc = sa;
             uint32_t size = 0;
+#if RMC_COMMIT_EARLY
+            ulonglong2 fi = make_ulonglong2(0ull, 0ull);
+            uint64_t hi = 0;
+            unsigned long long prev = 0ull;
+#endif
 #pragma unroll
             for (int w = 0; w < S::CCW; w++) pk[w] = 0u;
             if (win) {
@@ -1969,7 +2054,12 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
                     P.xside[out] = make_uint4((uint32_t)pref, (uint32_t)(pref >> 32), key, size);
                 } else {
                     const uint64_t gid = P.gid_next_base + out;
+#if RMC_COMMIT_EARLY
+                    fi = r0 == 0 ? xf : P.fp[q];
+                    hi = seen_insert_begin(P.seen, fi, &prev);  // resolved after the record is out
+#else
                     seen_insert(P.seen, P.fp[q]);
+#endif
                     P.par[gid - P.trace_base] = P.gid_parent_base + p;
                     P.pslot[gid - P.trace_base] = (uint16_t)key;
                 }
@@ -2003,6 +2093,9 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
                 const uint32_t add[4] = {ay & 0xFFFFu, ay >> 16, az & 0xFFFFu, az >> 16};
                 write_ids<N, V, MR>(P.next, ring_wrap(rstart + S::CCW, P.rcap), P.rcap, id, nm, add, nadd, lane);
             }
+#if RMC_COMMIT_EARLY
+            if (win && !P.route) seen_insert_end(P.seen, fi, hi, prev);
+#endif
             done += (uint32_t)__popcll(m);
             done_w += wtot;
         }
@@ -2026,6 +2119,12 @@ struct Launch {
     static void fused(const KParams &P, hipStream_t s) {
         hipLaunchKernelGGL((k_expand<N, V, MR, M_FUSED, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s,
                            P);
+    }
+    static void probe(const KParams &P, uint64_t np, hipStream_t s) {
+        constexpr int MX = Spec<N, V, MR>::MAXS + (BFV ? Spec<N, V, MR>::MCAP : 0);
+        const uint64_t blocks = (np + 255) / 256;  // four one-group waves per block
+        hipLaunchKernelGGL((k_probe<MX>), dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u), dim3(256),
+                           0, s, P);
     }
     static void wincount(const KParams &P, uint64_t np, hipStream_t s) {
         const uint64_t tiles = (np + WTILE - 1) / WTILE;
@@ -2051,6 +2150,7 @@ static void fill(KernelSet *ks) {
     ks->maxsucc = S::MAXS + (BFV ? S::MCAP : 0);
     ks->single = &Launch<N, V, MR, BFV>::single;
     ks->fused = &Launch<N, V, MR, BFV>::fused;
+    ks->probe = &Launch<N, V, MR, BFV>::probe;
     ks->wincount = &Launch<N, V, MR>::wincount;
     ks->commit = &Launch<N, V, MR, BFV>::commit;
     ks->fp_states = &Launch<N, V, MR>::fps;
