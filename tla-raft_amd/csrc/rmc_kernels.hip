@@ -57,8 +57,16 @@ extern "C" int rmc_debug_phases(unsigned long long *out, int reset) {
 #ifndef RMC_GRID_PER_CU  // one-wave blocks per CU in the expansion / commit grids
 #define RMC_GRID_PER_CU 32
 #endif
-#ifndef RMC_COMMIT_EARLY  // k_commit: the seen-set insert's first CAS overlaps the record writes
-#define RMC_COMMIT_EARLY 1
+#ifndef RMC_COMMIT_EARLY  // k_commit: the seen-set insert's first CAS overlaps the record writes.
+// Measured off: it takes k_commit to 133 VGPRs (3 waves / SIMD: Raft.cfg commit 16.5 s) or, held
+// at 4 waves, to spills (14.4 s) against 14.2 s without (profiles/r03_ab1_raftcfg_*.txt)
+#define RMC_COMMIT_EARLY 0
+#endif
+#ifndef RMC_COMMIT_PREFETCH  // k_commit: the next parent's header loads go out with this parent's record
+#define RMC_COMMIT_PREFETCH 1
+#endif
+#ifndef RMC_EXPAND_PREFETCH_MSGS  // k_expand: the next parent's message-table words fetched ahead
+#define RMC_EXPAND_PREFETCH_MSGS 1
 #endif
 #ifndef RMC_WIDE_WAVES
 #define RMC_WIDE_WAVES 2
@@ -986,6 +994,92 @@ __device__ __forceinline__ void load_parent_words(const KParams &P, uint64_t sta
     __syncthreads();
 }
 
+// The message-table words of a fetched record (info word + hash pair per message), issued ahead of
+// use: k_expand loads them for its next parent while it hashes the current one (RMC_EXPAND_PREFETCH_MSGS),
+// which takes the table round trip off the start of every parent.
+template <int MR>
+struct MsgPre {
+    uint32_t id[MR], inf[MR];
+    ulonglong2 g[MR];
+};
+
+template <int N, int V, int MR>
+__device__ __forceinline__ void fetch_msgs(const KParams &P, uint32_t rw0, uint32_t rw1, int lane, MsgPre<MR> &pm) {
+    using Lo = Layout<N, V>;
+    using S = Spec<N, V, MR>;
+    uint32_t packed[S::CCW], c[Lo::NW];
+#pragma unroll
+    for (int k = 0; k < S::CCW; k++) packed[k] = rdlane(rw0, k);
+    decode_core<N, V>(packed, c);
+    const uint32_t nm = (c[Lo::W_MISC] >> 16) & 0xFFu;
+#pragma unroll
+    for (int r = 0; r < MR; r++) {
+        const uint32_t k = (uint32_t)(r * 64 + lane);
+        const uint32_t wi = (uint32_t)S::CCW + (k >> 1);
+        const uint32_t a = __shfl(rw0, (int)(wi & 63u), 64);
+        const uint32_t b = MR > 1 ? __shfl(rw1, (int)(wi & 63u), 64) : 0u;
+        const uint32_t word = wi < 64u ? a : b;
+        uint32_t id = 0xFFFFu, inf = 0;
+        ulonglong2 g = make_ulonglong2(0ull, 0ull);
+        if (k < nm) {
+            id = (word >> ((k & 1u) * 16u)) & 0xFFFFu;
+            inf = P.t.info[id];
+            g = P.t.gmsg[id];
+        }
+        pm.id[r] = id;
+        pm.inf[r] = inf;
+        pm.g[r] = g;
+    }
+}
+
+// load_parent_words with the message-table words already fetched (fetch_msgs)
+template <int N, int V, int MR>
+__device__ __forceinline__ void load_parent_pre(const KParams &P, uint64_t start, uint32_t rw0, int lane,
+                                                Wave<N, V, MR> &W, uint16_t *ids, uint64_t *M0, uint64_t *M1,
+                                                uint32_t *pcore, const MsgPre<MR> &pm) {
+    using Lo = Layout<N, V>;
+    using S = Spec<N, V, MR>;
+    uint32_t packed[S::CCW];
+#pragma unroll
+    for (int k = 0; k < S::CCW; k++) packed[k] = rdlane(rw0, k);
+    decode_core<N, V>(packed, W.c);
+    if (lane == 0) {
+#pragma unroll
+        for (int w = 0; w < Lo::NW; w++) pcore[w] = W.c[w];
+    }
+    W.lds = pcore;
+    W.nm = (W.c[Lo::W_MISC] >> 16) & 0xFFu;
+    W.idw = ring_wrap(start + S::CCW, P.rcap);
+    if (lane < N * N) { M0[lane] = 0; M1[lane] = 0; }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < MR; r++) {
+        const uint32_t k = (uint32_t)(r * 64 + lane);
+        if (k < W.nm) {
+            const uint32_t pr = mi_src(pm.inf[r]) * N + mi_dst(pm.inf[r]);
+            atomicAdd((unsigned long long *)&M0[pr], (unsigned long long)pm.g[r].x);
+            atomicAdd((unsigned long long *)&M1[pr], (unsigned long long)pm.g[r].y);
+        }
+        ids[k] = (uint16_t)pm.id[r];
+        W.id[r] = pm.id[r];
+        W.inf[r] = pm.inf[r];
+    }
+#pragma unroll
+    for (int s = 0; s < N; s++) {
+        const uint32_t ct = nib(W.c[Lo::W_CT], s);
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int r = 0; r < MR; r++) {
+            const uint32_t m = W.inf[r];
+            const bool hit = (uint32_t)(r * 64 + lane) < W.nm && mi_type(m) == VRESP && mi_dst(m) == (uint32_t)s &&
+                             mi_term(m) == ct;
+            cnt += (uint32_t)__popcll(__ballot(hit));
+        }
+        if (lane == 0) pcore[Lo::NW + s] = cnt;
+    }
+    __syncthreads();
+}
+
 template <int N, int V, int MR, bool SUMS>
 __device__ __forceinline__ void load_parent(const KParams &P, uint64_t start, int lane, Wave<N, V, MR> &W, uint16_t *ids,
                             uint64_t *M0, uint64_t *M1, uint32_t *pcore) {
@@ -1308,9 +1402,15 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
     // (offsets two parents ahead: an offset has a whole iteration to land before its record is fetched)
     uint64_t p = P.p_begin + blockIdx.x, nstart = 0, nnstart = 0;
     uint32_t nrw0 = 0, nrw1 = 0;
+    // PREM: the next parent's record goes out as soon as this one's is consumed, its message-table
+    // words once this one's actions are evaluated -- both land while this parent is hashed (one-round
+    // kernels: the two-round n >= 4 expansion is at its register limit already)
+    constexpr bool PREM = RMC_EXPAND_PREFETCH_MSGS && MR == 1;
+    MsgPre<MR> pm;
     if (p < P.p_end) {
         nstart = rec_start<S::RECW_MAX>(P, p);
         fetch_record<MR, S::RECW_MAX>(P, nstart, lane, nrw0, nrw1);
+        if constexpr (PREM) fetch_msgs<N, V, MR>(P, nrw0, nrw1, lane, pm);
         if (p + gridDim.x < P.p_end) nnstart = rec_start<S::RECW_MAX>(P, p + gridDim.x);
     }
     for (; p < P.p_end; p += gridDim.x) {
@@ -1319,7 +1419,12 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
         nstart = nnstart;
         if (p + 2ull * gridDim.x < P.p_end) nnstart = rec_start<S::RECW_MAX>(P, p + 2ull * gridDim.x);
         Wave<N, V, MR> W;
-        load_parent_words<N, V, MR, SUMS>(P, start, nrw0, nrw1, lane, W, ids, M0, M1, pcore);
+        if constexpr (PREM) {
+            load_parent_pre<N, V, MR>(P, start, nrw0, lane, W, ids, M0, M1, pcore, pm);
+            if (more) fetch_record<MR, S::RECW_MAX>(P, nstart, lane, nrw0, nrw1);
+        } else {
+            load_parent_words<N, V, MR, SUMS>(P, start, nrw0, nrw1, lane, W, ids, M0, M1, pcore);
+        }
         PHASE(0);
         Succ<N, V, MR> cand[NC];
         uint32_t akey = KEY_NONE;
@@ -1338,7 +1443,11 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
             eval_msg<N, V, MR, BFV>(P, W, ids, r, lane, cand[r], cand[BFV ? MR + 1 + r : r], akey,
                                     &sAinf[(r * 64 + lane) * S::NADD], mid[r]);
         eval_slot<N, V, MR>(P, W, ids, lane, cand[MR], &sAinf[(MR * 64 + lane) * S::NADD], sid);
-        if (more) fetch_record<MR, S::RECW_MAX>(P, nstart, lane, nrw0, nrw1);
+        if constexpr (PREM) {
+            if (more) fetch_msgs<N, V, MR>(P, nrw0, nrw1, lane, pm);
+        } else {
+            if (more) fetch_record<MR, S::RECW_MAX>(P, nstart, lane, nrw0, nrw1);
+        }
         PHASE(1);
         // rank of every enabled successor in TLC order
         uint64_t en[NC];
@@ -1950,21 +2059,52 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
     if (!level_args(P)) return;
     const int lane = threadIdx.x;
     const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
+    // every load of a parent that depends on no other load goes out at once: its winner count,
+    // offsets, successor count and first 64 election slots (read ahead of knowing whether they are
+    // needed; all in bounds; commit always reads a ring level: foff is set).  The header's uniform
+    // words travel in one VGPR: lane k loads word k (one load instruction for all of them, two
+    // registers per header in flight instead of ten).  RMC_COMMIT_PREFETCH: software pipeline --
+    // the next parent's header goes out with this parent's record, so its round trip overlaps this
+    // one's instead of starting the next iteration.
+    struct Hdr {
+        uint32_t hw, g0;
+    };
+    auto header = [&](uint64_t p) {
+        const uint64_t pl = p - P.p_begin;
+        const uint32_t *src;
+        switch (lane & 7) {
+        case 0: src = (const uint32_t *)(P.foff + p); break;
+        case 1: src = (const uint32_t *)(P.foff + p) + 1; break;
+        case 2: src = P.wcnt + pl; break;
+        case 3: src = P.boff + pl / WTILE; break;
+        case 4: src = P.wpos + pl; break;
+        case 5: src = P.cnt + pl; break;
+        case 6: src = P.boffw + pl / WTILE; break;
+        default: src = P.wposw + pl; break;
+        }
+        Hdr h;
+        h.hw = lane < 8 ? *src : 0u;
+        h.g0 = lane < MX ? P.lslot[pl * (uint64_t)MX + lane] : LS_SEEN;
+        return h;
+    };
+#if RMC_COMMIT_PREFETCH
+    Hdr nh{};
+    if (P.p_begin + blockIdx.x < P.p_end) nh = header(P.p_begin + blockIdx.x);
+#endif
     for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
         const uint64_t pl = p - P.p_begin;
-        // every load of the parent that depends on no other load goes out at once: its winner
-        // count, offsets, successor count and first 64 election slots (read ahead of knowing
-        // whether they are needed; all in bounds)
-        // (commit always reads a ring level: foff is set; in bounds for every p of the level)
-        const uint64_t foffp = P.foff[p];
-        const uint32_t g0 = lane < MX ? P.lslot[pl * (uint64_t)MX + lane] : LS_SEEN;
-        const uint32_t wc = P.wcnt[pl];
-        const uint32_t bo = P.boff[pl / WTILE], wp = P.wpos[pl], t = P.cnt[pl];
-        const uint32_t bow = P.boffw[pl / WTILE], wpw = P.wposw[pl];
-        // one wait for all of them: otherwise the compiler waits for the counts before it issues
-        // the offset load (or sinks that load behind the branch below) -- a second round trip
-        asm volatile("" ::"v"(foffp), "v"(g0), "v"(wc), "v"(bo), "v"(wp), "v"(t), "v"(bow), "v"(wpw));
+#if RMC_COMMIT_PREFETCH
+        const Hdr h = nh;
+        if (p + gridDim.x < P.p_end) nh = header(p + gridDim.x);
+#else
+        const Hdr h = header(p);
+#endif
+        const uint32_t g0 = h.g0;
+        const uint32_t wc = rdlane(h.hw, 2);
         if (!wc) continue;
+        const uint64_t foffp = ((uint64_t)rdlane(h.hw, 1) << 32) | rdlane(h.hw, 0);
+        const uint32_t bo = rdlane(h.hw, 3), wp = rdlane(h.hw, 4), t = rdlane(h.hw, 5);
+        const uint32_t bow = rdlane(h.hw, 6), wpw = rdlane(h.hw, 7);
         const uint64_t start = ring_wrap(P.fbase + foffp, P.rcap);
         // the parent's record in one round trip (as load_parent), and with it the election words
         // of the first 64 slots (their indices came with the first round trip)
