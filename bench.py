@@ -177,6 +177,7 @@ def sharded_child(args):
         # left for the rounds' buffers; the default gives the seen set half of HBM, far more than
         # this configuration's levels fill before the ring does
         cfg.seen_mem_bytes, cfg.frontier_mem_bytes = 48 << 30, 160 << 30
+        cfg.chunk_successors = 1 << 27  # rounds of 2^27 slots: the rounds' buffers stay within the ~80 GB left
         c4_child(args, cfg, w, rank, world)
         dist.destroy_process_group()
         return

@@ -444,15 +444,31 @@ def test_sharded_bfs_identical_to_one_shard(name, shards, shard_min):
     mc.close()
 
 
+@pytest.mark.parametrize("clear_rounds", ["1", "2", "5"])
+@pytest.mark.parametrize("name", ["n3_v1_e2_r3", "seeded_n3_v2_e2_r3", "n4_v1_e1_r3"])
+def test_sharded_owner_table_tags_across_clears(name, clear_rounds, monkeypatch):
+    """The owner's election table is cleared only every RMC_OT_CLEAR_ROUNDS rounds (owner_table): slots
+    and keys of earlier rounds must read as free / larger however many rounds lie between clears."""
+    monkeypatch.setenv("RMC_OT_CLEAR_ROUNDS", clear_rounds)
+    g = LEVELS[name]
+    mc, res = run_cfg(g, virtual_shards=4, chunk_successors=3000, shard_min_states=1)
+    check_levels(g, res)
+    mc.close()
+
+
 # The same protocol through the RCCL transport: world_size 1 with a unique id is a one-rank
-# communicator, so every collective of step_sharded (all-reduce of the level size, all-to-all of
-# the owner counts, grouped ncclSend/ncclRecv of successors, verdicts and winner records, the
-# round's failure table) runs through RCCL on the stream.  A one-GPU box cannot hold two ranks
-# (RCCL refuses two ranks on one device); this is the RCCL code path short of the xGMI hop.
+# communicator, so every collective of step_sharded (all-reduce of the level size, the gathered
+# count matrices, the round's failure table) runs through RCCL on the stream.  A rank's part for
+# itself is a device copy (its successor items placed in the receive buffer directly); with
+# RMC_SELF_VIA_RCCL=1 it goes through the grouped ncclSend/ncclRecv of successors, verdicts and
+# winner records like any peer's.  A one-GPU box cannot hold two ranks (RCCL refuses two ranks on
+# one device); this is the RCCL code path short of the xGMI hop.
+@pytest.mark.parametrize("self_rccl", ["0", "1"])
 @pytest.mark.parametrize("shard_min", [1, 40])
 @pytest.mark.parametrize("name", ["n3_v1_e2_r3", "n4_v1_e1_r3", "seeded_n3_v2_e2_r3", "deadlock_n3_v1_e1_r3",
                                   "n2_v2_e3_r3", "exist_lc_n3_v1_e2_r3"])
-def test_rccl_one_rank_identical_to_single(name, shard_min):
+def test_rccl_one_rank_identical_to_single(name, shard_min, self_rccl, monkeypatch):
+    monkeypatch.setenv("RMC_SELF_VIA_RCCL", self_rccl)
     g = LEVELS[name]
     mc, res = run_cfg(g, world_size=1, rank=0, comm_unique_id=raftmc.comm_unique_id(), chunk_successors=3000,
                       shard_min_states=shard_min)

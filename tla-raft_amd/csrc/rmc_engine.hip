@@ -379,6 +379,7 @@ struct Shard {
     ulonglong2 *OT = nullptr;
     unsigned long long *OK = nullptr;
     uint64_t ot_cap = 0;
+    uint32_t ot_round = 0;  // rounds on the owner table since it was last cleared (its tag, k_owner_elect)
     uint32_t *ob = nullptr, *ib = nullptr;
     uint64_t ob_cap = 0, ib_cap = 0;
     uint4 *oside = nullptr, *iside = nullptr;
@@ -799,13 +800,13 @@ struct rmc_ctx {
 
         // successor slots per chunk: dense for the sharded path, sparse (parents x maxsucc) for
         // the fused single-GPU path, whose staging holds SW4 * 16 + 36 bytes per slot
-        // Fewer, larger chunks.  An RCCL rank's round (2^27 slots, ~2 M parents for 3 servers and 2
-        // values) pays a dozen host round trips and collectives (one-rank Raft.cfg 66.8 -> 60.6 s
-        // against 2^26); a one-GPU chunk (2^28 slots, ~4 M parents) a few launches and their tails
+        // Fewer, larger chunks.  An RCCL rank's round (2^28 slots, ~3 M parents for 3 servers and 2
+        // values) pays a dozen host round trips and collectives (one-rank Raft.cfg 66.8 s at 2^26,
+        // 57.4 at 2^27, 54.7 at 2^28); a one-GPU chunk (2^28 slots) a few launches and their tails
         // (Raft.cfg 55.0 s at 2^26, 52.7 at 2^27, 51.7 at 2^28).  On one GPU the slot buffers grow
         // on demand (ensure_chunk), so a small run does not pay for them; an RCCL rank allocates
         // them at create, its budgets may be explicit (bench's configs[3] leg).
-        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (virt ? (1ull << 23) : multi ? (1ull << 27) : (1ull << 28));
+        Gcap = cfg.chunk_successors ? cfg.chunk_successors : (virt ? (1ull << 23) : (1ull << 28));
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 30)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^30");
         chunk_parents = Gcap / ks.maxsucc;
@@ -1156,8 +1157,16 @@ struct rmc_ctx {
     }
 
     // owner election table of at least 2 * R slots, cleared for the round
+    // The owner's election table for a round of R items: slots and keys carry the round's 16-bit tag
+    // (k_owner_elect), so a round starts on the table as the last one left it -- it is cleared only
+    // when it is (re)allocated and once every 65533 rounds (one memset of up to ~0.8 GB per round
+    // before: ~1 s of a one-rank Raft.cfg exhaustion).  The tag only moves forward between clears,
+    // also across rmc_reset, so a stale slot never reads as current and its key is never smaller.
+    // rounds between clears of the owner table (RMC_OT_CLEAR_ROUNDS: tests take it down to a few)
+    const uint32_t ot_clear_rounds = (uint32_t)env_int("RMC_OT_CLEAR_ROUNDS", 0xFFFD, 1, 0xFFFD);
     uint64_t owner_table(Shard &o, uint64_t R) {
         const uint64_t need = next_pow2(std::max<uint64_t>(2 * R, 1024));
+        bool clear = false;
         if (need > o.ot_cap) {
             HIPCHK(hipStreamSynchronize(stream));
             dfree(o.OT);
@@ -1165,9 +1174,15 @@ struct rmc_ctx {
             o.OT = dmalloc<ulonglong2>(need);
             o.OK = dmalloc<unsigned long long>(need);
             o.ot_cap = need;
+            clear = true;
         }
-        HIPCHK(hipMemsetAsync(o.OT, 0, need * 16, stream));
-        HIPCHK(hipMemsetAsync(o.OK, 0xFF, need * 8, stream));
+        if (clear || o.ot_round >= ot_clear_rounds) {  // tags 2 .. 0xFFFE, increasing between clears
+            HIPCHK(hipMemsetAsync(o.OT, 0, o.ot_cap * 16, stream));
+            HIPCHK(hipMemsetAsync(o.OK, 0xFF, o.ot_cap * 8, stream));
+            o.ot_round = 1;
+        } else {
+            ++o.ot_round;
+        }
         return need;
     }
 
@@ -1260,26 +1275,44 @@ struct rmc_ctx {
     // One or more all-to-all-v payloads of fixed-size items, by the plans of rmc_plan.h
     // (plans[li] = sh[li]'s; P[k] the k-th payload): virtual shards copy every transfer on the
     // device, an RCCL rank posts one send and one receive per peer and payload, all in one group.
+    // RMC_SELF_VIA_RCCL=1: a rank's part for itself goes through ncclSend / ncclRecv like any other
+    // (the one-rank RCCL tests use it to run those calls on a one-GPU box); by default it is a
+    // device copy, and the successor items are placed in the receive buffer by k_route_place
+    const bool self_rccl = env_int("RMC_SELF_VIA_RCCL", 0, 0, 1) != 0;
     struct Payload {
         const std::vector<XPlan> *plans;
         std::vector<const void *> send;
         std::vector<void *> recv;
         size_t elem;
+        bool self_in_place = false;  // a shard's items to itself are already in its receive buffer
     };
+    // A shard's part for itself never goes through RCCL: a device copy (or nothing, self_in_place).
     void exchange(const std::vector<Payload> &P) {
         if (!rccl) {
             for (const Payload &p : P)
                 for (const Xfer &x : transfers(*p.plans))
-                    HIPCHK(hipMemcpyAsync((char *)p.recv[x.to] + x.dst_off * p.elem,
-                                          (const char *)p.send[x.from] + x.src_off * p.elem, x.n * p.elem,
-                                          hipMemcpyDeviceToDevice, stream));
+                    if (!(p.self_in_place && x.from == x.to))
+                        HIPCHK(hipMemcpyAsync((char *)p.recv[x.to] + x.dst_off * p.elem,
+                                              (const char *)p.send[x.from] + x.src_off * p.elem, x.n * p.elem,
+                                              hipMemcpyDeviceToDevice, stream));
             return;
         }
 #ifdef RMC_WITH_RCCL
+        if (!self_rccl)
+            for (const Payload &p : P) {
+                const XPlan &x = (*p.plans)[0];
+                const uint64_t n = x.send_cnt[rank];
+                if (n && !p.self_in_place)
+                    HIPCHK(hipMemcpyAsync((char *)p.recv[0] + x.recv_off[rank] * p.elem,
+                                          (const char *)p.send[0] + x.send_off[rank] * p.elem, n * p.elem,
+                                          hipMemcpyDeviceToDevice, stream));
+            }
+        if (W == 1 && !self_rccl) return;
         if (ncclGroupStart() != ncclSuccess) throw Fail(RMC_E_COMM, "ncclGroupStart failed");
         for (const Payload &p : P) {
             const XPlan &x = (*p.plans)[0];
             for (int peer = 0; peer < W; peer++) {
+                if (peer == rank && !self_rccl) continue;
                 const uint64_t ns = x.send_cnt[peer], nr = x.recv_cnt[peer];
                 if (ns && ncclSend((const char *)p.send[0] + x.send_off[peer] * p.elem, ns * p.elem, ncclUint8, peer,
                                    comm, stream) != ncclSuccess)
@@ -2232,18 +2265,21 @@ struct rmc_ctx {
             }
             SDBG("0");
             // (2) successors to their owners: owner-grouped items, cursors preset to the groups
-            Payload items{&xp, std::vector<const void *>(NL), std::vector<void *>(NL), sizeof(XItem)};
+            Payload items{&xp, std::vector<const void *>(NL), std::vector<void *>(NL), sizeof(XItem), !self_rccl};
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
                 if (s.G) {
-                    uint32_t *hc = reinterpret_cast<uint32_t *>(s.hsum);
+                    // (pinned words 96..127 of hsum: nothing else uses them, and a later sync of the
+                    // round orders this copy before the next round writes them)
+                    uint32_t *hc = reinterpret_cast<uint32_t *>(s.hsum + 96);
                     for (int d = 0; d < W; d++) hc[d] = (uint32_t)xp[li].send_off[d];
                     HIPCHK(hipMemcpyAsync(s.ocnt, hc, W * 4, hipMemcpyHostToDevice, stream));
+                    // items for this shard itself go straight to its receive buffer
+                    const int64_t delta = (int64_t)xp[li].recv_off[s.id] - (int64_t)xp[li].send_off[s.id];
                     timed(PH_XCHG, [&] {
                         launch_route_place(s.fp, s.cnt, s.np, (uint32_t)MS, (uint32_t)W, s.ocnt, s.gblk, s.xs, s.perm,
-                                           stream);
+                                           self_rccl ? nullptr : s.xr, (uint32_t)s.id, delta, stream);
                     });
-                    HIPCHK(hipStreamSynchronize(stream));  // hsum is reused below
                 }
                 items.send[li] = s.xs;
                 items.recv[li] = s.xr;
@@ -2264,8 +2300,8 @@ struct rmc_ctx {
                     grow_seen(o, o.T_count + R);
                     const uint64_t cap = owner_table(o, R);
                     timed(PH_DEDUP, [&] {
-                        launch_owner_elect(o.xr, R, o.seen(), o.OT, o.OK, cap - 1, o.rslot, stream);
-                        launch_owner_flags(o.xr, R, o.rslot, o.OK, o.seen(), o.rflag, o.sum + 9, stream);
+                        launch_owner_elect(o.xr, R, o.seen(), o.OT, o.OK, cap - 1, o.ot_round, o.rslot, stream);
+                        launch_owner_flags(o.xr, R, o.rslot, o.OK, o.ot_round, o.seen(), o.rflag, o.sum + 9, stream);
                     });
                 });
                 // a failed owner answers "no winner" everywhere (the round is abandoned at the next agreement)
@@ -2459,7 +2495,7 @@ struct rmc_ctx {
             }
             std::vector<XPlan> xs_(NL), xw_(NL);
             Payload sides{&xs_, std::vector<const void *>(NL), std::vector<void *>(NL), 16};
-            Payload words_{&xw_, std::vector<const void *>(NL), std::vector<void *>(NL), 4};
+            Payload words_{&xw_, std::vector<const void *>(NL), std::vector<void *>(NL), 4, !self_rccl};
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
                 xs_[li] = make_plan(M2.data(), W, K2, s.id);
@@ -2497,7 +2533,15 @@ struct rmc_ctx {
                 trace_restart(o);
                 trace_fence(o);
                 timed(PH_OTHER, [&] {
-                    ring_copy_in(o, ring_wrap(o.nbase() + o.nxt_words, o.rcap), o.ib, words);
+                    const uint64_t at = ring_wrap(o.nbase() + o.nxt_words, o.rcap);
+                    const uint64_t a = xw_[li].recv_off[o.id], sw = xw_[li].recv_cnt[o.id];
+                    if (words_.self_in_place && sw) {  // this shard's own winners come from its outbox
+                        ring_copy_in(o, at, o.ib, a);
+                        ring_copy_in(o, ring_wrap(at + a, o.rcap), o.ob + xw_[li].send_off[o.id], sw);
+                        ring_copy_in(o, ring_wrap(at + a + sw, o.rcap), o.ib + a + sw, words - a - sw);
+                    } else {
+                        ring_copy_in(o, at, o.ib, words);
+                    }
                     launch_side_sizes(o.iside, n, o.isz, stream);
                     HIPCHK(hipMemsetAsync(o.isz + n, 0, 4, stream));
                     HIPCHK(hipcub::DeviceScan::ExclusiveSum(o.tmp, o.tmp_bytes, o.isz, o.ioff, (int)n + 1, stream));

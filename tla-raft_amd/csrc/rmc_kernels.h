@@ -188,11 +188,12 @@ struct XItem { unsigned long long x, y, key; };
 void launch_route_count(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
                         uint32_t *ocnt, hipStream_t s);
 void launch_route_place(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
-                        uint32_t *cursor, uint64_t g0, XItem *items, uint32_t *perm, hipStream_t s);
+                        uint32_t *cursor, uint64_t g0, XItem *items, uint32_t *perm, XItem *self_items, uint32_t self,
+                        int64_t self_delta, hipStream_t s);
 void launch_owner_elect(const XItem *it, uint64_t R, Seen seen, ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
-                        uint32_t *rslot, hipStream_t s);
-void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const unsigned long long *OK, Seen seen,
-                        uint32_t *flag, unsigned long long *inserted, hipStream_t s);
+                        uint32_t round, uint32_t *rslot, hipStream_t s);
+void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const unsigned long long *OK, uint32_t round,
+                        Seen seen, uint32_t *flag, unsigned long long *inserted, hipStream_t s);
 void launch_scatter_win(const uint32_t *perm, const uint32_t *flag, uint64_t G, const uint4 *score, uint32_t sw4,
                         const uint32_t *pnm, uint32_t maxsucc, uint32_t *lslot, uint32_t *wacc, hipStream_t s);
 void launch_side_sizes(const uint4 *side, uint64_t n, uint32_t *sz, hipStream_t s);

@@ -2395,9 +2395,12 @@ __global__ __launch_bounds__(256) void k_route_count(const ulonglong2 *__restric
 // next free item, preset to its start): {fingerprint, global key = (parent's global index in the
 // level << 10) | rank among its successors (< 1024, checked at create)} -- the key orders the level's successors as TLC
 // generates them -- and perm[item] = its slot q, for the owner's verdict to come back to.
+// Items owned by the source itself (owner == self) go straight to their place in its receive
+// buffer (self_items[pos + self_delta]): no copy of them through the exchange.
 __global__ __launch_bounds__(256) void k_route_place(const ulonglong2 *__restrict__ fp, const uint32_t *__restrict__ cnt,
                                                      uint64_t np, uint32_t maxsucc, uint32_t W, uint32_t *__restrict__ cursor,
-                                                     uint64_t g0, XItem *__restrict__ items, uint32_t *__restrict__ perm) {
+                                                     uint64_t g0, XItem *__restrict__ items, uint32_t *__restrict__ perm,
+                                                     XItem *__restrict__ self_items, uint32_t self, int64_t self_delta) {
     __shared__ uint32_t h[64], base[64];
     for (uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x; t0 < np; t0 += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t pl = t0 + threadIdx.x;
@@ -2417,7 +2420,9 @@ __global__ __launch_bounds__(256) void k_route_place(const ulonglong2 *__restric
             const ulonglong2 f = fp[q];
             const uint32_t o = fp_owner(f, W);
             const uint32_t pos = base[o] + atomicAdd(&h[o], 1u);
-            items[pos] = XItem{f.x, f.y, ((g0 + pl) << 10) | r};
+            const XItem it{f.x, f.y, ((g0 + pl) << 10) | r};
+            if (o == self && self_items) self_items[(int64_t)pos + self_delta] = it;
+            else items[pos] = it;
             perm[pos] = (uint32_t)q;
         }
         __syncthreads();
@@ -2425,44 +2430,58 @@ __global__ __launch_bounds__(256) void k_route_place(const ulonglong2 *__restric
 }
 
 // Owner: the received successors of the round.  A fingerprint already in the seen set loses;
-// otherwise it takes (or finds) its slot in the round's election table (OT: fingerprint, zero =
-// free, cleared before the round; OK: smallest key, all-ones before the round) and bids its key.
+// otherwise it takes (or finds) its slot in the round's election table and bids its key.  The table
+// is cleared only every 65533 rounds (owner_table): `round` counts the rounds since, and both words
+// of a slot carry its 16-bit tag round + 1 in their low bits, so a slot of an earlier round reads as
+// free, and a key word is the round's key below ((0xFFFF - tag) << 48) -- smaller than any earlier
+// round's -- so every bid just takes the minimum (OT: fingerprint, OK: smallest tagged key; the same
+// protocol as the fused election).
+__device__ __forceinline__ unsigned long long owner_key(uint32_t tag, uint64_t key) {
+    return ((unsigned long long)(0xFFFFu - tag) << 48) | key;  // key = global parent index << 10 | rank < 2^48
+}
+
 __global__ __launch_bounds__(256) void k_owner_elect(const XItem *__restrict__ it, uint64_t R, Seen seen,
                                                      ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
-                                                     uint32_t *__restrict__ rslot) {
+                                                     uint32_t round, uint32_t *__restrict__ rslot) {
+    const unsigned long long tag = round + 1u;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
         const XItem e = it[i];
         const ulonglong2 f = make_ulonglong2(e.x, e.y);
         if (seen_contains(seen, f)) { rslot[i] = LS_SEEN; continue; }
+        const unsigned long long xk = (f.x & ~0xFFFFull) | tag, yk = (f.y & ~0xFFFFull) | tag;
         // one exit at the bottom (no break): a claimer stores its y inside the loop, in the same
         // iteration as its CAS, before any lane of its wave waits for that y (a divergent break
         // lets the compiler defer the claimer's store until every lane has left the loop)
         uint64_t g = l_index(f, mask);
+        unsigned long long v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         bool done = false;
         while (!done) {
-            unsigned long long v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             bool next = false;
-            if (v == 0ull) {  // fp.x is odd (nonzero): 0 marks a free slot
-                const unsigned long long prev = atomicCAS(&OT[g].x, 0ull, f.x);
-                if (prev == 0ull) {
-                    __hip_atomic_store(&OT[g].y, f.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((v & 0xFFFFull) != tag) {  // free, or an earlier round's: claim it
+                const unsigned long long prev = atomicCAS(&OT[g].x, v, xk);
+                if (prev == v) {
+                    __hip_atomic_store(&OT[g].y, yk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     done = true;
                 } else {
                     v = prev;
                 }
             }
-            if (!done) {
-                if (v == f.x) {
+            if (!done && (v & 0xFFFFull) == tag) {
+                if (v == xk) {
                     const unsigned long long y = __hip_atomic_load(&OT[g].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (y == f.y) done = true;
-                    else if (y != 0ull) next = true;  // 0: the claimer's y not visible yet, this slot again
+                    if (y == yk) done = true;
+                    else if ((y & 0xFFFFull) == tag) next = true;
+                    else v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // y not visible yet
                 } else {
                     next = true;
                 }
             }
-            if (next) g = (g + 1) & mask;
+            if (next) {
+                g = (g + 1) & mask;
+                v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
-        atomicMin(&OK[g], e.key);
+        atomicMin(&OK[g], owner_key((uint32_t)tag, e.key));
         rslot[i] = (uint32_t)g;
     }
 }
@@ -2471,13 +2490,14 @@ __global__ __launch_bounds__(256) void k_owner_elect(const XItem *__restrict__ i
 // before); each winner goes into the seen set, *inserted counts them.
 __global__ __launch_bounds__(256) void k_owner_flags(const XItem *__restrict__ it, uint64_t R,
                                                      const uint32_t *__restrict__ rslot,
-                                                     const unsigned long long *__restrict__ OK, Seen seen,
+                                                     const unsigned long long *__restrict__ OK, uint32_t round, Seen seen,
                                                      uint32_t *__restrict__ flag, unsigned long long *inserted) {
+    const uint32_t tag = round + 1u;
     uint32_t mine = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t g = rslot[i];
         const XItem e = it[i];
-        const bool w = g != LS_SEEN && OK[g] == e.key;
+        const bool w = g != LS_SEEN && OK[g] == owner_key(tag, e.key);
         flag[i] = w ? 1u : 0u;
         if (w) {
             seen_insert(seen, make_ulonglong2(e.x, e.y));
@@ -2535,18 +2555,21 @@ void launch_route_count(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, 
     if (np) hipLaunchKernelGGL(k_route_count, dim3(grid256(np)), dim3(256), 0, s, fp, cnt, np, maxsucc, W, ocnt);
 }
 void launch_route_place(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
-                        uint32_t *cursor, uint64_t g0, XItem *items, uint32_t *perm, hipStream_t s) {
+                        uint32_t *cursor, uint64_t g0, XItem *items, uint32_t *perm, XItem *self_items, uint32_t self,
+                        int64_t self_delta, hipStream_t s) {
     if (np)
         hipLaunchKernelGGL(k_route_place, dim3(grid256(np)), dim3(256), 0, s, fp, cnt, np, maxsucc, W, cursor, g0, items,
-                           perm);
+                           perm, self_items, self, self_delta);
 }
 void launch_owner_elect(const XItem *it, uint64_t R, Seen seen, ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
-                        uint32_t *rslot, hipStream_t s) {
-    if (R) hipLaunchKernelGGL(k_owner_elect, dim3(grid256(R)), dim3(256), 0, s, it, R, seen, OT, OK, mask, rslot);
+                        uint32_t round, uint32_t *rslot, hipStream_t s) {
+    if (R) hipLaunchKernelGGL(k_owner_elect, dim3(grid256(R)), dim3(256), 0, s, it, R, seen, OT, OK, mask, round, rslot);
 }
-void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const unsigned long long *OK, Seen seen,
-                        uint32_t *flag, unsigned long long *inserted, hipStream_t s) {
-    if (R) hipLaunchKernelGGL(k_owner_flags, dim3(grid256(R)), dim3(256), 0, s, it, R, rslot, OK, seen, flag, inserted);
+void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const unsigned long long *OK, uint32_t round,
+                        Seen seen, uint32_t *flag, unsigned long long *inserted, hipStream_t s) {
+    if (R)
+        hipLaunchKernelGGL(k_owner_flags, dim3(grid256(R)), dim3(256), 0, s, it, R, rslot, OK, round, seen, flag,
+                           inserted);
 }
 void launch_scatter_win(const uint32_t *perm, const uint32_t *flag, uint64_t G, const uint4 *score, uint32_t sw4,
                         const uint32_t *pnm, uint32_t maxsucc, uint32_t *lslot, uint32_t *wacc, hipStream_t s) {
