@@ -55,14 +55,20 @@ TIMED_PHASES = 1 << PHASES.index("expand_hash")  # HIP-event timing of the domin
 TIMING_EVERY = 4
 
 
-def alg_bytes(phase, F, G, N, S, CCWB, slot_bytes=16, SWB=32):
+def alg_bytes(phase, F, G, N, S, CCWB, slot_bytes=16, SWB=32, split=False):
     """Algorithmic HBM bytes of one phase of the fused single-GPU level (DESIGN.md "Kernels"):
     F parents of S-byte records (S = the run's average packed record: CCWB core bytes + message
     ids), G generated successors, N new states; SWB = staging bytes per successor (the acting row),
-    slot_bytes = seen-set slot (16 full, 8 compact)."""
+    slot_bytes = seen-set slot (16 full, 8 compact).  split: the host-driven chunk's probe and
+    election run in k_probe ("probe"), not in the expansion."""
+    if phase == "expand_hash" and split:  # k_expand<FUSED>, split chunk: staged row + fp + extra-words word out
+        return F * S + F * 8 + G * (SWB + 16 + 4)
     if phase == "expand_hash":   # k_expand<FUSED>: parents in, count + |msgs| out; per successor: staged row +
         # fp + election slot, one seen-set probe; per new fingerprint at least one election (16-B slot, 8-B word, count)
         return F * S + F * 8 + G * (SWB + 16 + 4) + G * slot_bytes + N * (16 + 8 + 4)
+    if phase == "probe":         # k_probe: per parent its count; per successor fp + extra words in, verdict out,
+        # one seen-set probe; per new fingerprint at least one election (16-B slot, 8-B word, count)
+        return F * 4 + G * (16 + 4 + 4) + G * slot_bytes + N * (16 + 8 + 4)
     if phase == "dedup":         # k_wincount: per parent successor count, packed winner count (read + re-arm),
         # |msgs|; out winner count and the two scans
         return F * (4 + 4 + 4 + 4 + 4 + 4 + 4)
@@ -490,6 +496,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_scale:
         mc.close()  # the at-scale run gets the whole device (this checker's chunk buffers are ~12 GB)
         line["at_scale"] = at_scale(local, probes_per_s=pk_hbm)
+        if not args.no_cpu_baseline:
+            line["cpu_baseline_at_scale"] = cpu_baseline_at_scale(local)
     if rank == 0 and sharded is not None:
         line["at_scale_sharded"] = sharded
     if rank == 0 and sharded_c4 is not None:
@@ -501,6 +509,75 @@ def main():
     mc.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def counters_at_scale(workload="raftcfg"):
+    """The at-scale kernel counters committed under profiles/ (tools/pmc_scale.sh on Raft.cfg's first
+    levels + tools/pmc_scale_report.py): per kernel, the HBM traffic (PMC FETCH_SIZE x2 + WRITE_SIZE)
+    and the algorithmic bytes of its launches at >= 0.5 M parents against their HIP-event time, and
+    the VALU-issue fraction (SQ_INSTS_VALU).  Recomputable from the per-level rows in the file."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_scale_{workload}_levels.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    out = {"source": os.path.relpath(files[-1], ROOT), "workload": d.get("workload")}
+    for k, v in d.get("kernels", {}).items():
+        a = v["aggregate"]
+        out[k] = {x: a[x] for x in ("levels", "alg_frac", "hbm_frac", "ratio", "ratio_fetch_x1", "valu_frac",
+                                    "valu_per_successor", "alg_GBps", "hbm_GBps")}
+    return out
+
+
+def cpu_baseline_at_scale(device, workload="raftcfg", max_states=20_000_000):
+    """The CPU restatement (oracle/raft_mt.c, every host thread this job may use) on the at-scale workload's
+    first levels -- up to the first level boundary past max_states (Raft.cfg: 24 levels, 21.6 M states, a
+    bounded 10-30 s sample) -- and the GPU over the same levels (a fresh checker, Init + one rmc_step per
+    level): same workload, same host, same levels."""
+    import raftmc
+    so = os.path.join(ROOT, "oracle", "build", "libraft_mt.so")
+    if not os.path.exists(so):
+        return None
+    w = WORKLOADS[workload]
+    lib = ctypes.CDLL(so)
+    P64 = ctypes.POINTER(ctypes.c_uint64)
+    lib.orc_mt_levels.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint64, P64, P64, ctypes.c_int, P64, P64,
+                                                       ctypes.POINTER(ctypes.c_int)]
+    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    cap = 256
+    d, g = (ctypes.c_uint64 * cap)(), (ctypes.c_uint64 * cap)()
+    dist, gen, depth = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+    t0 = time.perf_counter()
+    v = lib.orc_mt_levels(w["n"], w["V"], w["E"], w["R"], threads, max_states, d, g, cap, ctypes.byref(dist),
+                          ctypes.byref(gen), ctypes.byref(depth))
+    dt = time.perf_counter() - t0
+    D = depth.value
+    cpu_levels = list(d[:D])
+    # the GPU's levels 1..D: Init plus the expansions of levels 1..D-1
+    cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
+                             invariants=("Inv",), check_deadlock=False, device=device)
+    with raftmc.ModelChecker(cfg) as mc:
+        mc.init()  # (buffers grow on the way: one untimed pass first)
+        for _ in range(D - 1):
+            mc.step()
+        mc.reset()
+        t0 = time.perf_counter()
+        gpu_levels = [mc.init().new_states]
+        for _ in range(D - 1):
+            gpu_levels.append(mc.step().new_states)
+        gpu_s = time.perf_counter() - t0
+    return {"value": round(dist.value / dt, 1), "unit": "distinct states/s", "cores": threads, "cpu_model": cpu_model(),
+            "kind": "port", "levels": D, "distinct_states": dist.value, "seconds": round(dt, 3),
+            "gpu_seconds_same_levels": round(gpu_s, 4),
+            "gpu_distinct_per_s_same_levels": round(dist.value / gpu_s, 1) if gpu_s > 0 else None,
+            "gpu_over_cpu_same_levels": round(dt / gpu_s, 1) if gpu_s > 0 else None,
+            "levels_match_gpu": cpu_levels == gpu_levels, "verdict_code": v,
+            "sample": f"Raft.cfg levels 1-{D} ({dist.value} distinct states) by oracle/raft_mt.c on {threads} threads "
+                      f"(C restatement of Raft.tla, exact canonical forms, level-synchronous first-wins BFS; not TLC: no "
+                      f"JVM/tla2tools.jar on the box), {dt:.1f} s; the GPU's seconds are those of the same levels of the "
+                      f"at-scale run (the small early levels are latency-bound on the GPU, so the ratio over the whole "
+                      f"exhaustion is larger)"}
 
 
 def at_scale(device, workload="raftcfg", probes_per_s=None):
@@ -523,12 +600,14 @@ def at_scale(device, workload="raftcfg", probes_per_s=None):
         res = mc.run()
         dt = time.perf_counter() - t0
     ms = sum(ls.kernel_ms[PHASES.index("expand_hash")] for ls in cold.levels)
-    F = sum(ls.expanded for ls in cold.levels)
-    G = sum(ls.generated for ls in cold.levels)
-    N = sum(ls.new_states for ls in cold.levels)
     S, CCWB = record_bytes(cold, cfg)
-    gbs = alg_bytes("expand_hash", F, G, N, S, CCWB, cold.seen_slot_bytes, staging_bytes(cfg)) / (ms / 1e3) / 1e9 \
-        if ms > 0 else 0.0
+    # each level's expansion bytes: split (k_probe) levels of >= 2^16 parents without the probe and election
+    alg = 0
+    for i, ls in enumerate(cold.levels[:-1]):
+        nxt = cold.levels[i + 1]
+        alg += alg_bytes("expand_hash", nxt.expanded, nxt.generated, nxt.new_states, S, CCWB, cold.seen_slot_bytes,
+                         staging_bytes(cfg), split=nxt.expanded >= (1 << 16))
+    gbs = alg / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     gold = {}
     gpath = os.path.join(ROOT, "tests", "golden", "levels_prefix.json")
     if os.path.exists(gpath):
@@ -549,6 +628,7 @@ def at_scale(device, workload="raftcfg", probes_per_s=None):
             "record_bytes_avg": round(S, 2),
             "expand_kernel_ms": round(ms, 3), "expand_alg_GBps": round(gbs, 1),
             "expand_frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
+            "counters": counters_at_scale(workload),
             "survey_roofline": survey_roofline(res.levels, S, dt, probes_per_s)}
 
 

@@ -1,6 +1,7 @@
 """CPU tests of the product's host side: C-ABI exports, cfg parsing, spec identification,
 launcher argument handling.  No compute call is made here (no GPU in this container)."""
 import ctypes
+import json
 import os
 import re
 import subprocess
@@ -229,3 +230,40 @@ def test_bench_xgmi_model():
     per = 100 * 28 + 800 + 16 * 20 + 10 * 28
     assert bench.xgmi_model(levels, 2) == per // 2
     assert bench.xgmi_model(levels, 8) == int(per * 7 / 8)
+
+
+def _bench():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench
+
+
+def test_bench_split_bytes_account_for_the_probe_pass():
+    """A split chunk's expansion + k_probe move the fused expansion's algorithmic bytes plus what the
+    split adds: each successor's fingerprint and extra-words word read back (20 B) and its verdict
+    written (4 B), and each parent's count read (4 B)."""
+    bench = _bench()
+    F, G, N, S = 1000, 5200, 1000, 69.5
+    fused = bench.alg_bytes("expand_hash", F, G, N, S, 16, 8, 32)
+    split = bench.alg_bytes("expand_hash", F, G, N, S, 16, 8, 32, split=True) + bench.alg_bytes("probe", F, G, N, S, 16, 8)
+    assert split == fused + F * 4 + G * 24
+
+
+def test_bench_counters_at_scale_read_from_profiles():
+    """bench.py's at-scale counters come from the newest committed per-level PMC report, and every
+    aggregate is recomputable from its per-level rows."""
+    bench = _bench()
+    c = bench.counters_at_scale()
+    if c is None:
+        pytest.skip("no at-scale PMC report committed")
+    d = json.load(open(os.path.join(ROOT, c["source"])))
+    for k, v in d["kernels"].items():
+        rows = v["per_level"]
+        alg = sum(r["alg_bytes"] for r in rows)
+        hbm = sum(r["hbm_bytes"] for r in rows)
+        ms = sum(r["ms"] for r in rows)
+        assert abs(hbm / alg - v["aggregate"]["ratio"]) < 2e-3
+        assert abs(alg / ms / 1e6 / bench.HBM_PEAK_GBS - v["aggregate"]["alg_frac"]) < 2e-5
+        assert c[k]["ratio"] == v["aggregate"]["ratio"]

@@ -218,6 +218,15 @@ int usage(const char *msg) {
 
 }  // namespace
 
+// RMC_LAUNCHER_TIMES=1: seconds since process start at each phase, on stderr (stdout stays TLC's)
+static const auto g_t_start = std::chrono::steady_clock::now();
+static void phase_time(const char *what) {
+    static const bool on = std::getenv("RMC_LAUNCHER_TIMES") && std::string(std::getenv("RMC_LAUNCHER_TIMES")) == "1";
+    if (on)
+        std::fprintf(stderr, "raftmc: %s at %.3f s\n", what,
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - g_t_start).count());
+}
+
 int main(int argc, char **argv) {
     std::string tla_path, cfg_path;
     int check_deadlock = 1, device = -1, msgcap = 0, seenlog2 = 0, workers = 1;
@@ -289,7 +298,9 @@ int main(int argc, char **argv) {
     std::printf("Starting... (%s)\n", now_str().c_str());
     const auto t0 = std::chrono::steady_clock::now();
     void *ctx = nullptr;
+    phase_time("create");
     int rc = rmc_create(&cfg, &ctx);
+    phase_time("created");
     if (rc != RMC_OK) { std::printf("Error: could not start the GPU model checker (code %d)\n", rc); return 75; }
     rmc_level_stats st;
     if (!recover_dir.empty()) {
@@ -418,6 +429,8 @@ int main(int argc, char **argv) {
     std::printf("Finished in %.2fs at (%s)\n", el, now_str().c_str());
     std::printf("GPU: %.0f distinct states/s over %.3f s of BFS levels (MI355X, 1 device).\n",
                 gpu_seconds > 0 ? res.distinct / gpu_seconds : 0.0, gpu_seconds);
+    phase_time("destroy");
     rmc_destroy(ctx);
+    phase_time("destroyed");
     return exit_code;
 }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one configuration level by level on the GPU and print TLC-style progress per level.
 
-usage: explore.py N V E R [--budget SECONDS] [--seeded] [--chunk G] [--seenlog2 K] [--rccl1 [--shard-min K]]"""
+usage: explore.py N V E R [--budget SECONDS] [--levels L] [--seeded] [--chunk G] [--seenlog2 K] [--rccl1 [--shard-min K]]"""
 import argparse
 import json
 import os
@@ -18,6 +18,7 @@ ap.add_argument("V", type=int)
 ap.add_argument("E", type=int)
 ap.add_argument("R", type=int)
 ap.add_argument("--budget", type=float, default=120)
+ap.add_argument("--levels", type=int, default=0, help="stop after expanding this many levels (0: no limit)")
 ap.add_argument("--seeded", action="store_true")
 ap.add_argument("--chunk", type=int, default=0)
 ap.add_argument("--seenlog2", type=int, default=0)
@@ -41,7 +42,7 @@ ls = mc.init()
 t1 = time.time()
 rows = []
 stopped = ""
-while ls.status == "ok" and time.time() - t1 < a.budget:
+while ls.status == "ok" and time.time() - t1 < a.budget and not (a.levels and ls.level >= a.levels):
     try:
         ls = mc.step()
     except raftmc.RmcError as e:  # capacity: report how far one GPU got

@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
-"""At-scale counters of the expansion and commit kernels, per BFS level (tools/pmc_scale.sh output).
+"""At-scale counters of the expansion, probe and commit kernels, per BFS level (tools/pmc_scale.sh output).
 
-tools/pmc_scale.sh runs tools/explore.py (default 3 servers / 2 values / MaxElection 2: 18.5 M states,
-levels of up to 1.5 M parents, a compact seen set of ~140 GB -- far beyond the 256 MB Infinity Cache,
-so FETCH_SIZE / WRITE_SIZE are HBM traffic) once per counter pass.  Every level is one dispatch of
-each kernel, so dispatch k (in dispatch order) is level k + 1, and the explore log of the same pass
-gives that level's parents F, successors G, new states N, average record bytes S and the HIP-event
-duration of each kernel.  Per level this prints and records:
+tools/pmc_scale.sh runs tools/explore.py once per counter pass: by default 3 servers / 2 values /
+MaxElection 2 (18.5 M states), or Raft.cfg's first levels (CFG="3 2 3 3 --levels 44"); either way the
+compact seen set is ~140 GB -- far beyond the 256 MB Infinity Cache, so FETCH_SIZE / WRITE_SIZE are
+HBM traffic.  explore.py steps level by level on the host-driven path: a level of F parents is
+ceil(F / chunk_parents) chunks, one dispatch of each kernel per chunk (k_probe only for chunks of at
+least --split-min parents), in dispatch order.  The explore log of the same pass gives each level's
+parents F, successors G, new states N, average record bytes S and the HIP-event time of each kernel
+phase.  Per level (dispatches of a level summed) this records:
 
   alg_bytes    bench.py alg_bytes() -- the algorithmic bytes of the kernel
   hbm_bytes    2 * 1024 * FETCH_SIZE + 1024 * WRITE_SIZE (MI355X_MICROARCH.md rocprofv3 section; the
@@ -16,7 +18,7 @@ duration of each kernel.  Per level this prints and records:
   valu_frac    SQ_INSTS_VALU / duration against 256 CUs x 4 SIMDs x 2.4 GHz / 2 wave64 issues per s
   alg_GBps     alg_bytes / duration, hbm_GBps = hbm_bytes / duration (peak 8 TB/s)
 
-usage: pmc_scale_report.py gpurun_out/pmcs out.json [--min-parents 500000]"""
+usage: pmc_scale_report.py gpurun_out/pmcs out.json [--min-parents 500000] [--n 3 --V 2]"""
 import argparse
 import collections
 import csv
@@ -30,7 +32,9 @@ sys.path.insert(0, ROOT)
 from bench import HBM_PEAK_GBS, VALU_PEAK, alg_bytes  # noqa: E402
 
 LEVEL = re.compile(r"^L\s*(\d+) F=\s*(\d+) G=\s*(\d+) N=\s*(\d+) tot=\s*\d+\s+[\d.]+ms \[([^\]]*)\].*rec=([\d.]+)B")
-KERNELS = {"expand": ("k_expand", 1, "expand_hash"), "commit": ("k_commit", 3, "materialize")}
+# name -> (kernel name fragment, explore phase column of its HIP-event time, alg_bytes phase)
+KERNELS = {"expand": ("k_expand", 1, "expand_hash"), "probe": ("k_probe", 5, "probe"),
+           "commit": ("k_commit", 3, "materialize")}
 
 
 def levels_of(log):
@@ -58,38 +62,58 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--min-parents", type=int, default=500000)
     ap.add_argument("--n", type=int, default=3)
+    ap.add_argument("--V", type=int, default=2)
+    ap.add_argument("--split-min", type=int, default=1 << 16)
+    ap.add_argument("--workload", default="")
     a = ap.parse_args()
-    report = {"workload": "tools/explore.py 3 2 2 3 (n3 V2 E2: 18.5 M states, 51 levels; compact seen set beyond the "
-                          "Infinity Cache)", "hbm_peak_GBps": HBM_PEAK_GBS, "valu_peak_insts_per_s": VALU_PEAK,
-              "note": "one dispatch per level per kernel; durations are the explore run's HIP events of the same pass",
+    maxsucc = 64 + a.n * (4 + a.V + a.n - 1)           # rmc_kernels.hip Spec::MAXS (one message round)
+    chunk = min((1 << 28) // maxsucc, 1024 * 4096)     # rmc_engine.hip chunk_parents on one GPU
+    report = {"workload": a.workload or "tools/explore.py (see the pass logs)", "hbm_peak_GBps": HBM_PEAK_GBS,
+              "valu_peak_insts_per_s": VALU_PEAK, "chunk_parents": chunk,
+              "note": "dispatches of a level summed; durations are the explore run's HIP events of the same pass",
               "kernels": {}}
     swb = 48 if a.n >= 4 else 32
+    lv_f = levels_of(os.path.join(a.root, "fetch.log"))
     for key, (kname, ph, phase) in KERNELS.items():
-        rows, tot = [], collections.Counter()
         fetch = per_dispatch(os.path.join(a.root, "fetch", "run_counter_collection.csv"), kname)
         write = per_dispatch(os.path.join(a.root, "write", "run_counter_collection.csv"), kname)
         sq = per_dispatch(os.path.join(a.root, "sqa", "run_counter_collection.csv"), kname)
-        lv_f = levels_of(os.path.join(a.root, "fetch.log"))
-        if not (len(fetch) == len(write) == len(sq) == len(lv_f)):
-            sys.exit(f"{kname}: dispatches {len(fetch)}/{len(write)}/{len(sq)} vs {len(lv_f)} levels")
-        for i, L in enumerate(lv_f):
-            if L["F"] < a.min_parents:
+        if not fetch:
+            continue
+        # dispatches per level
+        per = []
+        for L in lv_f:
+            nch = max(1, -(-L["F"] // chunk))
+            if key == "probe":
+                nch = sum(1 for c in range(nch) if min(chunk, L["F"] - c * chunk) >= a.split_min)
+            per.append(nch)
+        if not (len(fetch) == len(write) == len(sq) == sum(per)):
+            sys.exit(f"{kname}: dispatches {len(fetch)}/{len(write)}/{len(sq)} vs {sum(per)} expected from the levels")
+        rows, tot, k = [], collections.Counter(), 0
+        for L, nch in zip(lv_f, per):
+            d0, k = k, k + nch
+            if L["F"] < a.min_parents or nch == 0:
                 continue
             ms = L["ms"][ph]
-            alg = alg_bytes(phase, L["F"], L["G"], L["N"], L["rec"], 0, 8, swb)
-            rd, wr = 1024 * fetch[i]["FETCH_SIZE"], 1024 * write[i]["WRITE_SIZE"]
+            split = L["F"] >= a.split_min  # (every chunk of such a level is split at Raft.cfg's sizes)
+            alg = alg_bytes(phase, L["F"], L["G"], L["N"], L["rec"], 0, 8, swb, split=split)
+            rd = 1024 * sum(fetch[i]["FETCH_SIZE"] for i in range(d0, k))
+            wr = 1024 * sum(write[i]["WRITE_SIZE"] for i in range(d0, k))
             hbm = 2 * rd + wr
-            valu = sq[i]["SQ_INSTS_VALU"]
-            rows.append({"level": L["level"], "parents": L["F"], "successors": L["G"], "new": L["N"], "ms": ms,
-                         "alg_bytes": round(alg), "hbm_bytes": round(hbm), "hbm_bytes_fetch_x1": round(rd + wr),
+            valu = sum(sq[i]["SQ_INSTS_VALU"] for i in range(d0, k))
+            rows.append({"level": L["level"], "parents": L["F"], "successors": L["G"], "new": L["N"], "chunks": nch,
+                         "ms": ms, "alg_bytes": round(alg), "hbm_bytes": round(hbm), "hbm_bytes_fetch_x1": round(rd + wr),
                          "ratio": round(hbm / alg, 3), "ratio_fetch_x1": round((rd + wr) / alg, 3),
                          "alg_GBps": round(alg / ms / 1e6, 1), "hbm_GBps": round(hbm / ms / 1e6, 1),
                          "valu_insts": round(valu), "valu_per_successor": round(valu / max(1, L["G"]), 1),
                          "valu_frac": round(valu / (ms / 1e3) / VALU_PEAK, 4)})
-            for k, v in (("alg", alg), ("hbm", hbm), ("hbm1", rd + wr), ("ms", ms), ("valu", valu), ("G", L["G"])):
-                tot[k] += v
-        agg = {"levels": len(rows), "alg_bytes": round(tot["alg"]), "hbm_bytes": round(tot["hbm"]),
-               "ratio": round(tot["hbm"] / tot["alg"], 3), "ratio_fetch_x1": round(tot["hbm1"] / tot["alg"], 3),
+            for kk, v in (("alg", alg), ("hbm", hbm), ("hbm1", rd + wr), ("ms", ms), ("valu", valu), ("G", L["G"])):
+                tot[kk] += v
+        if not rows:
+            continue
+        agg = {"levels": len(rows), "ms": round(tot["ms"], 3), "alg_bytes": round(tot["alg"]),
+               "hbm_bytes": round(tot["hbm"]), "ratio": round(tot["hbm"] / tot["alg"], 3),
+               "ratio_fetch_x1": round(tot["hbm1"] / tot["alg"], 3),
                "alg_GBps": round(tot["alg"] / tot["ms"] / 1e6, 1), "hbm_GBps": round(tot["hbm"] / tot["ms"] / 1e6, 1),
                "alg_frac": round(tot["alg"] / tot["ms"] / 1e6 / HBM_PEAK_GBS, 5),
                "hbm_frac": round(tot["hbm"] / tot["ms"] / 1e6 / HBM_PEAK_GBS, 5),
