@@ -481,6 +481,7 @@ struct rmc_ctx {
         P.t.perms = d_perms;
         P.t.seeds = d_seeds;
         P.t.np = np;
+        P.t.bmw = (uint32_t)((U.info.size() + 31) / 32);
         P.seen = s.seen();
         P.rcap = ~0ull;  // fixed-stride buffers unless a ring is set
         P.err = s.err;

@@ -15,6 +15,7 @@ struct Tables {
     const uint8_t *perms;     // [np][MAXN] server permutations (pi[i] = image of i)
     const uint64_t *seeds;    // [2][MAXN + MAXN*MAXN] position seeds of the structured hash
     int np;
+    uint32_t bmw;             // 32-bit words of a bitmap over the universe's ids: ceil(U / 32)
 };
 
 // Seen set (TLC's FPSet): open addressing over 128-bit fingerprints {x | 1, y}.

@@ -68,6 +68,9 @@ extern "C" int rmc_debug_phases(unsigned long long *out, int reset) {
 #ifndef RMC_EXPAND_PREFETCH_MSGS  // k_expand: the next parent's message-table words fetched ahead
 #define RMC_EXPAND_PREFETCH_MSGS 1
 #endif
+#ifndef RMC_MSG_BITMAP  // k_expand: m \in msgs by an LDS bitmap of the parent's ids (0: binary search)
+#define RMC_MSG_BITMAP 1
+#endif
 #ifndef RMC_WIDE_WAVES
 #define RMC_WIDE_WAVES 2
 #endif
@@ -174,6 +177,11 @@ __device__ __forceinline__ uint32_t lw_byte(uint32_t lw, uint32_t x) {  // x >= 
 }
 
 // membership in the parent's sorted id list (LDS)
+// m \in msgs for the parent of the wave: one LDS read of the wave's bitmap over the universe's ids
+// (k_expand builds it with the parent: msg_bitmap); replaced a binary search over the sorted ids --
+// a chain of up to 7 dependent LDS reads per test, several tests per successor kind
+__device__ __forceinline__ bool in_msgs(const uint32_t *bm, uint32_t id) { return (bm[id >> 5] >> (id & 31u)) & 1u; }
+
 __device__ __forceinline__ bool has_id(const uint16_t *ids, uint32_t nm, uint32_t id) {
     uint32_t lo = 0, hi = nm;
     while (lo < hi) {
@@ -569,7 +577,25 @@ struct Wave {
     uint64_t idw;        // ring position of the parent's first message-id word
     uint32_t id[MR];     // message id owned by this lane per round (0xFFFF = none)
     uint32_t inf[MR];
+    const uint32_t *bm;  // LDS bitmap of the parent's message ids (msg_bitmap), or nullptr: binary search
 };
+
+// membership test of the evaluation: the bitmap when the kernel built one, else the sorted ids
+template <int N, int V, int MR>
+__device__ __forceinline__ bool msg_in(const Wave<N, V, MR> &W, const uint16_t *ids, uint32_t id) {
+    return W.bm ? in_msgs(W.bm, id) : has_id(ids, W.nm, id);
+}
+
+// The wave's parent's ids as a bitmap in LDS (bmw words): cleared, then one LDS OR per message.
+template <int N, int V, int MR>
+__device__ __forceinline__ void msg_bitmap(uint32_t *bm, uint32_t bmw, const Wave<N, V, MR> &W, int lane) {
+    for (uint32_t i = (uint32_t)lane; i < bmw; i += 64) bm[i] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < MR; r++)
+        if ((uint32_t)(r * 64 + lane) < W.nm) atomicOr(&bm[W.id[r] >> 5], 1u << (W.id[r] & 31u));
+    __syncthreads();
+}
 
 // ---- message-id lookups of the actions, issued before any branch -------------------------------
 // An action that sends a message looks its id up in nat2id; done inside the divergent action
@@ -708,7 +734,7 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
         const uint32_t llt = lw_term(lw, ll), mlli = mi_x1(m), mllt = mi_x2(m);
         if (!(mllt > llt || (mllt == llt && mlli >= ll))) return;
         const uint32_t g = pid;  // nat2id[nat_vresp(s, src, mt)]
-        if (has_id(ids, W.nm, g)) return;
+        if (msg_in(W, ids, g)) return;
         o.c[Lo::W_VF] = setnib(o.c[Lo::W_VF], s, src);
         o.add[0] = g; o.nadd = 1;
         ainf[0] = minfo(VRESP, s, src, mt, 0, 0, 0, 0, 0, 0);
@@ -738,14 +764,14 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
                 o.lw = nlw;
                 o.c[Lo::W_LL] = setnib(o.c[Lo::W_LL], s, nl);
             }
-            if (!has_id(ids, W.nm, resp)) {
+            if (!msg_in(W, ids, resp)) {
                 o.add[0] = resp; o.nadd = 1;
                 ainf[0] = minfo(ARESP, s, src, mt, pli + ent, 1, 0, 0, 0, 0);
             }
             o.key = slot_key(s, FAE, k);
         } else {
             const uint32_t resp = pid;  // nat2id[nat_aresp(s, src, mt, pli, FALSE)]
-            if (has_id(ids, W.nm, resp)) return;
+            if (msg_in(W, ids, resp)) return;
             o.add[0] = resp; o.nadd = 1;
             ainf[0] = minfo(ARESP, s, src, mt, pli, 0, 0, 0, 0, 0);
             o.key = slot_key(s, FRE, k);
@@ -824,7 +850,7 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
             uint32_t id = 0;
 #pragma unroll
             for (int i = 0; i < N - 1; i++) id = i == ix ? sid[i] : id;
-            if (!has_id(ids, W.nm, id)) {
+            if (!msg_in(W, ids, id)) {
 #pragma unroll
                 for (int a = 0; a < S::NADD; a++) o.add[a] = ((uint32_t)a == na) ? id : o.add[a];
                 ainf[na] = minfo(VREQ, s, (uint32_t)p, term, ll, llt, 0, 0, 0, 0);
@@ -887,7 +913,7 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
         const uint32_t ent = ni <= ll ? 1u : 0u;
         const uint32_t eb = ent ? lw_byte(lw, ni) : 0u;
         const uint32_t id = sid[0];  // nat2id[nat_areq(s, dst, ct, pli, plt, ent, eb, ci)]
-        if (has_id(ids, W.nm, id)) return;  // m \notin msgs
+        if (msg_in(W, ids, id)) return;  // m \notin msgs
         o.c[Lo::W_PEND] = W.c[Lo::W_PEND] | (1u << pb);
         o.add[0] = id;
         o.nadd = 1;
@@ -1374,6 +1400,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
     __shared__ uint32_t sRk[MAXG], sKoff[MAXG], sTl[SIG ? 64 : 1];
     __shared__ ulonglong2 sBest[MAXG];
     __shared__ uint32_t sAinf[(MR + 1) * 64 * S::NADD];  // info words of the messages each candidate adds
+    extern __shared__ uint32_t sBM[];                    // bitmap of the parent's message ids (P.t.bmw words)
     if (MODE == M_FUSED && !level_args(P)) return;
     // device loop: the levels committed so far go to the host as this level starts (the write to
     // host memory completes in the shadow of the expansion; see finish_level)
@@ -1425,6 +1452,12 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
         } else {
             load_parent_words<N, V, MR, SUMS>(P, start, nrw0, nrw1, lane, W, ids, M0, M1, pcore);
         }
+#if RMC_MSG_BITMAP
+        msg_bitmap<N, V, MR>(sBM, P.t.bmw, W, lane);
+        W.bm = sBM;
+#else
+        W.bm = nullptr;
+#endif
         PHASE(0);
         Succ<N, V, MR> cand[NC];
         uint32_t akey = KEY_NONE;
@@ -2253,12 +2286,13 @@ static inline unsigned grid_for(uint64_t n) {
 
 template <int N, int V, int MR, bool BFV = false>
 struct Launch {
+    static size_t bm_bytes(const KParams &P) { return RMC_MSG_BITMAP ? (size_t)P.t.bmw * 4 : 0; }
     static void single(const KParams &P, hipStream_t s) {
-        hipLaunchKernelGGL((k_expand<N, V, MR, M_SINGLE, BFV>), dim3(1), dim3(64), 0, s, P);
+        hipLaunchKernelGGL((k_expand<N, V, MR, M_SINGLE, BFV>), dim3(1), dim3(64), bm_bytes(P), s, P);
     }
     static void fused(const KParams &P, hipStream_t s) {
-        hipLaunchKernelGGL((k_expand<N, V, MR, M_FUSED, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s,
-                           P);
+        hipLaunchKernelGGL((k_expand<N, V, MR, M_FUSED, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64),
+                           bm_bytes(P), s, P);
     }
     static void probe(const KParams &P, uint64_t np, hipStream_t s) {
         constexpr int MX = Spec<N, V, MR>::MAXS + (BFV ? Spec<N, V, MR>::MCAP : 0);

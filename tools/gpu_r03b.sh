@@ -17,4 +17,9 @@ if [ -d scratch_myrun ]; then
   ( cd scratch_myrun && RMC_LAUNCHER_TIMES=1 timeout -k 10 200 bash ../tla-raft_amd/myrun.sh > ../gpurun_out/myrun_stdout.txt 2> ../gpurun_out/myrun_stderr.txt; cp raft.log ../gpurun_out/myrun_raft.log ) || exit 1
   grep "raftmc:" gpurun_out/myrun_raft.log gpurun_out/myrun_stderr.txt; tail -3 gpurun_out/myrun_raft.log
 fi
+if [ -f tla-raft_amd/build_prof/librmc.so ]; then
+  step phase_prof
+  RMC_LIBRARY=tla-raft_amd/build_prof/librmc.so timeout -k 10 200 python -u tools/phase_prof.py 3 2 3 3 --levels 40 > gpurun_out/phase_raftcfg_l40.txt 2>&1 || { tail -5 gpurun_out/phase_raftcfg_l40.txt; exit 1; }
+  cat gpurun_out/phase_raftcfg_l40.txt
+fi
 echo "== done ($(date +%T))"
