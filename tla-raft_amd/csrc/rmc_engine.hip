@@ -1708,7 +1708,7 @@ struct rmc_ctx {
                 Q.gid_next_base = gid_nxt; Q.gid_parent_base = gid_cur;
                 Q.Lmask = Lcap - 1;
                 Q.epoch = s.epoch;
-                Q.split = split ? 1 : 0;
+                Q.split = split ? (split_insert ? 3 : 1) : 0;
                 return Q;
             };
             // expand + fingerprint + seen-set probe + staging, one evaluation per parent
@@ -1726,6 +1726,7 @@ struct rmc_ctx {
                 grow_seen(s, s.T_count + Wub);
             }
             trace_fence(s);
+            if (split && split_insert) timed(PH_OTHER, [&] { ks.insert(params(), np_, stream); });
             timed(PH_MAT, [&] { ks.commit(params(), stream); });  // + chunk summary
             HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
@@ -1787,6 +1788,8 @@ struct rmc_ctx {
     // parents per host-driven chunk from which the seen-set probe and election run as their own
     // pass (k_probe; 0 = always fused into the expansion)
     const uint64_t split_min = (uint64_t)env_int("RMC_SPLIT_MIN", 1 << 16, 0, 1 << 30);
+    // ... and their winners go into the seen set in a pass of their own too (k_insert_winners)
+    const bool split_insert = env_int("RMC_SPLIT_INSERT", 1, 0, 1) != 0;
     const int dl_group = env_int("RMC_DL_GROUP", 2, 1, 64);
     const int dl_ahead = env_int("RMC_DL_AHEAD", 2, 1, 64);
     const int dl_query_us = env_int("RMC_DL_QUERY_US", 2000, 0, 1 << 30);

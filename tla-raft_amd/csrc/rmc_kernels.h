@@ -116,7 +116,8 @@ struct KParams {
     uint4 *xside;
     // split probe (host-driven chunks of many parents): expand writes each successor's fingerprint and
     // its extra record words (lslot = e) and k_probe gives every successor a lane of its own for the
-    // seen-set probe and the election
+    // seen-set probe and the election (bit 0); bit 1: k_insert_winners puts the winners into the seen
+    // set, not the commit
     int split;
     // fused single-shard level: expand (+hash, +seen-set probe, +election, +staging) -> wincount
     // -> commit.  Successor slot q = (p - p_begin) * maxsucc + rank is sparse and increases in
@@ -155,6 +156,7 @@ struct KernelSet {
     void (*single)(const KParams &, hipStream_t);           // all successors of front[0] -> next, fp, out_keys
     void (*fused)(const KParams &, hipStream_t);            // expand + hash + probe + election + staging
     void (*probe)(const KParams &, uint64_t np, hipStream_t);     // split probe: seen set + election per successor
+    void (*insert)(const KParams &, uint64_t np, hipStream_t);    // split chunk: winners into the seen set
     void (*wincount)(const KParams &, uint64_t np, hipStream_t);  // winners per parent + their scan, successors generated
     void (*commit)(const KParams &, hipStream_t);           // winners -> next level, seen set, trace, invariants;
                                                             // chunk summary (and the device loop's next level)

@@ -30,22 +30,25 @@
 // phase profile (tools/phase_prof.py): a build with -DRMC_PHASE_PROF adds up, per phase of
 // k_expand, the shader clock its waves spend there (lane 0 of each wave, flushed once per wave)
 #ifdef RMC_PHASE_PROF
-__device__ unsigned long long g_phase[8];
+// (slots 0-7 k_expand, 8-15 k_commit: PHASE_BASE)
+__device__ unsigned long long g_phase[16];
 #define PHASE_DECL unsigned long long _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; long long _tp = clock64();
 #define PHASE(k) do { const long long _t = clock64(); _acc[k] += (unsigned long long)(_t - _tp); _tp = _t; } while (0)
-#define PHASE_FLUSH do { if (threadIdx.x == 0) for (int _k = 0; _k < 8; _k++) atomicAdd(&g_phase[_k], _acc[_k]); } while (0)
+#define PHASE_FLUSH_AT(b) do { if (threadIdx.x == 0) for (int _k = 0; _k < 8; _k++) atomicAdd(&g_phase[(b) + _k], _acc[_k]); } while (0)
+#define PHASE_FLUSH PHASE_FLUSH_AT(0)
 extern "C" int rmc_debug_phases(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[16] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z)) != hipSuccess) return -1;
     }
-    return 8;
+    return 16;
 }
 #else
 #define PHASE_DECL
 #define PHASE(k) do {} while (0)
 #define PHASE_FLUSH do {} while (0)
+#define PHASE_FLUSH_AT(b) do {} while (0)
 #endif
 
 #ifndef RMC_N3_WAVES  // n = 3 expansion (and commit): waves per SIMD the register budget is cut for
@@ -1790,8 +1793,11 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
 // 64 independent probe chains in flight instead of the ~5 of one parent.  A wave takes 64
 // consecutive parents: their successor counts are scanned across the wave and successor i of the
 // group goes to lane i % 64 of round i / 64 (its parent found by a binary search over the scan).
-template <int MX>
-__global__ __launch_bounds__(256) void k_probe(KParams P) {
+// Successor slot q of every successor of the chunk, a lane each: a wave takes 64 consecutive
+// parents, their successor counts are scanned across the wave and successor i of the group goes to
+// lane i % 64 of round i / 64 (its parent found by a binary search over the scan).
+template <int MX, class F>
+__device__ __forceinline__ void each_successor(const KParams &P, F &&f) {
     const int lane = threadIdx.x & 63;
     const uint64_t np = P.p_end - P.p_begin;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -1811,16 +1817,36 @@ __global__ __launch_bounds__(256) void k_probe(KParams P) {
                 j = v <= i ? j + st : j;
             }
             const uint32_t exj = (uint32_t)__shfl(ex, j, 64);
-            if (i >= tot) continue;
-            const uint64_t q = (g0 + (uint64_t)j) * (uint64_t)MX + (i - exj);
-            const ulonglong2 f = P.fp[q];
-            const uint32_t e = P.lslot[q];
-            const uint64_t g = l_index(f, P.Lmask);
-            const unsigned long long v0 = __hip_atomic_load(&P.LXY[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            P.lslot[q] = seen_contains(P.seen, f) ? LS_SEEN
-                                                  : elect_slot<MX>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g, v0);
+            if (i < tot) f((g0 + (uint64_t)j) * (uint64_t)MX + (i - exj));
         }
     }
+}
+
+// Split probe of a host-driven chunk: the expansion (P.split) wrote every successor's fingerprint
+// fp[q] and its extra record words e in lslot[q]; here each successor gets a lane of its own for the
+// seen-set probe and the election (elect_slot, the same protocol as the fused pass), so a wave keeps
+// 64 independent probe chains in flight instead of the ~5 of one parent.
+template <int MX>
+__global__ __launch_bounds__(256) void k_probe(KParams P) {
+    each_successor<MX>(P, [&](uint64_t q) {
+        const ulonglong2 f = P.fp[q];
+        const uint32_t e = P.lslot[q];
+        const uint64_t g = l_index(f, P.Lmask);
+        const unsigned long long v0 = __hip_atomic_load(&P.LXY[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        P.lslot[q] = seen_contains(P.seen, f) ? LS_SEEN
+                                              : elect_slot<MX>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g, v0);
+    });
+}
+
+// Split chunk, once the election is over: every winner's fingerprint into the seen set, a lane per
+// successor (the commit then writes records only: its insert was a dependent atomic round trip per
+// parent with winners)
+template <int MX>
+__global__ __launch_bounds__(256) void k_insert_winners(KParams P) {
+    each_successor<MX>(P, [&](uint64_t q) {
+        const uint32_t g = P.lslot[q];
+        if (g < LS_ELECT && elect_q(P.L[g]) == (uint32_t)q) seen_insert(P.seen, P.fp[q]);
+    });
 }
 
 // fingerprints of whole states (Init, test hooks): one wave per state
@@ -2124,6 +2150,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
     Hdr nh{};
     if (P.p_begin + blockIdx.x < P.p_end) nh = header(P.p_begin + blockIdx.x);
 #endif
+    PHASE_DECL
     for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
         const uint64_t pl = p - P.p_begin;
 #if RMC_COMMIT_PREFETCH
@@ -2134,6 +2161,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
 #endif
         const uint32_t g0 = h.g0;
         const uint32_t wc = rdlane(h.hw, 2);
+        PHASE(0);
         if (!wc) continue;
         const uint64_t foffp = ((uint64_t)rdlane(h.hw, 1) << 32) | rdlane(h.hw, 0);
         const uint32_t bo = rdlane(h.hw, 3), wp = rdlane(h.hw, 4), t = rdlane(h.hw, 5);
@@ -2177,6 +2205,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
             const uint32_t b = MR > 1 ? __shfl(rw1, (int)(wi & 63u), 64) : 0u;
             id[r] = k < nm ? (((wi < 64u ? a : b) >> ((k & 1u) * 16u)) & 0xFFFFu) : 0xFFFFu;
         }
+        PHASE(1);
         const uint32_t w0 = bo + wp;
         const uint64_t wd0 = P.next_wbase + bow + wpw;
         uint32_t done = 0;
@@ -2192,6 +2221,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
                 win = P.route ? g == LS_WIN : (g < LS_ELECT && elect_q(r0 == 0 ? L0 : P.L[g]) == (uint32_t)q);
             }
             const uint64_t m = __ballot(win);
+            PHASE(2);
             if (!m) continue;
             uint32_t pk[S::CCW];
             uint4 sa = make_uint4(0u, 0u, 0u, 0u), sb = sa, sc = sa;
@@ -2231,7 +2261,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
                     fi = r0 == 0 ? xf : P.fp[q];
                     hi = seen_insert_begin(P.seen, fi, &prev);  // resolved after the record is out
 #else
-                    seen_insert(P.seen, P.fp[q]);
+                    if (!(P.split & 2)) seen_insert(P.seen, P.fp[q]);  // (split chunk: k_insert_winners)
 #endif
                     P.par[gid - P.trace_base] = P.gid_parent_base + p;
                     P.pslot[gid - P.trace_base] = (uint16_t)key;
@@ -2244,6 +2274,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
                     atomicMin(&P.err[iv == 0 ? ERR_INV : ERR_EVAL], ek);
                 }
             }
+            PHASE(4);
             uint32_t wtot;
             const uint32_t wpre = wave_excl_scan(size, lane, &wtot);
             if (win) {
@@ -2271,8 +2302,10 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
 #endif
             done += (uint32_t)__popcll(m);
             done_w += wtot;
+            PHASE(5);
         }
     }
+    PHASE_FLUSH_AT(8);
     // the last block to leave finishes the level (finish_level)
     const uint64_t np = P.p_end - P.p_begin;
     const uint32_t nb = np < gridDim.x ? (np ? (uint32_t)np : 1u) : gridDim.x;
@@ -2300,6 +2333,12 @@ struct Launch {
         hipLaunchKernelGGL((k_probe<MX>), dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u), dim3(256),
                            0, s, P);
     }
+    static void insert(const KParams &P, uint64_t np, hipStream_t s) {
+        constexpr int MX = Spec<N, V, MR>::MAXS + (BFV ? Spec<N, V, MR>::MCAP : 0);
+        const uint64_t blocks = (np + 255) / 256;
+        hipLaunchKernelGGL((k_insert_winners<MX>), dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u),
+                           dim3(256), 0, s, P);
+    }
     static void wincount(const KParams &P, uint64_t np, hipStream_t s) {
         const uint64_t tiles = (np + WTILE - 1) / WTILE;
         hipLaunchKernelGGL((k_wincount<N, V, MR>), dim3(tiles ? (unsigned)tiles : 1u), dim3(1024), 0, s, P);
@@ -2325,6 +2364,7 @@ static void fill(KernelSet *ks) {
     ks->single = &Launch<N, V, MR, BFV>::single;
     ks->fused = &Launch<N, V, MR, BFV>::fused;
     ks->probe = &Launch<N, V, MR, BFV>::probe;
+    ks->insert = &Launch<N, V, MR, BFV>::insert;
     ks->wincount = &Launch<N, V, MR>::wincount;
     ks->commit = &Launch<N, V, MR, BFV>::commit;
     ks->fp_states = &Launch<N, V, MR>::fps;

@@ -22,7 +22,11 @@ sys.path.insert(0, os.path.join(ROOT, "tla-raft_amd"))
 import raftmc  # noqa: E402
 
 NAMES = ["load parent", "evaluate actions", "ranks + error keys", "staging", "hash inputs",
-         "symmetry min", "seen-set probe + election", "-"]
+         "symmetry min", "seen-set probe + election", "-",
+         # k_commit (slots 8-15)
+         "commit: header wait (+ parents w/o winners)", "commit: record + election words + staged rows",
+         "commit: winner test", "-", "commit: rebuild, encode, seen insert, trace, invariants",
+         "commit: scan + record writes", "-", "-"]
 
 ap = argparse.ArgumentParser()
 ap.add_argument("n", type=int)
@@ -37,7 +41,7 @@ mc = raftmc.ModelChecker(cfg)
 lib = raftmc.load_library()
 if not hasattr(lib, "rmc_debug_phases"):
     sys.exit("this librmc.so was not built with -DRMC_PHASE_PROF")
-buf = (ctypes.c_ulonglong * 8)()
+buf = (ctypes.c_ulonglong * 16)()
 lib.rmc_debug_phases(buf, 1)
 ls = mc.init()
 t = time.time()
@@ -47,9 +51,11 @@ while ls.status == "ok" and lv < a.levels:
     lv += 1
 el = time.time() - t
 lib.rmc_debug_phases(buf, 0)
-tot = sum(buf) or 1
 res = mc.result()
 print(f"config n{a.n}_v{a.V}_e{a.E}_r{a.R}: {lv} levels, {res.distinct} distinct, {el:.2f} s")
-for i, v in enumerate(buf):
-    if v:
-        print(f"  {i} {NAMES[i]:32s} {100.0 * v / tot:6.2f} %  ({v / 1e9:.2f} G wave-clocks)")
+for lo, what in ((0, "k_expand"), (8, "k_commit")):
+    tot = sum(buf[lo:lo + 8]) or 1
+    print(f" {what}: share of its waves' time")
+    for i in range(lo, lo + 8):
+        if buf[i]:
+            print(f"  {i} {NAMES[i]:46s} {100.0 * buf[i] / tot:6.2f} %  ({buf[i] / 1e9:.2f} G wave-clocks)")
