@@ -278,10 +278,13 @@ constexpr uint64_t PAIR_K0 = 0x9e3779b97f4a7c15ULL, PAIR_K1 = 0xc2b2ae3d27d4eb4f
 // from the message's info word: the host's table (Universe::gmsg) and the expansion kernel's
 // added messages use this one definition
 struct MsgHash { uint64_t x, y; };
+// One mix64 per family: body * K + seed is a bijection of the 32-bit body and mix64 a bijection, so
+// each family is a well-mixed injective image of the body (an outer mix64 over a seeded inner one
+// added nothing but 2 of the 4 multiply-heavy mixes the expansion pays per added message).
 RMC_HD MsgHash msg_hash(uint32_t info) {
     const uint64_t body = (uint64_t)info & ~0xFCull;
-    return {mix64(SEED_MSG ^ mix64(body * 0x9e3779b97f4a7c15ULL + 1)),
-            mix64((SEED_MSG + 0x632be59bd9b4e019ULL) ^ mix64(body * 0xc2b2ae3d27d4eb4fULL + 7))};
+    return {mix64(body * 0x9e3779b97f4a7c15ULL + SEED_MSG),
+            mix64(body * 0xc2b2ae3d27d4eb4fULL + (SEED_MSG + 0x632be59bd9b4e019ULL))};
 }
 
 // slot key (16 bit): server<<11 | position<<7 | witness -- increasing in TLC order; the position
