@@ -261,6 +261,20 @@ def test_bfs_matches_golden_levels(name):
     mc.close()
 
 
+@pytest.mark.parametrize("name", sorted(LEVELS))
+def test_split_probe_chunks_match_golden_levels(name, monkeypatch):
+    """Every chunk split (RMC_SPLIT_MIN=1, host-driven levels): k_probe elects, k_insert_winners inserts
+    and leaves its verdicts for the commit -- levels, counters at an error and traces as the golden run."""
+    monkeypatch.setenv("RMC_SPLIT_MIN", "1")
+    g = LEVELS[name]
+    mc, res = run_cfg(g, device_levels=1)
+    check_levels(g, res)
+    if name in TRACES:
+        assert [(list(k) if k else None, st) for k, st in mc.trace()] == \
+               [(e["key"], e["state"]) for e in TRACES[name]["steps"]]
+    mc.close()
+
+
 @pytest.mark.parametrize("name", sorted(LEVELS_BIG))
 def test_bfs_matches_golden_levels_at_scale(name):
     """bench.py's at-scale workload (10^7 states) against the C oracle's full BFS, level by level."""

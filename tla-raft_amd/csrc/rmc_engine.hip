@@ -1708,7 +1708,7 @@ struct rmc_ctx {
                 Q.gid_next_base = gid_nxt; Q.gid_parent_base = gid_cur;
                 Q.Lmask = Lcap - 1;
                 Q.epoch = s.epoch;
-                Q.split = split ? (split_insert ? 3 : 1) : 0;
+                Q.split = split ? (split_insert ? split_flags : 1) : 0;
                 return Q;
             };
             // expand + fingerprint + seen-set probe + staging, one evaluation per parent
@@ -1790,6 +1790,9 @@ struct rmc_ctx {
     const uint64_t split_min = (uint64_t)env_int("RMC_SPLIT_MIN", 1 << 16, 0, 1 << 30);
     // ... and their winners go into the seen set in a pass of their own too (k_insert_winners)
     const bool split_insert = env_int("RMC_SPLIT_INSERT", 1, 0, 1) != 0;
+    // KParams.split of such chunks (measurement knob): 7 = verdicts in lslot for the commit, 3 = the
+    // commit reads the election words itself
+    const int split_flags = env_int("RMC_SPLIT_FLAGS", 7, 3, 7) == 3 ? 3 : 7;
     const int dl_group = env_int("RMC_DL_GROUP", 2, 1, 64);
     const int dl_ahead = env_int("RMC_DL_AHEAD", 2, 1, 64);
     const int dl_query_us = env_int("RMC_DL_QUERY_US", 2000, 0, 1 << 30);
@@ -2019,8 +2022,9 @@ struct rmc_ctx {
             HIPCHK(hipMemcpy(ls.data(), s.lslot + pl * ks.maxsucc, upto * 4, hipMemcpyDeviceToHost));
             uint64_t w = 0;
             for (uint32_t r = 0; r < upto; r++)
-                w += route ? ls[r] == LS_WIN
-                           : (ls[r] < LS_ELECT && ((uint32_t)d2h(s.L + ls[r]) >> 2) == (uint32_t)(pl * ks.maxsucc + r));
+                // (LS_WIN: an owner's verdict, or a split chunk's after k_insert_winners)
+                w += ls[r] == LS_WIN ||
+                     (!route && ls[r] < LS_ELECT && ((uint32_t)d2h(s.L + ls[r]) >> 2) == (uint32_t)(pl * ks.maxsucc + r));
             return w;
         };
         // successors of p, in order, to find the sub-action batch boundaries

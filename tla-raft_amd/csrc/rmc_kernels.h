@@ -117,7 +117,7 @@ struct KParams {
     // split probe (host-driven chunks of many parents): expand writes each successor's fingerprint and
     // its extra record words (lslot = e) and k_probe gives every successor a lane of its own for the
     // seen-set probe and the election (bit 0); bit 1: k_insert_winners puts the winners into the seen
-    // set, not the commit
+    // set, not the commit; bit 2: ... and leaves its verdicts in lslot (LS_WIN / LS_SEEN) for the commit
     int split;
     // fused single-shard level: expand (+hash, +seen-set probe, +election, +staging) -> wincount
     // -> commit.  Successor slot q = (p - p_begin) * maxsucc + rank is sparse and increases in

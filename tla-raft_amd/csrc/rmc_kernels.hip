@@ -1839,13 +1839,17 @@ __global__ __launch_bounds__(256) void k_probe(KParams P) {
 }
 
 // Split chunk, once the election is over: every winner's fingerprint into the seen set, a lane per
-// successor (the commit then writes records only: its insert was a dependent atomic round trip per
-// parent with winners)
+// successor, and every candidate's verdict in its slot (LS_WIN / LS_SEEN, as the owners' verdicts of a
+// sharded round) -- the commit then reads neither the election words nor inserts: both were
+// dependent round trips per parent with winners
 template <int MX>
 __global__ __launch_bounds__(256) void k_insert_winners(KParams P) {
     each_successor<MX>(P, [&](uint64_t q) {
         const uint32_t g = P.lslot[q];
-        if (g < LS_ELECT && elect_q(P.L[g]) == (uint32_t)q) seen_insert(P.seen, P.fp[q]);
+        if (g >= LS_ELECT) return;
+        const bool w = elect_q(P.L[g]) == (uint32_t)q;
+        if (w) seen_insert(P.seen, P.fp[q]);
+        P.lslot[q] = w ? LS_WIN : LS_SEEN;  // the verdict: the commit needs no election word
     });
 }
 
@@ -2173,7 +2177,9 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
         const uint32_t rw1 =
             (MR > 1 && 64 + lane < S::RECW_MAX) ? ring_word(P.front, start, 64u + (uint32_t)lane, P.rcap) : 0u;
         // (slots past the parent's t successors hold a stale lslot from an earlier chunk: never an index)
-        const unsigned long long L0 = (!P.route && (uint32_t)lane < t && g0 < LS_ELECT) ? P.L[g0] : 0ull;
+        // (verdicts in lslot -- sharded round, or a split chunk after k_insert_winners -- need no election word)
+        const bool verdict = P.route || (P.split & 4);
+        const unsigned long long L0 = (!verdict && (uint32_t)lane < t && g0 < LS_ELECT) ? P.L[g0] : 0ull;
         // and the staged rows of the first 64 slots that may win (new fingerprints; in a sharded
         // round the owner's verdict is already known): a speculative read instead of a third round
         // trip once the election words are in
@@ -2181,7 +2187,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
 #if RMC_COMMIT_EARLY
         ulonglong2 xf = make_ulonglong2(0ull, 0ull);  // and their fingerprints (the seen-set insert)
 #endif
-        if ((uint32_t)lane < t && (P.route ? g0 == LS_WIN : g0 < LS_ELECT)) {
+        if ((uint32_t)lane < t && (verdict ? g0 == LS_WIN : g0 < LS_ELECT)) {
             const uint4 *src = P.score + (pl * (uint64_t)MX + (uint32_t)lane) * (uint64_t)S::SW4;
             xa = src[0];
             xb = src[1];
@@ -2218,7 +2224,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
             bool win = false;
             if (r < t) {
                 const uint32_t g = r0 == 0 ? g0 : P.lslot[q];
-                win = P.route ? g == LS_WIN : (g < LS_ELECT && elect_q(r0 == 0 ? L0 : P.L[g]) == (uint32_t)q);
+                win = verdict ? g == LS_WIN : (g < LS_ELECT && elect_q(r0 == 0 ? L0 : P.L[g]) == (uint32_t)q);
             }
             const uint64_t m = __ballot(win);
             PHASE(2);
