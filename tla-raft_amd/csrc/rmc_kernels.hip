@@ -1849,7 +1849,7 @@ __global__ __launch_bounds__(256) void k_insert_winners(KParams P) {
         if (g >= LS_ELECT) return;
         const bool w = elect_q(P.L[g]) == (uint32_t)q;
         if (w) seen_insert(P.seen, P.fp[q]);
-        P.lslot[q] = w ? LS_WIN : LS_SEEN;  // the verdict: the commit needs no election word
+        if (P.split & 4) P.lslot[q] = w ? LS_WIN : LS_SEEN;  // the verdict: the commit needs no election word
     });
 }
 
@@ -2151,13 +2151,21 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
         return h;
     };
 #if RMC_COMMIT_PREFETCH
-    Hdr nh{};
+    // (RMC_COMMIT_PREFETCH 2: two headers ahead, so a run of parents without winners -- each only a
+    // header wait -- pays half a round trip per parent)
+    Hdr nh{}, nnh{};
     if (P.p_begin + blockIdx.x < P.p_end) nh = header(P.p_begin + blockIdx.x);
+    if (RMC_COMMIT_PREFETCH > 1 && P.p_begin + blockIdx.x + gridDim.x < P.p_end)
+        nnh = header(P.p_begin + blockIdx.x + gridDim.x);
 #endif
     PHASE_DECL
     for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
         const uint64_t pl = p - P.p_begin;
-#if RMC_COMMIT_PREFETCH
+#if RMC_COMMIT_PREFETCH > 1
+        const Hdr h = nh;
+        nh = nnh;
+        if (p + 2ull * gridDim.x < P.p_end) nnh = header(p + 2ull * gridDim.x);
+#elif RMC_COMMIT_PREFETCH
         const Hdr h = nh;
         if (p + gridDim.x < P.p_end) nh = header(p + gridDim.x);
 #else
