@@ -74,6 +74,9 @@ extern "C" int rmc_debug_phases(unsigned long long *out, int reset) {
 #ifndef RMC_MSG_BITMAP  // k_expand: m \in msgs by an LDS bitmap of the parent's ids (0: binary search)
 #define RMC_MSG_BITMAP 1
 #endif
+#ifndef RMC_HASH_COMPACT  // k_expand (n <= 3): successor hash rows in one pass over compacted successors
+#define RMC_HASH_COMPACT 1
+#endif
 #ifndef RMC_WIDE_WAVES
 #define RMC_WIDE_WAVES 2
 #endif
@@ -1120,13 +1123,13 @@ __device__ __forceinline__ void load_parent(const KParams &P, uint64_t start, in
 
 // hash row of the acting server: parent sums + the messages this successor adds
 template <int N, int V, int MR>
-__device__ __forceinline__ void succ_row(const Succ<N, V, MR> &o, const uint64_t *M0, const uint64_t *M1,
-                                         const uint32_t *ainf, uint64_t *row0, uint64_t *row1) {
+__device__ __forceinline__ void succ_row_at(uint32_t s, uint32_t nadd, const uint64_t *M0, const uint64_t *M1,
+                                            const uint32_t *ainf, uint64_t *row0, uint64_t *row1) {
 #pragma unroll
-    for (int j = 0; j < N; j++) { row0[j] = M0[o.s * N + j]; row1[j] = M1[o.s * N + j]; }
+    for (int j = 0; j < N; j++) { row0[j] = M0[s * N + j]; row1[j] = M1[s * N + j]; }
 #pragma unroll
     for (int a = 0; a < Spec<N, V, MR>::NADD; a++) {
-        if ((uint32_t)a >= o.nadd) break;
+        if ((uint32_t)a >= nadd) break;
         // the added message's hash from its info word, built where it was generated: no
         // dependent table loads after the id lookup
         const uint32_t inf = ainf[a];
@@ -1138,6 +1141,11 @@ __device__ __forceinline__ void succ_row(const Succ<N, V, MR> &o, const uint64_t
             row1[j] += ((uint32_t)j == dst) ? g.y : 0ull;
         }
     }
+}
+template <int N, int V, int MR>
+__device__ __forceinline__ void succ_row(const Succ<N, V, MR> &o, const uint64_t *M0, const uint64_t *M1,
+                                         const uint32_t *ainf, uint64_t *row0, uint64_t *row1) {
+    succ_row_at<N, V, MR>(o.s, o.nadd, M0, M1, ainf, row0, row1);
 }
 
 // Merge the parent's sorted ids (per lane: id[r] = id r*64+lane, 0xFFFF past nm) with a
@@ -1397,6 +1405,12 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
     __shared__ uint8_t pimg[NPM * N];                   // permutation images
     __shared__ uint64_t sU[MAXS], sX[2][MAXS * N];      // compacted successor rows
     __shared__ uint8_t sS[MAXS], sNa[MAXS];             // acting server, |added ids| per successor
+    // CPT (n <= 3): the successors' hash rows are built in one pass over the compacted successors (a
+    // lane each) instead of once per candidate kind -- per successor its rows and votedFor (sCp) and
+    // where its added messages' info words are (sCa)
+    constexpr bool CPT = RMC_HASH_COMPACT && !SIG && N <= 3;
+    __shared__ uint32_t sCp[CPT ? MAXS : 1];
+    __shared__ uint16_t sCa[CPT ? MAXS : 1];
     // signature pre-sort: parent rows / signatures, per successor the tie ranks, the first task
     // of its coset (exclusive scan of coset sizes) and its running minimum; per task its successor
     __shared__ uint64_t pU[SIG ? N : 1], pX[2][SIG ? N * N : 1], psig[SIG ? N : 1];
@@ -1589,8 +1603,36 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
                 __syncthreads();
             }
             // (b) every enabled successor writes its acting row to LDS slot rank
+            if constexpr (CPT) {
 #pragma unroll
-            for (int r = 0; r < NC; r++) {
+                for (int r = 0; r < NC; r++) {
+                    if (cand[r].key == KEY_NONE) continue;
+                    const Succ<N, V, MR> &o = cand[r];
+                    const uint32_t sl = rank[r];
+                    const uint32_t vfs = nib(o.c[Lo::W_VF], o.s);
+                    sU[sl] = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI], o.c[Lo::W_LL],
+                                         o.lw, o.mirow, o.nirow, o.s);
+                    sS[sl] = (uint8_t)o.s;
+                    sNa[sl] = (uint8_t)o.nadd;
+                    sCp[sl] = o.mirow | (o.nirow << 12) | (vfs << 24);  // rows of N <= 3 nibbles
+                    sCa[sl] = (uint16_t)(((r <= MR ? r : 0) * 64 + lane) * S::NADD);
+                }
+                __syncthreads();
+                for (uint32_t l = (uint32_t)lane; l < total; l += 64) {
+                    const uint32_t sv = sS[l], cp = sCp[l];
+                    const uint32_t mirow = cp & 0xFFFu, nirow = (cp >> 12) & 0xFFFu, vfs = cp >> 24;
+                    uint64_t row0[N], row1[N];
+                    succ_row_at<N, V, MR>(sv, sNa[l], M0, M1, &sAinf[sCa[l]], row0, row1);
+#pragma unroll
+                    for (int j = 0; j < N; j++) {
+                        const uint64_t sm = pair_small(mirow, nirow, vfs, j);
+                        sX[0][l * N + j] = row0[j] ^ (sm * PAIR_K0);
+                        sX[1][l * N + j] = row1[j] ^ (sm * PAIR_K1);
+                    }
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < NC && !CPT; r++) {
                 if (cand[r].key == KEY_NONE) continue;
                 const Succ<N, V, MR> &o = cand[r];
                 const uint32_t sl = rank[r];

@@ -10,13 +10,14 @@ case "$1" in
   w1) FLAGS="-DRMC_WIDE_WAVES=1" ;;
   bm0) FLAGS="-DRMC_MSG_BITMAP=0" ;;  # k_expand: m \in msgs by binary search over the sorted ids
   pm0) FLAGS="-DRMC_EXPAND_PREFETCH_MSGS=0" ;;  # k_expand without the next parent's message-table prefetch
+  hc0) FLAGS="-DRMC_HASH_COMPACT=0" ;;  # k_expand: successor hash rows once per candidate kind
   cp2) FLAGS="-DRMC_COMMIT_PREFETCH=2" ;;  # k_commit: two headers ahead
   cp0) FLAGS="-DRMC_COMMIT_PREFETCH=0" ;;  # k_commit without the next parent's header prefetch
   ce1) FLAGS="-DRMC_COMMIT_EARLY=1" ;;  # k_commit: early seen-set insert (measured slower, off by default)
   # n = 3 occupancy: expansion waves / SIMD, commit waves / SIMD, grid blocks / CU (e.g. n3w6c4g32)
   n3w*) X=${1#n3w}; W=${X%%c*}; X=${X#*c}; C=${X%%g*}; G=${X#*g}
         FLAGS="-DRMC_N3_WAVES=$W -DRMC_N3_COMMIT_WAVES=$C -DRMC_GRID_PER_CU=$G" ;;
-  *) echo "usage: $0 prof|w1|ce1|cp0|cp2|pm0|bm0|n3w<W>c<C>g<G>" >&2; exit 2 ;;
+  *) echo "usage: $0 prof|w1|ce1|cp0|cp2|pm0|bm0|hc0|n3w<W>c<C>g<G>" >&2; exit 2 ;;
 esac
 OUT=build_$1
 mkdir -p "$OUT"
