@@ -69,6 +69,9 @@ def alg_bytes(phase, F, G, N, S, CCWB, slot_bytes=16, SWB=32, split=False):
     if phase == "probe":         # k_probe: per parent its count; per successor fp + extra words in, verdict out,
         # one seen-set probe; per new fingerprint at least one election (16-B slot, 8-B word, count)
         return F * 4 + G * (16 + 4 + 4) + G * slot_bytes + N * (16 + 8 + 4)
+    if phase == "insert":        # k_insert_winners: per parent its count; per successor its slot word; per new
+        # state its election word, fingerprint, seen-set insert and verdict
+        return F * 4 + G * 4 + N * (8 + 16 + slot_bytes + 4)
     if phase == "dedup":         # k_wincount: per parent successor count, packed winner count (read + re-arm),
         # |msgs|; out winner count and the two scans
         return F * (4 + 4 + 4 + 4 + 4 + 4 + 4)

@@ -1726,7 +1726,8 @@ struct rmc_ctx {
                 grow_seen(s, s.T_count + Wub);
             }
             trace_fence(s);
-            if (split && split_insert) timed(PH_OTHER, [&] { ks.insert(params(), np_, stream); });
+            // (timed with the winner count: PH_OTHER stays the probe pass alone)
+            if (split && split_insert) timed(PH_DEDUP, [&] { ks.insert(params(), np_, stream); });
             timed(PH_MAT, [&] { ks.commit(params(), stream); });  // + chunk summary
             HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));

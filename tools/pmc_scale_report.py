@@ -8,7 +8,8 @@ HBM traffic.  explore.py steps level by level on the host-driven path: a level o
 ceil(F / chunk_parents) chunks, one dispatch of each kernel per chunk (k_probe only for chunks of at
 least --split-min parents), in dispatch order.  The explore log of the same pass gives each level's
 parents F, successors G, new states N, average record bytes S and the HIP-event time of each kernel
-phase.  Per level (dispatches of a level summed) this records:
+phase; each dispatch's duration is its own (start / end timestamps of the FETCH_SIZE pass's records).
+Per level (dispatches of a level summed) this records:
 
   alg_bytes    bench.py alg_bytes() -- the algorithmic bytes of the kernel
   hbm_bytes    2 * 1024 * FETCH_SIZE + 1024 * WRITE_SIZE (MI355X_MICROARCH.md rocprofv3 section; the
@@ -16,6 +17,7 @@ phase.  Per level (dispatches of a level summed) this records:
                8-16 B random accesses that dominate here -- both readings are reported)
   ratio        hbm_bytes / alg_bytes (traffic well above 1 = whole lines moved for a few useful bytes)
   valu_frac    SQ_INSTS_VALU / duration against 256 CUs x 4 SIMDs x 2.4 GHz / 2 wave64 issues per s
+               (the SQ pass's own dispatch durations would differ by the pass-to-pass spread)
   alg_GBps     alg_bytes / duration, hbm_GBps = hbm_bytes / duration (peak 8 TB/s)
 
 usage: pmc_scale_report.py gpurun_out/pmcs out.json [--min-parents 500000] [--n 3 --V 2]"""
@@ -34,7 +36,7 @@ from bench import HBM_PEAK_GBS, VALU_PEAK, alg_bytes  # noqa: E402
 LEVEL = re.compile(r"^L\s*(\d+) F=\s*(\d+) G=\s*(\d+) N=\s*(\d+) tot=\s*\d+\s+[\d.]+ms \[([^\]]*)\].*rec=([\d.]+)B")
 # name -> (kernel name fragment, explore phase column of its HIP-event time, alg_bytes phase)
 KERNELS = {"expand": ("k_expand", 1, "expand_hash"), "probe": ("k_probe", 5, "probe"),
-           "commit": ("k_commit", 3, "materialize")}
+           "insert": ("k_insert_winners", 5, "insert"), "commit": ("k_commit", 3, "materialize")}
 
 
 def levels_of(log):
@@ -49,10 +51,14 @@ def levels_of(log):
 
 
 def per_dispatch(csvf, kname):
+    """Per dispatch of the kernel, in dispatch order: its counters and its duration in ms (the
+    collection record's start / end timestamps)."""
     vals = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(csvf)):
         if kname in r["Kernel_Name"]:
-            vals[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+            d = vals[int(r["Dispatch_Id"])]
+            d[r["Counter_Name"]] += float(r["Counter_Value"])
+            d["_ms"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
     return [vals[k] for k in sorted(vals)]
 
 
@@ -84,7 +90,7 @@ def main():
         per = []
         for L in lv_f:
             nch = max(1, -(-L["F"] // chunk))
-            if key == "probe":
+            if key in ("probe", "insert"):
                 nch = sum(1 for c in range(nch) if min(chunk, L["F"] - c * chunk) >= a.split_min)
             per.append(nch)
         if not (len(fetch) == len(write) == len(sq) == sum(per)):
@@ -94,7 +100,9 @@ def main():
             d0, k = k, k + nch
             if L["F"] < a.min_parents or nch == 0:
                 continue
-            ms = L["ms"][ph]
+            # duration: the dispatches' own timestamps in the FETCH_SIZE pass (the explore log's
+            # HIP-event columns lump k_probe and k_insert_winners together)
+            ms = sum(fetch[i]["_ms"] for i in range(d0, k))
             split = L["F"] >= a.split_min  # (every chunk of such a level is split at Raft.cfg's sizes)
             alg = alg_bytes(phase, L["F"], L["G"], L["N"], L["rec"], 0, 8, swb, split=split)
             rd = 1024 * sum(fetch[i]["FETCH_SIZE"] for i in range(d0, k))
