@@ -59,6 +59,14 @@ extern "C" {
 #define RMC_SPEC_BECOME_FOLLOWER 2  /* Raft.tla with Next's `\/ BecomeFollower(s)` uncommented (Raft.tla:420):
                                        FollowerUpdateTerm / CandidateToFollower / LeaderToFollower
                                        (Raft.tla:190-229) right after UpdateTerm; trace action id 12 */
+/* Test variants (tools/make_seeded_spec.py --split-brain / --commit-past-log) in which TLC's two error
+ * kinds other than an invariant violation are reachable in a BFS, so their precedence and counters
+ * are checked end to end (the shipped specs reach neither): */
+#define RMC_SPEC_SPLIT_BRAIN 3      /* RaftSplitBrain: BecomeLeader's quorum (Raft.tla:164) is 1 -> two
+                                       leaders of one term -> UpdateTerm's Assert (Raft.tla:185) fails */
+#define RMC_SPEC_COMMIT_PAST_LOG 4  /* RaftCommitPastLog: FollowerAcceptEntry's newCommitIndex (Raft.tla:294)
+                                       is Max(commitIndex, leaderCommit) -> Inv's logs[p][index]
+                                       (Raft.tla:499) out of its domain */
 
 /* Model configuration: what Raft.cfg's CONSTANTS (Raft.cfg:1-21), INVARIANT
  * (Raft.cfg:33-34) and TLC's -deadlock flag (myrun.sh:3) bind.  VIEW view

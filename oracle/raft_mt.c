@@ -203,7 +203,7 @@ static int mt_bfs(int n, int V, int E, int R, int threads, uint64_t max_states, 
                   int lcap, uint64_t *distinct, uint64_t *generated, int *depth) {
     if (threads < 1) threads = 1;
     if (threads > 256) threads = 256;
-    ocfg_t c = {n, V, E, R, 0, 0, 1u << I_LHACE, 0, 0, 0, 0};
+    ocfg_t c = {n, V, E, R, 0, 0, 1u << I_LHACE, 0, 0, 0, 0, 0, 0};
     perms_t *P = (perms_t *)malloc(sizeof(perms_t));
     make_perms(n, P);
     uint64_t seen_cap = 1u << 20;

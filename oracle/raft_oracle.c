@@ -70,9 +70,14 @@ typedef struct {
     int order;          /* 0 = TLC -workers 1 order; 1 = reversed; 2 = seeded shuffle (order-sensitivity probe) */
     uint64_t seed;
     int bf;             /* the BecomeFollower variant (tla:420 uncommented) */
+    int sb;             /* RaftSplitBrain (test variant): BecomeLeader's quorum (tla:164) is 1 */
+    int cpl;            /* RaftCommitPastLog (test variant): newCommitIndex (tla:294) = Max(ci, leaderCommit) */
 } ocfg_t;
-/* spec flags of the C API's `seeded` argument: bit 0 RaftSeeded, bit 1 BecomeFollower variant */
-static void set_variant(ocfg_t *c, int flags) { c->seeded = flags & 1; c->bf = (flags >> 1) & 1; }
+/* spec flags of the C API's `seeded` argument: bit 0 RaftSeeded, bit 1 BecomeFollower variant,
+ * bit 2 RaftSplitBrain, bit 3 RaftCommitPastLog */
+static void set_variant(ocfg_t *c, int flags) {
+    c->seeded = flags & 1; c->bf = (flags >> 1) & 1; c->sb = (flags >> 2) & 1; c->cpl = (flags >> 3) & 1;
+}
 
 typedef struct {
     int8_t vf[MAXN], ct[MAXN], role[MAXN], ci[MAXN], ll[MAXN];
@@ -277,7 +282,7 @@ static void gen_action(const ocfg_t *c, const st_t *st, int s, int a, batch_t *b
             msg_t m; k_decode(st->m[w], &m);
             cnt += (m.dst == s && m.term == st->ct[s] && m.type == MT_VRESP);
         }
-        if (!(cnt + 1 >= n / 2 + 1)) return;
+        if (!(cnt + 1 >= (c->sb ? 1 : n / 2 + 1))) return;
         st_t *t = emit(b, 0); copy_state(t, st);
         int L = st->ll[s];
         t->role[s] = R_L;
@@ -327,7 +332,7 @@ static void gen_action(const ocfg_t *c, const st_t *st, int s, int a, batch_t *b
                     /* newLog # SubSeq(logs[s], 1, Len(newLog)): only the entry can differ */
                     if (m.elen && (st->lt[s][nl] != m.et || st->lv[s][nl] != m.ev)) truncated = 1;
                 }
-                int mn = m.lc < nl ? m.lc : nl;
+                int mn = (c->cpl || m.lc < nl) ? m.lc : nl;
                 int nci = st->ci[s] > mn ? st->ci[s] : mn;
                 st_t *t = emit(b, w); copy_state(t, st);
                 add_msg(t, k_aresp(s, m.src, m.term, m.pli + m.elen, 1));
@@ -876,7 +881,7 @@ int orc_trace_state(void *h, int idx, int32_t *out, int cap_ints, uint32_t *key)
 /* successors of an unpacked state in TLC order; returns count, -1 on Assert, -2 on capacity */
 int orc_successors(int n, int V, int E, int R, int seeded, const int32_t *in, int32_t *out, int stride_ints,
                    int cap_states, uint32_t *keys) {
-    ocfg_t c = {n, V, E, R, 0, 0, 1, 0, 0, 0, 0};
+    ocfg_t c = {n, V, E, R, 0, 0, 1, 0, 0, 0, 0, 0, 0};
     set_variant(&c, seeded);
     st_t *st = (st_t *)malloc(sizeof(st_t));
     batch_t b; b.buf = (st_t *)malloc(sizeof(st_t) * BATCH_CAP); b.w = (int32_t *)malloc(sizeof(int32_t) * BATCH_CAP); b.cap = BATCH_CAP;
@@ -903,7 +908,7 @@ out:
 }
 
 int orc_canon_hash(int n, int V, const int32_t *in, uint64_t *out2) {
-    ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0, 0, 0, 0};
+    ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0, 0, 0, 0, 0, 0};
     perms_t *P = (perms_t *)malloc(sizeof(perms_t));
     make_perms(n, P);
     st_t *st = (st_t *)malloc(sizeof(st_t));
@@ -914,7 +919,7 @@ int orc_canon_hash(int n, int V, const int32_t *in, uint64_t *out2) {
 }
 
 int orc_inv(int n, int V, const int32_t *in, int inv_id) {
-    ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0, 0, 0, 0};
+    ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0, 0, 0, 0, 0, 0};
     st_t *st = (st_t *)malloc(sizeof(st_t));
     int r = pack_from(&c, in, st);
     if (r >= 0) r = inv_eval(&c, st, inv_id);

@@ -439,7 +439,7 @@ int orc_prefix_levels(int n, int V, int E, int R, int threads, uint64_t max_stat
                       int *depth) {
     if (threads < 1) threads = 1;
     if (threads > PMAXT) threads = PMAXT;
-    ocfg_t c = {n, V, E, R, 0, 0, 1u << I_LHACE, 0, 0, 0, 0};
+    ocfg_t c = {n, V, E, R, 0, 0, 1u << I_LHACE, 0, 0, 0, 0, 0, 0};
     perms_t *P = (perms_t *)malloc(sizeof(perms_t));
     make_perms(n, P);
     pcodec_t C;
@@ -562,7 +562,7 @@ int orc_prefix_levels(int n, int V, int E, int R, int threads, uint64_t max_stat
 
 /* codec self-check: encode/decode round trip of every state of a small BFS (tests/test_oracle.py) */
 int orc_prefix_codec_check(int n, int V, int E, int R, uint64_t max_states) {
-    ocfg_t c = {n, V, E, R, 0, 0, 1u << I_LHACE, 0, 0, 0, 0};
+    ocfg_t c = {n, V, E, R, 0, 0, 1u << I_LHACE, 0, 0, 0, 0, 0, 0};
     pcodec_t C;
     pc_build(&C, n, V, E);
     st_t *s = (st_t *)calloc(1, sizeof(st_t)), *t = (st_t *)calloc(1, sizeof(st_t));

@@ -182,6 +182,12 @@ class Config:
     seeded: bool = False       # RaftSeeded: Median threshold Cardinality(Servers)
     follower_append_entry: bool = False  # variant: tla:425's `\/ FollowerAppendEntry(s)` uncommented
     become_follower: bool = False  # variant: tla:420's `\/ BecomeFollower(s)` uncommented
+    # test-only variants (tools/make_seeded_spec.py) that make TLC's two error kinds reachable in a BFS:
+    split_brain: bool = False  # RaftSplitBrain: BecomeLeader's quorum (tla:164) is 1 -- two leaders of
+    #                            one term, so UpdateTerm's Assert (tla:185) fails
+    commit_past_log: bool = False  # RaftCommitPastLog: FollowerAcceptEntry's newCommitIndex (tla:294) is
+    #                            Max(commitIndex, leaderCommit) -- commitIndex past the log, so Inv's
+    #                            logs[p][index] (tla:499) is out of domain
     symmetry: bool = True      # SYMMETRY symmServers (cfg:24)
     view: bool = True          # VIEW view (cfg:26)
 
@@ -349,7 +355,7 @@ def become_leader(cfg, st: State, s):
         return
     resps = sum(1 for m in st.msgs
                 if mdst(m) == s and mterm(m) == st.currentTerm[s] and mtype(m) == "VoteResp")
-    if not (resps + 1 >= cfg.majority):
+    if not (resps + 1 >= (1 if cfg.split_brain else cfg.majority)):
         return
     L = len(st.logs[s])
     yield 0, State(
@@ -430,7 +436,8 @@ def follower_accept_entry(cfg, st: State, s, msgs_sorted):
         new_log = log[:f["prevLogIndex"]] + ent
         append_new = len(new_log) > len(log)
         truncated = len(new_log) <= len(log) and new_log != log[:len(new_log)]
-        new_ci = max(st.commitIndex[s], min(f["leaderCommit"], len(new_log)))
+        new_ci = max(st.commitIndex[s], f["leaderCommit"] if cfg.commit_past_log
+                     else min(f["leaderCommit"], len(new_log)))
         updated = new_log if (truncated or append_new) else log
         yield w, State(
             votedFor=st.votedFor, currentTerm=st.currentTerm,

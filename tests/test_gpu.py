@@ -31,6 +31,10 @@ TRACES = load("traces.json")
 LEVELS_BF = load("levels_bf.json")
 SAMPLES_BF = load("successors_bf.json")
 TRACES_BF = load("traces_bf.json")
+# the test variants in which the Assert / the evaluation error are reachable in a BFS
+# (tools/make_seeded_spec.py --split-brain / --commit-past-log; tests/golden/make_golden_errors.py)
+LEVELS_ERR = load("levels_errors.json")
+TRACES_ERR = load("traces_errors.json")
 
 _cache = {}
 
@@ -226,6 +230,8 @@ def test_eval_error_state():
 def spec_of(g):
     if g.get("become_follower"):
         return raftmc.SPEC_BECOME_FOLLOWER
+    if g.get("variant"):
+        return {"split_brain": raftmc.SPEC_SPLIT_BRAIN, "commit_past_log": raftmc.SPEC_COMMIT_PAST_LOG}[g["variant"]]
     return raftmc.SPEC_SEEDED if g["seeded"] else raftmc.SPEC_RAFT
 
 
@@ -770,6 +776,58 @@ def test_become_follower_bfs_matches_golden_levels(name):
         tr = mc.trace()
         assert [(list(k) if k else None, st) for k, st in tr] == [(e["key"], e["state"]) for e in TRACES_BF[name]["steps"]]
     mc.close()
+
+
+def _trace_matches(mc, t):
+    assert [(list(k) if k else None, st) for k, st in mc.trace()] == [(e["key"], e["state"]) for e in t["steps"]]
+
+
+@pytest.mark.parametrize("mode", ["default", "host_levels", "split", "virtual2", "virtual4", "rccl1"])
+@pytest.mark.parametrize("name", sorted(LEVELS_ERR))
+def test_bfs_error_precedence_matches_golden(name, mode, monkeypatch):
+    """The Assert (Raft.tla:185) and Inv's evaluation error (Raft.tla:499) met inside a BFS -- the test
+    variants RaftSplitBrain / RaftCommitPastLog -- stop the run where both oracles stop it: the same
+    verdict, TLC's counters at the error (states generated and distinct, queue left), the levels before
+    it and the counterexample, on the device loop, host-driven levels, split chunks, 2/4 virtual shards
+    and the one-rank RCCL communicator."""
+    g = LEVELS_ERR[name]
+    kw = {}
+    if mode == "host_levels":
+        kw = dict(device_levels=1)
+    elif mode == "split":
+        monkeypatch.setenv("RMC_SPLIT_MIN", "1")
+        kw = dict(device_levels=1)
+    elif mode.startswith("virtual"):
+        kw = dict(virtual_shards=int(mode[-1]), chunk_successors=3000, shard_min_states=1)
+    elif mode == "rccl1":
+        kw = dict(world_size=1, rank=0, comm_unique_id=raftmc.comm_unique_id(), chunk_successors=3000,
+                  shard_min_states=1)
+    mc, res = run_cfg(g, **kw)
+    check_levels(g, res)
+    assert [ls.new_states for ls in res.levels if ls.new_states][:len(g["levels"]) - 1] == g["levels"][:-1]
+    _trace_matches(mc, TRACES_ERR[name])
+    mc.close()
+
+
+@pytest.mark.parametrize("name,code,line", [("sb_n3_v1_e2_r3", 14, "Error: The first argument of Assert evaluated to FALSE"),
+                                            ("cpl_n3_v2_e1_r3", 75, "Error: Evaluating invariant Inv failed.")])
+def test_launcher_reports_bfs_errors(name, code, line, tmp_path):
+    """raftmc on the test variants (named as tools/make_seeded_spec.py writes them): TLC's error lines
+    and exit codes for the Assert and the evaluation error, the counterexample's length and TLC's
+    counters at the error."""
+    import subprocess
+    from test_host import LAUNCHER, cfg_text
+    g = LEVELS_ERR[name]
+    mod = {"split_brain": "RaftSplitBrain", "commit_past_log": "RaftCommitPastLog"}[g["variant"]]
+    (tmp_path / f"{mod}.cfg").write_text(cfg_text(E=g["E"], R=g["R"], vals=", ".join(f"v{i + 1}" for i in range(g["V"]))))
+    env = dict(os.environ, RMC_SKIP_SPEC_CHECK="1")
+    r = subprocess.run([LAUNCHER, "-deadlock", "-config", str(tmp_path / f"{mod}.cfg"), str(tmp_path / f"{mod}.tla")],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == code, r.stdout + r.stderr
+    assert any(ln.startswith(line) for ln in r.stdout.splitlines()), r.stdout
+    assert sum(1 for ln in r.stdout.splitlines() if ln.startswith("State ")) == g["trace_len"]
+    assert (f"{g['generated']} states generated, {g['distinct']} distinct states found, {g['queue_left']} states "
+            f"left on queue.") in r.stdout
 
 
 @pytest.mark.parametrize("shards", [2, 4])

@@ -267,3 +267,18 @@ def test_bench_counters_at_scale_read_from_profiles():
         assert abs(hbm / alg - v["aggregate"]["ratio"]) < 2e-3
         assert abs(alg / ms / 1e6 / bench.HBM_PEAK_GBS - v["aggregate"]["alg_frac"]) < 2e-5
         assert c[k]["ratio"] == v["aggregate"]["ratio"]
+
+
+def test_error_variant_specs_recognised():
+    """tools/make_seeded_spec.py --split-brain / --commit-past-log on Raft.tla (skipped where the
+    reference is absent): the parser maps each text to its variant by content hash."""
+    if not os.path.exists(REF_TLA):
+        pytest.skip("reference Raft.tla not present")
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import make_seeded_spec as M
+    tla = open(REF_TLA).read()
+    assert raftmc.parse_config(cfg_text(), M.split_brain(tla)).spec_variant == raftmc.SPEC_SPLIT_BRAIN
+    assert raftmc.parse_config(cfg_text(), M.commit_past_log(tla)).spec_variant == raftmc.SPEC_COMMIT_PAST_LOG
+    with pytest.raises(raftmc.RmcError, match="not kikimo"):
+        raftmc.parse_config(cfg_text(), M.split_brain(tla).replace(">= 1 ", ">= 2 "))

@@ -295,3 +295,17 @@ def test_deep_fixture_coverage_and_python_recheck():
                 except R.EvalError:
                     got = None
                 assert got == v, nm
+
+
+@pytest.mark.parametrize("name", ["sb_n3_v1_e2_r3", "sb_n2_v1_e2_r3", "cpl_n3_v2_e1_r3", "sb_n3_v1_e3_r3"])
+def test_error_variant_fixtures_recheck(name):
+    """The test variants that reach the Assert / Inv's evaluation error in a BFS (RaftSplitBrain,
+    RaftCommitPastLog): the Python restatement reproduces the committed fixture (generated by both
+    oracles, tests/golden/make_golden_errors.py) -- verdict, TLC's counters, trace length."""
+    g = json.load(open(os.path.join(GOLDEN, "levels_errors.json")))[name]
+    cfg = R.Config(n=g["n"], V=g["V"], max_election=g["E"], max_restart=g["R"], invariants=tuple(g["invariants"]),
+                   **{g["variant"]: True})
+    p = R.bfs(cfg)
+    assert (p.verdict, p.generated, p.distinct, p.queue_left, len(p.trace)) == \
+        (g["verdict"], g["generated"], g["distinct"], g["queue_left"], g["trace_len"])
+    assert p.levels[:-1] == g["levels"][:-1]

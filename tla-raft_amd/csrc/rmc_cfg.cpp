@@ -25,6 +25,10 @@ static const uint64_t FNV_RAFT_FAPP = 0x1319b28a1b001651ULL;
 // Raft.tla with Next's `\/ BecomeFollower(s)` uncommented (tla:420; tools/make_variant_spec.py
 // --become-follower): RMC_SPEC_BECOME_FOLLOWER.
 static const uint64_t FNV_RAFT_BF = 0xc3850410336560ebULL;
+// test variants (tools/make_seeded_spec.py --split-brain / --commit-past-log): the Assert (tla:185) and
+// the evaluation error (tla:499) reachable in a BFS
+static const uint64_t FNV_RAFT_SPLIT_BRAIN = 0x3dd92c869822b066ULL;
+static const uint64_t FNV_RAFT_COMMIT_PAST_LOG = 0x1d4d6d5e2014bcc5ULL;
 
 uint64_t fnv1a_spec(const std::string &text) {
     uint64_t h = 0xcbf29ce484222325ULL;
@@ -272,6 +276,11 @@ bool parse_model(const std::string &cfg_text, const char *tla_text, ParsedModel 
         if (h == FNV_RAFT || h == FNV_RAFT_FAPP) { pm->cfg.spec_variant = RMC_SPEC_RAFT; pm->module = "Raft"; }
         else if (h == FNV_RAFT_SEEDED) { pm->cfg.spec_variant = RMC_SPEC_SEEDED; pm->module = "RaftSeeded"; }
         else if (h == FNV_RAFT_BF) { pm->cfg.spec_variant = RMC_SPEC_BECOME_FOLLOWER; pm->module = "Raft"; }
+        else if (h == FNV_RAFT_SPLIT_BRAIN) { pm->cfg.spec_variant = RMC_SPEC_SPLIT_BRAIN; pm->module = "RaftSplitBrain"; }
+        else if (h == FNV_RAFT_COMMIT_PAST_LOG) {
+            pm->cfg.spec_variant = RMC_SPEC_COMMIT_PAST_LOG;
+            pm->module = "RaftCommitPastLog";
+        }
         else {
             char buf[64];
             snprintf(buf, sizeof buf, "%016llx", (unsigned long long)h);

@@ -472,6 +472,7 @@ struct rmc_ctx {
         P.E = cfg.max_election;
         P.R = cfg.max_restart;
         P.seeded = cfg.spec_variant == RMC_SPEC_SEEDED;
+        P.quirks = (cfg.spec_variant == RMC_SPEC_SPLIT_BRAIN ? 1u : 0u) | (cfg.spec_variant == RMC_SPEC_COMMIT_PAST_LOG ? 2u : 0u);
         P.check_deadlock = cfg.check_deadlock;
         P.inv_mask = cfg.invariants;
         P.inv_order = inv_order;
@@ -716,7 +717,7 @@ struct rmc_ctx {
         N = cfg.n_servers;
         V = cfg.n_vals;
         int cap = cfg.msg_cap ? cfg.msg_cap : (N <= 3 ? 64 : 128);
-        if (cfg.spec_variant < RMC_SPEC_RAFT || cfg.spec_variant > RMC_SPEC_BECOME_FOLLOWER)
+        if (cfg.spec_variant < RMC_SPEC_RAFT || cfg.spec_variant > RMC_SPEC_COMMIT_PAST_LOG)
             throw Fail(RMC_E_ARG, "unknown spec_variant " + std::to_string(cfg.spec_variant));
         if (!get_kernels(N, V, cap, cfg.spec_variant == RMC_SPEC_BECOME_FOLLOWER, &ks))
             throw Fail(RMC_E_ARG, "no compiled kernels for n_servers=" + std::to_string(N) + " n_vals=" +

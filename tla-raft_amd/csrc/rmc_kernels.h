@@ -119,6 +119,9 @@ struct KParams {
     // seen-set probe and the election (bit 0); bit 1: k_insert_winners puts the winners into the seen
     // set, not the commit; bit 2: ... and leaves its verdicts in lslot (LS_WIN / LS_SEEN) for the commit
     int split;
+    // test variants: bit 0 RaftSplitBrain (BecomeLeader's quorum 1), bit 1 RaftCommitPastLog
+    // (FollowerAcceptEntry's newCommitIndex without Min(., Len(newLog)))
+    uint32_t quirks;
     // fused single-shard level: expand (+hash, +seen-set probe, +election, +staging) -> wincount
     // -> commit.  Successor slot q = (p - p_begin) * maxsucc + rank is sparse and increases in
     // TLC order; it indexes fp, lslot and score (the staged successor: its acting server's row,

@@ -755,7 +755,7 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
             const bool append_new = nl > ll;
             const uint32_t eb = mi_et(m) | (mi_ev(m) << 4);
             const bool truncated = nl <= ll && ent && lw_byte(lw, nl) != eb;
-            const uint32_t mn = lc < nl ? lc : nl;
+            const uint32_t mn = (lc < nl || (P.quirks & 2u)) ? lc : nl;  // (RaftCommitPastLog: no Min)
             const uint32_t ci = nib(W.c[Lo::W_CI], s);
             const uint32_t nci = ci > mn ? ci : mn;
             const uint32_t resp = pid;  // nat2id[nat_aresp(s, src, mt, pli + ent, TRUE)]
@@ -870,7 +870,7 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
     if (t == 1) {  // BecomeLeader tla:157-173
         if (role != CAN) return;
         const uint32_t vp = W.lds[Lo::NW + s];
-        if (!(vp + 1 >= (uint32_t)(N / 2 + 1))) return;
+        if (!(vp + 1 >= ((P.quirks & 1u) ? 1u : (uint32_t)(N / 2 + 1)))) return;  // (RaftSplitBrain: quorum 1)
         uint32_t mirow = 0, nirow = 0;
 #pragma unroll
         for (int u = 0; u < N; u++) {

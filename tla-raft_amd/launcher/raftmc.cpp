@@ -282,6 +282,8 @@ int main(int argc, char **argv) {
     if (skip_spec) {
         const std::string base = tla_path.substr(tla_path.find_last_of('/') + 1);
         if (base == "RaftSeeded.tla") { pm.cfg.spec_variant = RMC_SPEC_SEEDED; pm.module = "RaftSeeded"; }
+        if (base == "RaftSplitBrain.tla") { pm.cfg.spec_variant = RMC_SPEC_SPLIT_BRAIN; pm.module = "RaftSplitBrain"; }
+        if (base == "RaftCommitPastLog.tla") { pm.cfg.spec_variant = RMC_SPEC_COMMIT_PAST_LOG; pm.module = "RaftCommitPastLog"; }
     }
     if (pm.check_deadlock_cfg >= 0 && check_deadlock) check_deadlock = pm.check_deadlock_cfg;
     rmc_config cfg = pm.cfg;

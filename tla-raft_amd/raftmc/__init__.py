@@ -35,6 +35,7 @@ ACTIONS = ("BecomeCandidate", "UpdateTerm", "ResponseVote", "BecomeLeader", "Cli
            "FollowerAcceptEntry", "FollowerRejectEntry", "HandleAppendResp", "LeaderCanCommit", "Restart",
            "FollowerAppendEntry", "BecomeFollower")  # 11: never enabled (tla:425 variant); 12: tla:420 variant
 SPEC_RAFT, SPEC_SEEDED, SPEC_BECOME_FOLLOWER = 0, 1, 2
+SPEC_SPLIT_BRAIN, SPEC_COMMIT_PAST_LOG = 3, 4  # test variants: Assert / evaluation error reachable in a BFS
 
 
 class RmcError(RuntimeError):
