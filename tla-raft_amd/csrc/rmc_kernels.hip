@@ -1399,18 +1399,26 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
     constexpr bool SIG = SUMS && N >= 4;                // signature pre-sort (coset minimum)
     constexpr int NPM = (SUMS && !SIG) ? factorial(N) : 1;  // |Permutations(Servers)| (tla:21)
     constexpr int MAXS = SUMS ? MX : 1;
-    constexpr int MAXG = SIG ? MAXS : 1;
+    // n >= 4 (signature path): the successors are hashed in batches of 64 (by TLC rank), so the row
+    // arrays hold one batch -- the LDS of a block no longer caps the 2 waves / SIMD the registers allow
+    // (25.8 -> ~15 KB for 5 servers); a parent has more than 64 successors only rarely
+    constexpr int SBAT = SIG ? 64 : MAXS;
+    constexpr int MAXG = SIG ? SBAT : 1;
     __shared__ uint64_t Rt[2][NPM * N], Tt[2][NPM];     // parent row terms / totals per permutation
     __shared__ uint64_t sdS[2][N], sdP[2][N * N];       // position seeds
     __shared__ uint8_t pimg[NPM * N];                   // permutation images
-    __shared__ uint64_t sU[MAXS], sX[2][MAXS * N];      // compacted successor rows
+    __shared__ uint64_t sU[SBAT], sX[2][SBAT * N];      // compacted successor rows (of one batch when SIG)
+    // SIG: every successor's row inputs by TLC rank (own word; matchIndex row | votedFor << 20;
+    // nextIndex row; its added messages' info words in sAinf: sCa)
+    __shared__ uint64_t sUg[SIG ? MAXS : 1];
+    __shared__ uint32_t sW1[SIG ? MAXS : 1], sW2[SIG ? MAXS : 1];
     __shared__ uint8_t sS[MAXS], sNa[MAXS];             // acting server, |added ids| per successor
     // CPT (n <= 3): the successors' hash rows are built in one pass over the compacted successors (a
     // lane each) instead of once per candidate kind -- per successor its rows and votedFor (sCp) and
     // where its added messages' info words are (sCa)
     constexpr bool CPT = RMC_HASH_COMPACT && !SIG && N <= 3;
     __shared__ uint32_t sCp[CPT ? MAXS : 1];
-    __shared__ uint16_t sCa[CPT ? MAXS : 1];
+    __shared__ uint16_t sCa[(CPT || SIG) ? MAXS : 1];
     // signature pre-sort: parent rows / signatures, per successor the tie ranks, the first task
     // of its coset (exclusive scan of coset sizes) and its running minimum; per task its successor
     __shared__ uint64_t pU[SIG ? N : 1], pX[2][SIG ? N * N : 1], psig[SIG ? N : 1];
@@ -1631,8 +1639,26 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
                     }
                 }
             }
+            if constexpr (SIG) {
+                // stage each successor's row inputs by its TLC rank; the batches below build its hash rows
+                // and signature ranks a lane per successor, 64 successors at a time
 #pragma unroll
-            for (int r = 0; r < NC && !CPT; r++) {
+                for (int r = 0; r < NC; r++) {
+                    if (cand[r].key == KEY_NONE) continue;
+                    const Succ<N, V, MR> &o = cand[r];
+                    const uint32_t g = rank[r];
+                    const uint32_t vfs = nib(o.c[Lo::W_VF], o.s);
+                    sUg[g] = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI], o.c[Lo::W_LL],
+                                         o.lw, o.mirow, o.nirow, o.s);
+                    sW1[g] = o.mirow | (vfs << 20);  // rows of N <= 5 nibbles
+                    sW2[g] = o.nirow;
+                    sCa[g] = (uint16_t)(((r <= MR ? r : 0) * 64 + lane) * S::NADD);
+                    sS[g] = (uint8_t)o.s;
+                    sNa[g] = (uint8_t)o.nadd;
+                }
+            } else if constexpr (!CPT) {
+#pragma unroll
+            for (int r = 0; r < NC; r++) {
                 if (cand[r].key == KEY_NONE) continue;
                 const Succ<N, V, MR> &o = cand[r];
                 const uint32_t sl = rank[r];
@@ -1643,27 +1669,15 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
                 const uint64_t u = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI],
                                                o.c[Lo::W_LL], o.lw, o.mirow, o.nirow, o.s);
                 sU[sl] = u;
-                uint64_t sg = sig_part_u(u);
 #pragma unroll
                 for (int j = 0; j < N; j++) {
                     const uint64_t sm = pair_small(o.mirow, o.nirow, vfs, j);
-                    const uint64_t x0 = row0[j] ^ (sm * PAIR_K0);
-                    sX[0][sl * N + j] = x0;
+                    sX[0][sl * N + j] = row0[j] ^ (sm * PAIR_K0);
                     sX[1][sl * N + j] = row1[j] ^ (sm * PAIR_K1);
-                    if ((uint32_t)j != o.s) sg += sig_part_x(x0);
                 }
                 sS[sl] = (uint8_t)o.s;
                 sNa[sl] = (uint8_t)o.nadd;
-                if (SIG) {
-                    // only the acting server's row changes (every message it adds is its own)
-                    uint64_t sig[N];
-#pragma unroll
-                    for (int t = 0; t < N; t++) sig[t] = (uint32_t)t == o.s ? sg : psig[t];
-                    const uint32_t rk = coset_ranks<N>(sig);
-                    sRk[sl] = rk;
-                    sKoff[sl] = coset_size<N>(rk);
-                    sBest[sl] = make_ulonglong2(~0ull, ~0ull);
-                }
+            }
             }
             __syncthreads();
             // the successor's fingerprint: seen-set probe + election (fused), or the hash pass output
@@ -1693,59 +1707,86 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
                 }
             };
             if (SIG) {
-                // (c') one task per (successor, allowed permutation): exclusive scan of the coset
-                //      sizes, then 64 tasks per round; a successor's tasks are consecutive, so the
-                //      first lane of each run folds the run into the successor's minimum
-                uint32_t ntask = 0;
-                for (uint32_t b0 = 0; b0 < total; b0 += 64) {
-                    const uint32_t l = b0 + (uint32_t)lane;
-                    uint32_t rt;
-                    const uint32_t ex = wave_excl_scan(l < total ? sKoff[l] : 0u, lane, &rt);
-                    if (l < total) sKoff[l] = ntask + ex;
-                    ntask += rt;
-                }
-                __syncthreads();
-                for (uint32_t tb = 0; tb < ntask; tb += 64) {
-                    const uint32_t ti = tb + (uint32_t)lane;
-                    uint32_t l = 0xFFFFFFFFu;
-                    ulonglong2 h = make_ulonglong2(~0ull, ~0ull);
-                    if (ti < ntask) {
-                        uint32_t a = 0, b = total;  // sKoff[a] <= ti < sKoff[b]
-                        while (b - a > 1) {
-                            const uint32_t m = (a + b) >> 1;
-                            if (sKoff[m] <= ti) a = m; else b = m;
+                // (c') per batch of 64 successors: one task per (successor, allowed permutation) --
+                //      exclusive scan of the coset sizes, then 64 tasks per round; a successor's tasks
+                //      are consecutive, so the first lane of each run folds the run into its minimum
+                for (uint32_t b0 = 0; b0 < total; b0 += (uint32_t)SBAT) {
+                    const uint32_t nb = total - b0 < (uint32_t)SBAT ? total - b0 : (uint32_t)SBAT;
+                    if ((uint32_t)lane < nb) {  // successor b0 + lane: hash rows, signature, coset
+                        const uint32_t l = (uint32_t)lane, g = b0 + l;
+                        const uint32_t sv = sS[g], w1 = sW1[g];
+                        const uint32_t mirow = w1 & 0xFFFFFu, vfs = w1 >> 20, nirow = sW2[g];
+                        const uint64_t u = sUg[g];
+                        uint64_t row0[N], row1[N];
+                        succ_row_at<N, V, MR>(sv, sNa[g], M0, M1, &sAinf[sCa[g]], row0, row1);
+                        sU[l] = u;
+                        uint64_t sg = sig_part_u(u);
+#pragma unroll
+                        for (int j = 0; j < N; j++) {
+                            const uint64_t sm = pair_small(mirow, nirow, vfs, j);
+                            const uint64_t x0 = row0[j] ^ (sm * PAIR_K0);
+                            sX[0][l * N + j] = x0;
+                            sX[1][l * N + j] = row1[j] ^ (sm * PAIR_K1);
+                            if ((uint32_t)j != sv) sg += sig_part_x(x0);
                         }
-                        l = a;
-                        uint32_t img[N];
-                        coset_img<N>(sRk[l], ti - sKoff[l], img);
-                        const uint32_t sv = sS[l];
-                        const uint64_t su = sU[l];
-                        h = hash_at<N>(
-                            img, [&](int t) { return (uint32_t)t == sv ? su : pU[t]; },
-                            [&](int f, int t, int j) {
-                                return (uint32_t)t == sv ? sX[f][l * N + j] : pX[f][t * N + j];
-                            },
-                            [&](int f, uint32_t x) { return sdS[f][x]; },
-                            [&](int f, uint32_t x, uint32_t y) { return sdP[f][x * N + y]; });
-                    }
-                    sPart[lane] = h;
-                    sTl[lane] = l;
-                    __syncthreads();
-                    if (ti < ntask && (lane == 0 || sTl[lane - 1] != l)) {
-                        ulonglong2 best = sBest[l];
-                        for (int j = lane; j < 64 && sTl[j] == l; j++)
-                            if (lex_less(sPart[j], best)) best = sPart[j];
-                        sBest[l] = best;
+                        // only the acting server's row changes (every message it adds is its own)
+                        uint64_t sig[N];
+#pragma unroll
+                        for (int t = 0; t < N; t++) sig[t] = (uint32_t)t == sv ? sg : psig[t];
+                        const uint32_t rk = coset_ranks<N>(sig);
+                        sRk[l] = rk;
+                        sKoff[l] = coset_size<N>(rk);
+                        sBest[l] = make_ulonglong2(~0ull, ~0ull);
                     }
                     __syncthreads();
+                    uint32_t ntask = 0;
+                    {
+                        const uint32_t l = (uint32_t)lane;
+                        uint32_t rt;
+                        const uint32_t ex = wave_excl_scan(l < nb ? sKoff[l] : 0u, lane, &rt);
+                        if (l < nb) sKoff[l] = ex;
+                        ntask = rt;
+                    }
+                    __syncthreads();
+                    for (uint32_t tb = 0; tb < ntask; tb += 64) {
+                        const uint32_t ti = tb + (uint32_t)lane;
+                        uint32_t l = 0xFFFFFFFFu;
+                        ulonglong2 h = make_ulonglong2(~0ull, ~0ull);
+                        if (ti < ntask) {
+                            uint32_t a = 0, b = nb;  // sKoff[a] <= ti < sKoff[b]
+                            while (b - a > 1) {
+                                const uint32_t m = (a + b) >> 1;
+                                if (sKoff[m] <= ti) a = m; else b = m;
+                            }
+                            l = a;
+                            uint32_t img[N];
+                            coset_img<N>(sRk[l], ti - sKoff[l], img);
+                            const uint32_t sv = sS[b0 + l];
+                            const uint64_t su = sU[l];
+                            h = hash_at<N>(
+                                img, [&](int t) { return (uint32_t)t == sv ? su : pU[t]; },
+                                [&](int f, int t, int j) {
+                                    return (uint32_t)t == sv ? sX[f][l * N + j] : pX[f][t * N + j];
+                                },
+                                [&](int f, uint32_t x) { return sdS[f][x]; },
+                                [&](int f, uint32_t x, uint32_t y) { return sdP[f][x * N + y]; });
+                        }
+                        sPart[lane] = h;
+                        sTl[lane] = l;
+                        __syncthreads();
+                        if (ti < ntask && (lane == 0 || sTl[lane - 1] != l)) {
+                            ulonglong2 best = sBest[l];
+                            for (int j = lane; j < 64 && sTl[j] == l; j++)
+                                if (lex_less(sPart[j], best)) best = sPart[j];
+                            sBest[l] = best;
+                        }
+                        __syncthreads();
+                    }
+                    PHASE(5);
+                    if ((uint32_t)lane < nb) emit(b0 + (uint32_t)lane, sBest[lane]);
+                    __syncthreads();
+                    PHASE(6);
                 }
-                PHASE(5);
-                for (uint32_t b0 = 0; b0 < total; b0 += 64) {
-                    const uint32_t lo = b0 + (uint32_t)lane;
-                    if (lo < total) emit(lo, sBest[lo]);
-                }
-                __syncthreads();
-                PHASE(6);
             } else {
                 for (int pp = lane; pp < np; pp += 64) {
                     uint64_t t0 = 0, t1 = 0;
