@@ -33,6 +33,7 @@
 #include <vector>
 
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include "rmc.h"
@@ -163,135 +164,58 @@ uint64_t free_device_bytes() {
     return f;
 }
 
-// Pinned host blocks of one size, made ahead of need by a background thread once a run starts
-// taking them: pinning runs at a few GB/s, and done where a trace flush first needs the block it
-// stalls the level loop (a Raft.cfg exhaustion pins ~110 GB of trace).  A block the pool cannot
-// pin is pageable (new char[]).
-class PinnedPool {
-  public:
-    PinnedPool(size_t bytes, int ready) : bytes_(bytes), ready_(ready), th_([this] { run(); }) {}
-    ~PinnedPool() {
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        th_.join();
-        for (void *p : free_) (void)hipHostFree(p);
-    }
-    void *take(bool *pinned) {
-        {
-            std::unique_lock<std::mutex> lk(m_);
-            demand_ = true;
-            if (!free_.empty()) {
-                void *p = free_.back();
-                free_.pop_back();
-                lk.unlock();
-                cv_.notify_all();
-                *pinned = true;
-                return p;
-            }
-        }
-        cv_.notify_all();
-        void *p = nullptr;
-        if (hipHostMalloc(&p, bytes_, hipHostMallocDefault) == hipSuccess) {
-            *pinned = true;
-            return p;
-        }
-        (void)hipGetLastError();
-        *pinned = false;
-        return new char[bytes_];
-    }
+// Host memory of the trace (parent's global id + slot key of every state the run found: ~110 GB
+// at Raft.cfg): pageable blocks on transparent huge pages.  Round 2 kept it in pinned blocks (the
+// device copied straight into them; pinned ahead of need by a background thread, since pinning
+// runs at a few GB/s), but the process gives pinned memory back at ~9 GB/s when it exits: 12 s of
+// myrun.sh's wall time after TLC's "Finished" line.  Huge-page blocks go back ~3x faster and are
+// made ~2x faster (profiles/r03_teardown_probe.txt); the device copies into a few pinned staging
+// buffers instead and a host thread moves each into its blocks (TraceStager).
+static void *thp_alloc(size_t bytes) {
+    void *p = nullptr;
+    if (posix_memalign(&p, 2u << 20, bytes) != 0 || !p) throw Fail(RMC_E_MEMORY, "host memory for the trace");
+    (void)madvise(p, bytes, MADV_HUGEPAGE);
+    return p;
+}
 
-  private:
-    void run() {
-        std::unique_lock<std::mutex> lk(m_);
-        while (!stop_) {
-            if (demand_ && !failed_ && (int)free_.size() < ready_) {
-                lk.unlock();
-                void *p = nullptr;
-                const bool ok = hipHostMalloc(&p, bytes_, hipHostMallocDefault) == hipSuccess;
-                if (!ok) (void)hipGetLastError();
-                lk.lock();
-                if (ok) free_.push_back(p);
-                else failed_ = true;
-                continue;
-            }
-            cv_.wait(lk);
-        }
-    }
-    const size_t bytes_;
-    const int ready_;
-    std::mutex m_;
-    std::condition_variable cv_;
-    std::vector<void *> free_;
-    bool stop_ = false, demand_ = false, failed_ = false;
-    std::thread th_;
-};
-
-// Host array in pinned blocks (falls back to pageable blocks): the trace of every state the run
-// found, written by asynchronous device-to-host copies chunk by chunk, never reallocated.
+// Host array in huge-page blocks: the trace of every state the run found, never reallocated
+// (block pointers stay valid while later blocks are added).
 template <class T>
 struct HostArr {
     static constexpr uint64_t B = 1ull << 22;
-    struct Blk {
-        T *p = nullptr;
-        bool pinned = false;
-    };
-    std::vector<Blk> blk;
+    std::vector<T *> blk;
     uint64_t n = 0;
-    PinnedPool *pool = nullptr;  // blocks of B * sizeof(T) bytes, pinned ahead of need
     HostArr() = default;
     HostArr(const HostArr &) = delete;
     HostArr &operator=(const HostArr &) = delete;
-    HostArr(HostArr &&o) noexcept : blk(std::move(o.blk)), n(o.n), pool(o.pool) { o.blk.clear(); o.n = 0; }
+    HostArr(HostArr &&o) noexcept : blk(std::move(o.blk)), n(o.n) { o.blk.clear(); o.n = 0; }
     HostArr &operator=(HostArr &&o) noexcept {
-        if (this != &o) { release(); blk = std::move(o.blk); n = o.n; pool = o.pool; o.blk.clear(); o.n = 0; }
+        if (this != &o) { release(); blk = std::move(o.blk); n = o.n; o.blk.clear(); o.n = 0; }
         return *this;
     }
     ~HostArr() { release(); }
     void release() {
-        for (Blk &b : blk) {
-            if (b.pinned) (void)hipHostFree(b.p);
-            else delete[] reinterpret_cast<char *>(b.p);
-        }
+        for (T *p : blk) std::free(p);
         blk.clear();
         n = 0;
     }
     void reserve_to(uint64_t m) {
-        while ((uint64_t)blk.size() * B < m) {
-            Blk b;
-            if (pool) {
-                b.p = static_cast<T *>(pool->take(&b.pinned));
-            } else if (hipHostMalloc((void **)&b.p, B * sizeof(T), hipHostMallocDefault) == hipSuccess) {
-                b.pinned = true;
-            } else {
-                (void)hipGetLastError();
-                b.p = reinterpret_cast<T *>(new char[B * sizeof(T)]);
-            }
-            blk.push_back(b);
-        }
+        while ((uint64_t)blk.size() * B < m) blk.push_back(static_cast<T *>(thp_alloc(B * sizeof(T))));
     }
-    T get(uint64_t i) const { return blk[i / B].p[i % B]; }
+    T get(uint64_t i) const { return blk[i / B][i % B]; }
     void set(uint64_t i, T v) {
         reserve_to(i + 1);
-        blk[i / B].p[i % B] = v;
+        blk[i / B][i % B] = v;
         n = std::max(n, i + 1);
     }
-    // elements [at, at + cnt) from device memory, enqueued on `s` (the caller syncs before reading)
-    void from_device(const T *dev, uint64_t at, uint64_t cnt, hipStream_t s) {
+    void extend(uint64_t at, uint64_t cnt) {  // elements [at, at + cnt) will be written (TraceStager)
         reserve_to(at + cnt);
-        for (uint64_t i = 0; i < cnt;) {
-            const uint64_t g = at + i, k = std::min(cnt - i, B - g % B);
-            HIPCHK(hipMemcpyAsync(blk[g / B].p + g % B, dev + i, k * sizeof(T), hipMemcpyDeviceToHost, s));
-            i += k;
-        }
         n = std::max(n, at + cnt);
     }
     void to_device(T *dev, uint64_t at, uint64_t cnt) const {
         for (uint64_t i = 0; i < cnt;) {
             const uint64_t g = at + i, k = std::min(cnt - i, B - g % B);
-            HIPCHK(hipMemcpy(dev + i, blk[g / B].p + g % B, k * sizeof(T), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(dev + i, blk[g / B] + g % B, k * sizeof(T), hipMemcpyHostToDevice));
             i += k;
         }
     }
@@ -299,15 +223,128 @@ struct HostArr {
     void for_range(uint64_t at, uint64_t cnt, F &&f) const {  // f(pointer, count) over contiguous pieces
         for (uint64_t i = 0; i < cnt;) {
             const uint64_t g = at + i, k = std::min(cnt - i, B - g % B);
-            f(blk[g / B].p + g % B, k);
+            f(blk[g / B] + g % B, k);
             i += k;
         }
     }
     void copy_from(const HostArr &o, uint64_t at, uint64_t cnt) {
         reserve_to(at + cnt);
-        for (uint64_t i = 0; i < cnt; i++) blk[(at + i) / B].p[(at + i) % B] = o.get(at + i);
+        for (uint64_t i = 0; i < cnt; i++) blk[(at + i) / B][(at + i) % B] = o.get(at + i);
         n = std::max(n, at + cnt);
     }
+};
+
+// Trace flushes: device -> one of K pinned staging buffers on the copy stream, then a host thread
+// waits for that copy's event and moves the entries into the HostArr blocks (whose addresses the
+// caller resolved when it enqueued: the workers never touch a block vector).  The caller waits
+// for a free staging buffer, so at most K pieces are in flight.  Several workers: the first touch of
+// a fresh block (page faults) runs at a few GB/s per thread, and Raft.cfg's widest levels find
+// ~5 GB of trace per second.
+class TraceStager {
+  public:
+    static constexpr uint64_t S = 1ull << 22;  // entries per staging buffer
+    static constexpr int K = 8, NW = 4;        // staging buffers, worker threads
+    TraceStager() {
+        for (int b = 0; b < K; b++) {
+            HIPCHK(hipHostMalloc((void **)&par_[b], S * 8, hipHostMallocDefault));
+            HIPCHK(hipHostMalloc((void **)&slot_[b], S * 2, hipHostMallocDefault));
+            HIPCHK(hipEventCreateWithFlags(&ev_[b], hipEventDisableTiming));
+            free_.push_back(b);
+        }
+        for (int t = 0; t < NW; t++) th_[t] = std::thread([this] { run(); });
+    }
+    ~TraceStager() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread &t : th_) t.join();
+        for (int b = 0; b < K; b++) {
+            (void)hipHostFree(par_[b]);
+            (void)hipHostFree(slot_[b]);
+            (void)hipEventDestroy(ev_[b]);
+        }
+    }
+    // entries [at, at + cnt) of (hpar, hslot) from device memory, copied on stream `cs` after what
+    // is already enqueued there
+    void enqueue(const uint64_t *dpar, const uint16_t *dslot, uint64_t cnt, HostArr<uint64_t> &hpar,
+                 HostArr<uint16_t> &hslot, uint64_t at, hipStream_t cs) {
+        hpar.extend(at, cnt);
+        hslot.extend(at, cnt);
+        for (uint64_t i = 0; i < cnt;) {
+            const uint64_t k = std::min(cnt - i, S);
+            int b;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return !free_.empty() || failed_; });
+                if (failed_) throw Fail(RMC_E_DEVICE, "trace copy to the host failed");
+                b = free_.back();
+                free_.pop_back();
+            }
+            HIPCHK(hipMemcpyAsync(par_[b], dpar + i, k * 8, hipMemcpyDeviceToHost, cs));
+            HIPCHK(hipMemcpyAsync(slot_[b], dslot + i, k * 2, hipMemcpyDeviceToHost, cs));
+            HIPCHK(hipEventRecord(ev_[b], cs));
+            Job j;
+            j.b = b;
+            hpar.for_range(at + i, k, [&](uint64_t *p, uint64_t c) { j.pp[j.np] = p; j.pc[j.np++] = c; });
+            int q = 0;  // (same block size: the same pieces)
+            hslot.for_range(at + i, k, [&](uint16_t *p, uint64_t c) { j.sp[q] = p; j.sc[q++] = c; });
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                jobs_.push_back(j);
+            }
+            cv_.notify_all();
+            i += k;
+        }
+    }
+    // every enqueued piece is in its blocks (the copy stream is synchronised first by the caller)
+    void drain() {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return (jobs_.empty() && (int)free_.size() == K) || failed_; });
+        if (failed_) throw Fail(RMC_E_DEVICE, "trace copy to the host failed");
+    }
+
+  private:
+    struct Job {  // a piece of <= S entries spans at most two blocks (S == HostArr::B)
+        int b = 0, np = 0;
+        uint64_t *pp[2] = {};
+        uint64_t pc[2] = {};
+        uint16_t *sp[2] = {};
+        uint64_t sc[2] = {};
+    };
+    void run() {
+        std::unique_lock<std::mutex> lk(m_);
+        for (;;) {
+            cv_.wait(lk, [&] { return stop_ || !jobs_.empty(); });
+            if (jobs_.empty()) return;  // stop_
+            Job j = jobs_.front();
+            jobs_.erase(jobs_.begin());
+            lk.unlock();
+            const bool ok = hipEventSynchronize(ev_[j.b]) == hipSuccess;
+            if (ok) {
+                uint64_t o = 0;
+                for (int t = 0; t < j.np; t++) {
+                    std::memcpy(j.pp[t], par_[j.b] + o, j.pc[t] * 8);
+                    std::memcpy(j.sp[t], slot_[j.b] + o, j.sc[t] * 2);
+                    o += j.pc[t];
+                }
+            }
+            lk.lock();
+            if (!ok) failed_ = true;
+            free_.push_back(j.b);
+            cv_.notify_all();
+        }
+    }
+    uint64_t *par_[K] = {};
+    uint16_t *slot_[K] = {};
+    hipEvent_t ev_[K] = {};
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::vector<int> free_;
+    std::vector<Job> jobs_;
+    bool stop_ = false, failed_ = false;
+    std::thread th_[NW];
 };
 
 enum Phase { PH_COUNT = 0, PH_HASH = 1, PH_DEDUP = 2, PH_MAT = 3, PH_XCHG = 4, PH_OTHER = 5 };
@@ -363,6 +400,7 @@ struct Shard {
     uint4 *score = nullptr;
     uint32_t *wcnt = nullptr, *wacc = nullptr, *pnm = nullptr, *wposw = nullptr, *ctick = nullptr;
     uint32_t *bw = nullptr, *bg = nullptr, *boff = nullptr, *bww = nullptr, *boffw = nullptr, *tickets = nullptr;
+    uint32_t *bn = nullptr, *boffn = nullptr, *plist = nullptr;  // parents with winners (split chunks)
     // device-driven level loop: control block, per-level records, and their pinned host copies
     LevelCtl *ctl = nullptr, *hctl = nullptr;
     HostLoop *hloop = nullptr, *dloop = nullptr;  // device-loop mirror in mapped pinned memory (host / device view)
@@ -402,7 +440,7 @@ struct rmc_ctx {
     hipStream_t stream = nullptr;
     hipStream_t cstream = nullptr;  // trace flushes (device -> pinned host), overlapped with the level loop
     hipEvent_t flush_ev = nullptr;  // the main stream's point a flush starts from
-    std::unique_ptr<PinnedPool> pool_par, pool_slot;
+    std::unique_ptr<TraceStager> stager;  // trace flushes to the host arrays
     int N = 0, V = 0, RECW = 0;  // RECW = the longest record (fixed-stride buffers)
     uint32_t inv_order = 0;      // invariants in cfg order (check_invs)
     int W = 1, rank = 0;  // shards in the run, this process's first shard
@@ -510,6 +548,7 @@ struct rmc_ctx {
         ring_params(s, Q);
         Q.cnt = s.cnt; Q.fp = s.fp; Q.wpos = s.wpos; Q.wcnt = s.wcnt; Q.wacc = s.wacc; Q.pnm = s.pnm;
         Q.wposw = s.wposw; Q.bw = s.bw; Q.bg = s.bg; Q.boff = s.boff; Q.bww = s.bww; Q.boffw = s.boffw;
+        Q.bn = s.bn; Q.boffn = s.boffn;
         Q.tickets = s.tickets; Q.ctick = s.ctick; Q.sum = s.sum;
         Q.score = s.score; Q.lslot = s.lslot; Q.L = s.L; Q.LXY = s.LXY;
         return Q;
@@ -750,8 +789,7 @@ struct rmc_ctx {
         HIPCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&flush_ev, hipEventDisableTiming));
-        pool_par.reset(new PinnedPool(HostArr<uint64_t>::B * 8, 4));
-        pool_slot.reset(new PinnedPool(HostArr<uint16_t>::B * 2, 4));
+        stager.reset(new TraceStager());
         if (rccl) {
 #ifdef RMC_WITH_RCCL
             if (!cfg.comm_unique_id) throw Fail(RMC_E_ARG, "world_size > 1 needs comm_unique_id (rmc_comm_unique_id)");
@@ -864,8 +902,6 @@ struct rmc_ctx {
 
     void alloc_shard(Shard &s, int id) {
         s.id = id;
-        s.hpar.pool = pool_par.get();
-        s.hslot.pool = pool_slot.get();
         HIPCHK(hipEventCreateWithFlags(&s.tev, hipEventDisableTiming));
         s.cnt = dmalloc<uint32_t>(chunk_parents + 1);
         s.wpos = dmalloc<uint32_t>(Gcap + 1);
@@ -885,6 +921,9 @@ struct rmc_ctx {
         s.boff = dmalloc<uint32_t>(WTILES_MAX);
         s.bww = dmalloc<uint32_t>(WTILES_MAX);
         s.boffw = dmalloc<uint32_t>(WTILES_MAX);
+        s.bn = dmalloc<uint32_t>(WTILES_MAX);
+        s.boffn = dmalloc<uint32_t>(WTILES_MAX);
+        s.plist = dmalloc<uint32_t>(chunk_parents + 1);
         s.tickets = dmalloc<uint32_t>(4);
         HIPCHK(hipMemsetAsync(s.tickets, 0, 16, stream));
         s.ctl = dmalloc<LevelCtl>(1);
@@ -928,6 +967,7 @@ struct rmc_ctx {
         dfree(s.err); dfree(s.sum); dfree(s.flags);
         dfree(s.score); dfree(s.wcnt); dfree(s.wacc); dfree(s.pnm); dfree(s.wposw); dfree(s.ctick);
         dfree(s.bw); dfree(s.bg); dfree(s.boff); dfree(s.bww); dfree(s.boffw); dfree(s.tickets);
+        dfree(s.bn); dfree(s.boffn); dfree(s.plist);
         dfree(s.ctl); dfree(s.lrec);
         if (s.hsum) (void)hipHostFree(s.hsum);
         if (s.hctl) (void)hipHostFree(s.hctl);
@@ -943,6 +983,7 @@ struct rmc_ctx {
     void release() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (cstream) (void)hipStreamSynchronize(cstream);
+        stager.reset();  // (its thread finishes the pieces already copied: before the blocks go)
         for (Shard &s : sh) free_shard(s);
         sh.clear();
         dfree(d_info); dfree(d_nat2id); dfree(d_gmsg); dfree(d_perms); dfree(d_seeds);
@@ -964,8 +1005,6 @@ struct rmc_ctx {
         cstream = nullptr;
         if (flush_ev) (void)hipEventDestroy(flush_ev);
         flush_ev = nullptr;
-        pool_par.reset();
-        pool_slot.reset();
     }
 
     // ---- frontier storage --------------------------------------------------------------------
@@ -1038,8 +1077,7 @@ struct rmc_ctx {
         const uint64_t n = upto - s.tflushed, at = s.tflushed - s.tdev;
         HIPCHK(hipEventRecord(flush_ev, stream));
         HIPCHK(hipStreamWaitEvent(cstream, flush_ev, 0));
-        s.hpar.from_device(s.par + at, s.tflushed, n, cstream);
-        s.hslot.from_device(s.pslot + at, s.tflushed, n, cstream);
+        stager->enqueue(s.par + at, s.pslot + at, n, s.hpar, s.hslot, s.tflushed, cstream);
         HIPCHK(hipEventRecord(s.tev, cstream));
         s.tev_pending = true;
         s.tflushed = upto;
@@ -1053,7 +1091,10 @@ struct rmc_ctx {
         s.tev_pending = false;
     }
     // the host trace arrays are complete (every flush landed)
-    void sync_trace() { HIPCHK(hipStreamSynchronize(cstream)); }
+    void sync_trace() {
+        HIPCHK(hipStreamSynchronize(cstream));
+        stager->drain();
+    }
 
     // Seen set: keep the load <= 1/2 in the full (16-B) table, grown x4 by rehash, up to
     // 2^compact_log2 slots; then migrate once to the compact table sized from the budget, whose
@@ -1710,12 +1751,16 @@ struct rmc_ctx {
                 Q.Lmask = Lcap - 1;
                 Q.epoch = s.epoch;
                 Q.split = split ? (split_insert ? split_flags : 1) : 0;
+                Q.plist = split && nzlist ? s.plist : nullptr;
                 return Q;
             };
             // expand + fingerprint + seen-set probe + staging, one evaluation per parent
             timed(PH_HASH, [&] { ks.fused(params(), stream); });
             if (split) timed(PH_OTHER, [&] { ks.probe(params(), np_, stream); });
-            timed(PH_DEDUP, [&] { ks.wincount(params(), np_, stream); });
+            timed(PH_DEDUP, [&] {
+                ks.wincount(params(), np_, stream);
+                if (split && nzlist) launch_nzlist(params(), np_, stream);
+            });
             if (!small) {
                 HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
@@ -1792,6 +1837,8 @@ struct rmc_ctx {
     const uint64_t split_min = (uint64_t)env_int("RMC_SPLIT_MIN", 1 << 16, 0, 1 << 30);
     // ... and their winners go into the seen set in a pass of their own too (k_insert_winners)
     const bool split_insert = env_int("RMC_SPLIT_INSERT", 1, 0, 1) != 0;
+    // ... and their commit visits only the parents with winners (k_nzlist)
+    const bool nzlist = env_int("RMC_NZLIST", 1, 0, 1) != 0;
     // KParams.split of such chunks (measurement knob): 7 = verdicts in lslot for the commit, 3 = the
     // commit reads the election words itself
     const int split_flags = env_int("RMC_SPLIT_FLAGS", 7, 3, 7) == 3 ? 3 : 7;
@@ -2967,12 +3014,12 @@ struct rmc_ctx {
             s.hslot.reserve_to(c.trace_n);
             for (uint64_t j = 0; ok && j < c.trace_n;) {
                 const uint64_t k = std::min<uint64_t>(c.trace_n - j, HostArr<uint64_t>::B - j % HostArr<uint64_t>::B);
-                ok = std::fread(s.hpar.blk[j / HostArr<uint64_t>::B].p + j % HostArr<uint64_t>::B, 8, k, f) == k;
+                ok = std::fread(s.hpar.blk[j / HostArr<uint64_t>::B] + j % HostArr<uint64_t>::B, 8, k, f) == k;
                 j += k;
             }
             for (uint64_t j = 0; ok && j < c.trace_n;) {
                 const uint64_t k = std::min<uint64_t>(c.trace_n - j, HostArr<uint16_t>::B - j % HostArr<uint16_t>::B);
-                ok = std::fread(s.hslot.blk[j / HostArr<uint16_t>::B].p + j % HostArr<uint16_t>::B, 2, k, f) == k;
+                ok = std::fread(s.hslot.blk[j / HostArr<uint16_t>::B] + j % HostArr<uint16_t>::B, 2, k, f) == k;
                 j += k;
             }
             s.hpar.for_range(0, c.trace_n, [&](const uint64_t *p, uint64_t k) { sum.add(p, k * 8); });

@@ -69,6 +69,7 @@ struct HostLoop {
 constexpr uint32_t WTILE = 1024; // parents per tile of the winner-count scan
 constexpr uint32_t WTILES_MAX = 4096; // tiles per chunk (the last block scans four per thread)
 constexpr int SUM_WORDS = 7;     // chunk summary slot of the new states' record words
+constexpr int SUM_NZ = 16;       // ... and of the parents with winners (KParams::plist)
 
 // In device-loop mode the host sizes every grid on a bound of the level's parents (p_end -
 // p_begin of the KParams it passes); the kernels read the real range from the LevelCtl.
@@ -142,6 +143,10 @@ struct KParams {
     uint32_t *wposw;           // record words of the parent's winners, exclusive scan inside the tile
     uint32_t *bw, *bg, *boff;  // per tile: winners, successors generated, first winner's offset
     uint32_t *bww, *boffw;     // per tile: winners' record words, first winner's word offset
+    uint32_t *bn, *boffn;      // per tile: parents with winners, their exclusive scan (plist)
+    uint32_t *plist;           // split chunk: the chunk-local indices of the parents with winners, in
+                               // order (k_nzlist), sum[SUM_NZ] of them -- the commit's waves visit only
+                               // these; nullptr: every parent of the chunk
     uint32_t *tickets;         // [0] winner-count pass: last-block counter (0 between launches)
     uint32_t *ctick;           // commit pass: arrival counters (last_commit_block; 0 between launches)
     unsigned long long *sum;   // chunk summary {generated, winners, error keys[ERR_NSLOTS], flags, words}
@@ -187,6 +192,8 @@ void launch_init_level(uint32_t *ring, const uint32_t *rec, uint32_t words, uint
                        const ulonglong2 *fp, Seen seen, hipStream_t s);
 // out[i] = in[i] - sub (offset arrays rebased to a new level start)
 void launch_rebase(const uint64_t *in, uint64_t n, uint64_t sub, uint64_t *out, hipStream_t s);
+// after the winner count of a chunk with P.plist: the list of its parents with winners
+void launch_nzlist(const KParams &P, uint64_t np, hipStream_t s);
 
 // sharded round (W > 1), rmc_engine.hip step_sharded: a successor on its way to its fingerprint's
 // owner shard -- the fingerprint and its global key (parent's index in the level << 8 | rank)

@@ -2030,6 +2030,8 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
             P.wpos[pl] = x;
             P.wposw[pl] = xd;
         }
+        // parents with winners in the tile (for k_nzlist)
+        const uint32_t nt = P.plist ? (uint32_t)__syncthreads_count(w != 0u) : 0u;
         if (ntiles == 1) {  // one tile (small levels): its totals are the chunk's, no arrival round trips
             if (threadIdx.x == 0) {
                 P.boff[0] = 0u;
@@ -2037,6 +2039,11 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
                 P.sum[0] = gt;
                 P.sum[1] = wt;
                 P.sum[SUM_WORDS] = dt;
+                if (P.plist) {
+                    P.bn[0] = nt;
+                    P.boffn[0] = 0u;
+                    P.sum[SUM_NZ] = nt;
+                }
             }
             return;
         }
@@ -2045,6 +2052,7 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
             __hip_atomic_store(&P.bw[tile], wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&P.bg[tile], gt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(&P.bww[tile], dt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (P.plist) __hip_atomic_store(&P.bn[tile], nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     // arrivals: only the nb blocks that had a tile (MI355X guide: sc1 payload, drained, then an
@@ -2096,6 +2104,39 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
         P.sum[0] = gtot;
         P.sum[1] = wtot;
         P.sum[SUM_WORDS] = dtot;
+    }
+    if (P.plist) {  // parents with winners: tile offsets and the chunk's count
+        uint32_t nv[TPT], ns_ = 0, ntot;
+#pragma unroll
+        for (uint32_t k = 0; k < TPT; k++) {
+            const uint32_t tl = TPT * i + k;
+            nv[k] = tl < ntiles ? __hip_atomic_load(&P.bn[tl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            ns_ += nv[k];
+        }
+        uint32_t on = block_excl_scan(ns_, ws, &ntot);
+#pragma unroll
+        for (uint32_t k = 0; k < TPT; k++) {
+            const uint32_t tl = TPT * i + k;
+            if (tl < ntiles) P.boffn[tl] = on;
+            on += nv[k];
+        }
+        if (i == 0) P.sum[SUM_NZ] = ntot;
+    }
+}
+
+// The chunk-local indices of the parents with winners, in order (one 1024-thread block per tile of
+// the winner count: its parents' winner counts, scanned, at the tile's offset).  A split chunk's
+// commit visits only these: at Raft.cfg's wide levels most parents' successors are all seen.
+__global__ __launch_bounds__(1024) void k_nzlist(KParams P) {
+    __shared__ uint32_t ws[16];
+    const uint64_t np = P.p_end - P.p_begin;
+    const uint32_t ntiles = (uint32_t)((np + WTILE - 1) / WTILE);
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const uint64_t pl = (uint64_t)tile * WTILE + threadIdx.x;
+        const uint32_t w = pl < np ? P.wcnt[pl] : 0u;
+        uint32_t tot;
+        const uint32_t x = block_excl_scan(w ? 1u : 0u, ws, &tot);
+        if (w) P.plist[P.boffn[tile] + x] = (uint32_t)pl;
     }
 }
 
@@ -2233,24 +2274,38 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
         h.g0 = lane < MX ? P.lslot[pl * (uint64_t)MX + lane] : LS_SEEN;
         return h;
     };
+    // the parents this pass visits: k-th -> level-local index (a split chunk: only those with winners)
+    const uint64_t nvis = P.plist ? (uint64_t)P.sum[SUM_NZ] : P.p_end - P.p_begin;
+    auto parent_at = [&](uint64_t k) -> uint64_t { return P.p_begin + (P.plist ? (uint64_t)P.plist[k] : k); };
 #if RMC_COMMIT_PREFETCH
     // (RMC_COMMIT_PREFETCH 2: two headers ahead, so a run of parents without winners -- each only a
-    // header wait -- pays half a round trip per parent)
+    // header wait -- pays half a round trip per parent).  pq: the parents of k, k + grid, k + 2 grid
     Hdr nh{}, nnh{};
-    if (P.p_begin + blockIdx.x < P.p_end) nh = header(P.p_begin + blockIdx.x);
-    if (RMC_COMMIT_PREFETCH > 1 && P.p_begin + blockIdx.x + gridDim.x < P.p_end)
-        nnh = header(P.p_begin + blockIdx.x + gridDim.x);
+    uint64_t pq[3] = {0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+        if (blockIdx.x + (uint64_t)j * gridDim.x < nvis) pq[j] = parent_at(blockIdx.x + (uint64_t)j * gridDim.x);
+    if (blockIdx.x < nvis) nh = header(pq[0]);
+    if (RMC_COMMIT_PREFETCH > 1 && blockIdx.x + gridDim.x < nvis) nnh = header(pq[1]);
 #endif
     PHASE_DECL
-    for (uint64_t p = P.p_begin + blockIdx.x; p < P.p_end; p += gridDim.x) {
+    for (uint64_t k = blockIdx.x; k < nvis; k += gridDim.x) {
+#if RMC_COMMIT_PREFETCH
+        const uint64_t p = pq[0];
+        pq[0] = pq[1];
+        pq[1] = pq[2];
+        pq[2] = k + 3ull * gridDim.x < nvis ? parent_at(k + 3ull * gridDim.x) : 0ull;
+#else
+        const uint64_t p = parent_at(k);
+#endif
         const uint64_t pl = p - P.p_begin;
 #if RMC_COMMIT_PREFETCH > 1
         const Hdr h = nh;
         nh = nnh;
-        if (p + 2ull * gridDim.x < P.p_end) nnh = header(p + 2ull * gridDim.x);
+        if (k + 2ull * gridDim.x < nvis) nnh = header(pq[1]);
 #elif RMC_COMMIT_PREFETCH
         const Hdr h = nh;
-        if (p + gridDim.x < P.p_end) nh = header(p + gridDim.x);
+        if (k + gridDim.x < nvis) nh = header(pq[0]);
 #else
         const Hdr h = header(p);
 #endif
@@ -2536,6 +2591,10 @@ void launch_init_level(uint32_t *ring, const uint32_t *rec, uint32_t words, uint
 
 void launch_insert_fps(const ulonglong2 *fp, uint64_t n, Seen seen, hipStream_t s) {
     hipLaunchKernelGGL(k_insert, dim3(grid256(n)), dim3(256), 0, s, fp, n, seen);
+}
+void launch_nzlist(const KParams &P, uint64_t np, hipStream_t s) {
+    const uint64_t tiles = (np + WTILE - 1) / WTILE;
+    hipLaunchKernelGGL(k_nzlist, dim3(tiles ? (unsigned)tiles : 1u), dim3(1024), 0, s, P);
 }
 void launch_rebase(const uint64_t *in, uint64_t n, uint64_t sub, uint64_t *out, hipStream_t s) {
     if (n) hipLaunchKernelGGL(k_rebase, dim3(grid256(n)), dim3(256), 0, s, in, n, sub, out);

@@ -431,7 +431,7 @@ int main(int argc, char **argv) {
     std::printf("Finished in %.2fs at (%s)\n", el, now_str().c_str());
     std::printf("GPU: %.0f distinct states/s over %.3f s of BFS levels (MI355X, 1 device).\n",
                 gpu_seconds > 0 ? res.distinct / gpu_seconds : 0.0, gpu_seconds);
-    // The process ends here: by default the device and pinned host memory (~250 GB and ~110 GB of
+    // The process ends here: by default the device and host memory (~250 GB and ~110 GB of
     // trace at Raft.cfg) go back with the process instead of through rmc_destroy, whose frees took
     // ~16 s after a Raft.cfg exhaustion (RMC_FAST_EXIT=0 destroys the context first).
     std::fflush(stdout);
