@@ -281,6 +281,26 @@ def test_split_probe_chunks_match_golden_levels(name, monkeypatch):
     mc.close()
 
 
+@pytest.mark.parametrize("mode", ["virtual2", "rccl1"])
+@pytest.mark.parametrize("name", sorted(LEVELS))
+def test_sharded_commit_list_matches_golden_levels(name, mode, monkeypatch):
+    """Sharded rounds whose commit visits only the parents with winners (k_nzlist; RMC_SPLIT_MIN=1
+    turns it on for every round): levels, counters at an error and traces as the golden run."""
+    monkeypatch.setenv("RMC_SPLIT_MIN", "1")
+    g = LEVELS[name]
+    if mode == "virtual2":
+        kw = dict(virtual_shards=2, chunk_successors=3000, shard_min_states=1)
+    else:
+        kw = dict(world_size=1, rank=0, comm_unique_id=raftmc.comm_unique_id(), chunk_successors=3000,
+                  shard_min_states=1)
+    mc, res = run_cfg(g, **kw)
+    check_levels(g, res)
+    if name in TRACES:
+        assert [(list(k) if k else None, st) for k, st in mc.trace()] == \
+               [(e["key"], e["state"]) for e in TRACES[name]["steps"]]
+    mc.close()
+
+
 @pytest.mark.parametrize("name", sorted(LEVELS_BIG))
 def test_bfs_matches_golden_levels_at_scale(name):
     """bench.py's at-scale workload (10^7 states) against the C oracle's full BFS, level by level."""

@@ -2151,6 +2151,10 @@ struct rmc_ctx {
         Q.next_base = 0;
         Q.xside = s.oside;
         Q.gid_next_base = 0;
+        // a round of many parents: the commit visits only those with winners (k_nzlist, as a split
+        // chunk of the single-GPU path; same switches)
+        const uint64_t split_min = (uint64_t)env_int("RMC_SPLIT_MIN", 1 << 16, 0, 1 << 30);
+        if (split_min && s.np >= split_min && env_int("RMC_NZLIST", 1, 0, 1)) Q.plist = s.plist;
         Q.trace_base = 0;
         return Q;
     }
@@ -2374,7 +2378,9 @@ struct rmc_ctx {
                 timed(PH_DEDUP, [&] {
                     launch_scatter_win(s.perm, s.sflag, s.G, s.score, (uint32_t)sw4(), s.pnm, (uint32_t)MS, s.lslot,
                                        s.wacc, stream);
-                    ks.wincount(round_params(s, gbase), s.np, stream);
+                    const KParams Q = round_params(s, gbase);
+                    ks.wincount(Q, s.np, stream);
+                    if (Q.plist) launch_nzlist(Q, s.np, stream);
                 });
             }
             SDBG("5");

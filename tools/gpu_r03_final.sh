@@ -10,6 +10,9 @@ O=gpurun_out/final
 mkdir -p $O
 export TMPDIR=/tmp
 step() { echo "== $1 ($(date +%T))"; }
+step tests_commit_list
+timeout -k 10 300 python -u -m pytest tests/ -m gpu -x -q --timeout 120 --timeout-method thread -k commit_list > $O/gpu_tests_commit_list.log 2>&1 || { tail -20 $O/gpu_tests_commit_list.log; exit 1; }
+tail -1 $O/gpu_tests_commit_list.log
 step smoke
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
