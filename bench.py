@@ -585,7 +585,7 @@ def cpu_baseline_at_scale(device, workload="raftcfg", max_states=20_000_000):
 
 def at_scale(device, workload="raftcfg", probes_per_s=None):
     """configs[0]/[2] -- Raft.cfg as shipped -- exhausted on this GPU (not the headline: one run is
-    ~75 s).  The first run includes growing every buffer (the seen set's move to 8-B slots, the
+    ~46 s).  The first run includes growing every buffer (the seen set's move to 8-B slots, the
     frontier ring, the host trace); the second, after rmc_reset, is the steady state.  Its
     first 34 levels are compared with the C oracle's (tests/golden/levels_prefix.json)."""
     import raftmc
