@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RMC_ABI_VERSION 3
+#define RMC_ABI_VERSION 4
 
 /* ---- return codes ---------------------------------------------------------- */
 #define RMC_OK 0
@@ -89,7 +89,8 @@ typedef struct rmc_config {
     /* multi-GPU (one process per GPU): world_size 0 or 1 = single GPU */
     int32_t rank, world_size;  /* world_size 0 or 1 = single GPU; world_size 1 WITH comm_unique_id = a one-rank
                                   RCCL communicator running the sharded protocol (self send/recv) */
-    const void *comm_unique_id; /* 128-byte RCCL unique id (rmc_comm_unique_id on rank 0), same on every rank */
+    const void *comm_unique_id; /* 128-byte RCCL unique id (rmc_comm_unique_id on rank 0), same on every rank;
+                                  NULL with world_size > 1: the host-staged transport (rmc_set_transport) */
     int32_t virtual_shards;    /* > 1: run that many fingerprint-owner shards in this process on one device
                                   (the multi-GPU partition/exchange logic with device copies for transport) */
     uint32_t timing_phases;    /* bit i: HIP-event time phase i into rmc_level_stats.kernel_ms (0 = all) */
@@ -151,6 +152,26 @@ int rmc_abi_version(void);
  * rank, pass as rmc_config.comm_unique_id).  Replaces nothing in the reference: TLC runs
  * in one JVM; this is the seen-set sharding of SURVEY.md 8(e). */
 int rmc_comm_unique_id(void *out128);
+
+/* ABI 4: a host-staged transport for the sharded protocol (world_size > 1 without comm_unique_id).
+ * The ranks' collectives go through these callbacks instead of RCCL: every rank of the run installs
+ * one (process-wide, before rmc_create; NULL removes it) whose calls meet their peers' -- e.g. a
+ * torch.distributed gloo group (raftmc.HostTransport).  It carries the same protocol as RCCL through
+ * host memory, so the multi-rank path runs as separate processes on one device (tests) or on hosts
+ * without a GPU interconnect.  Each callback returns 0 on success; anything else fails the step with
+ * RMC_E_COMM.
+ *   allreduce_u64  v[0..n) <- the elementwise sum (is_max = 0) or maximum over the ranks, in place
+ *   allgather_u64  out[0..W*k) <- every rank's row[0..k), in rank order
+ *   alltoallv      bytes send + send_off[p] .. + send_bytes[p] go to rank p, bytes from rank p land at
+ *                  recv + recv_off[p] (recv_bytes[p] of them); the caller's own entries are 0 */
+typedef struct rmc_transport {
+    void *user;
+    int32_t (*allreduce_u64)(void *user, uint64_t *v, int32_t n, int32_t is_max);
+    int32_t (*allgather_u64)(void *user, const uint64_t *row, int32_t k, uint64_t *out);
+    int32_t (*alltoallv)(void *user, const void *send, const uint64_t *send_off, const uint64_t *send_bytes,
+                         void *recv, const uint64_t *recv_off, const uint64_t *recv_bytes);
+} rmc_transport;
+int rmc_set_transport(const rmc_transport *t);
 
 /* Parse Raft.cfg text (replaces TLC's ModelConfig for the subset Raft.cfg uses,
  * Raft.cfg:1-34) and validate Raft.tla text by content (replaces SANY; only
@@ -232,6 +253,15 @@ void rmc_destroy(void *ctx);
 int rmc_successors(void *ctx, const int32_t *unpacked, int32_t *out, size_t stride_ints, uint32_t cap,
                    uint32_t *keys, uint64_t *fps, uint32_t *count);
 int rmc_fingerprint(void *ctx, const int32_t *unpacked, uint64_t fp[2]);
+/* ABI 4 -- checks of a finished run's deep levels (tests/test_gpu_deep.py).  The path of the explored
+ * state with global id `gid` (BFS order, Init = 0): len = its depth, keys[i] = how state i of the path
+ * was reached from state i - 1 (rmc_successors' key format; keys[0] = 0), gids[i] = its global id
+ * (gids[0] = 0, gids[len - 1] = gid); from TLC's parent pointers (the trace), any shard layout. */
+int rmc_state_path(void *ctx, uint64_t gid, uint32_t *keys, uint64_t *gids, uint32_t cap, uint32_t *len);
+/* Fingerprints of n unpacked states, stride_ints apart (2 words each), in one launch. */
+int rmc_fingerprints(void *ctx, const int32_t *unpacked, size_t stride_ints, uint64_t n, uint64_t *fps);
+/* Seen-set membership (TLC's FPSet) of n fingerprints: out[i] = 1 if present.  Not for RCCL ranks. */
+int rmc_seen_contains(void *ctx, const uint64_t *fps, uint64_t n, uint8_t *out);
 /* 1 = TRUE, 0 = FALSE, RMC_EVAL_ERROR; one invariant bit */
 int rmc_eval_invariant(void *ctx, const int32_t *unpacked, uint32_t invariant_bit, int32_t *value);
 

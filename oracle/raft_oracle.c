@@ -907,6 +907,36 @@ out:
     return ret ? ret : cnt;
 }
 
+/* Replay a path: from the unpacked state `in`, take at each step the successor whose key (as
+ * orc_successors) is keys[i]; the final state goes to `out`.  Returns its unpacked length, or
+ * -(i + 1) when keys[i] is not enabled (or the Assert fails) at step i, -1000000 on capacity. */
+int orc_replay(int n, int V, int E, int R, int seeded, const int32_t *in, const uint32_t *keys, int nkeys,
+               int32_t *out, int cap_ints) {
+    ocfg_t c = {n, V, E, R, 0, 0, 1, 0, 0, 0, 0, 0, 0};
+    set_variant(&c, seeded);
+    st_t *st = (st_t *)malloc(sizeof(st_t));
+    batch_t b; b.buf = (st_t *)malloc(sizeof(st_t) * BATCH_CAP); b.w = (int32_t *)malloc(sizeof(int32_t) * BATCH_CAP); b.cap = BATCH_CAP;
+    int ret = 0;
+    if (pack_from(&c, in, st) < 0) { ret = -1000000; goto out; }
+    for (int i = 0; i < nkeys && ret == 0; i++) {
+        const int s = (int)(keys[i] >> 24), a = (int)((keys[i] >> 16) & 0xFF), w = (int)(keys[i] & 0xFFFF);
+        if (s >= n || (a == A_BF && !c.bf)) { ret = -(i + 1); break; }
+        b.n = 0; b.assert_fail = 0;
+        gen_action(&c, st, s, a, &b);
+        int j = 0;
+        while (j < b.n && b.w[j] != w) j++;
+        if (b.assert_fail || j == b.n) { ret = -(i + 1); break; }
+        copy_state(st, &b.buf[j]);
+    }
+    if (ret == 0) {
+        ret = unpack_to(&c, st, out, cap_ints);
+        if (ret < 0) ret = -1000000;
+    }
+out:
+    free(st); free(b.buf); free(b.w);
+    return ret;
+}
+
 int orc_canon_hash(int n, int V, const int32_t *in, uint64_t *out2) {
     ocfg_t c = {n, V, 7, 7, 0, 0, 1, 0, 0, 0, 0, 0, 0};
     perms_t *P = (perms_t *)malloc(sizeof(perms_t));

@@ -382,6 +382,7 @@ struct Shard {
     uint64_t *par = nullptr;
     uint16_t *pslot = nullptr;
     uint64_t trace_cap = 0, tflushed = 0;
+    uint64_t trace_end = 0;  // gids with device trace entries (a finished run's last levels stay on the device)
     uint64_t tdev = 0;  // gid of device trace index 0 (set to tflushed when a kernel sequence starts)
     HostArr<uint64_t> hpar;
     HostArr<uint16_t> hslot;
@@ -401,6 +402,7 @@ struct Shard {
     uint32_t *wcnt = nullptr, *wacc = nullptr, *pnm = nullptr, *wposw = nullptr, *ctick = nullptr;
     uint32_t *bw = nullptr, *bg = nullptr, *boff = nullptr, *bww = nullptr, *boffw = nullptr, *tickets = nullptr;
     uint32_t *bn = nullptr, *boffn = nullptr, *plist = nullptr;  // parents with winners (split chunks)
+    uint32_t *hctx = nullptr;  // split chunks: each parent's hash context (KernelSet::ctxw words)
     // device-driven level loop: control block, per-level records, and their pinned host copies
     LevelCtl *ctl = nullptr, *hctl = nullptr;
     HostLoop *hloop = nullptr, *dloop = nullptr;  // device-loop mirror in mapped pinned memory (host / device view)
@@ -432,6 +434,10 @@ struct Shard {
     uint64_t p0 = 0, np = 0, G = 0, gblk = 0;
 };
 
+// the host-staged transport installed by rmc_set_transport (process-wide; read by rmc_create)
+static rmc_transport g_transport{};
+static bool g_transport_set = false;
+
 struct rmc_ctx {
     rmc_config cfg{};
     KernelSet ks{};
@@ -447,6 +453,8 @@ struct rmc_ctx {
     bool virt = false;    // all W shards live in this process
     bool multi = false;   // the sharded protocol runs (W > 1, or one RCCL rank talking to itself)
     bool rccl = false;    // shards exchange through an RCCL communicator (not device copies)
+    bool hostx = false;   // ... through the host-staged transport (rmc_set_transport)
+    rmc_transport tx{};
 #ifdef RMC_WITH_RCCL
     ncclComm_t comm = nullptr;
 #endif
@@ -460,7 +468,6 @@ struct rmc_ctx {
     uint32_t *d_info = nullptr;
     uint16_t *d_nat2id = nullptr;
     ulonglong2 *d_gmsg = nullptr;
-    uint8_t *d_perms = nullptr;
     uint64_t *d_seeds = nullptr;
     int np = 0;
     uint64_t scheme_hash = 0;  // identifies the fingerprint scheme (seeds, message hashes): checkpoints
@@ -517,7 +524,6 @@ struct rmc_ctx {
         P.t.info = d_info;
         P.t.nat2id = d_nat2id;
         P.t.gmsg = d_gmsg;
-        P.t.perms = d_perms;
         P.t.seeds = d_seeds;
         P.t.np = np;
         P.t.bmw = (uint32_t)((U.info.size() + 31) / 32);
@@ -550,7 +556,7 @@ struct rmc_ctx {
         Q.wposw = s.wposw; Q.bw = s.bw; Q.bg = s.bg; Q.boff = s.boff; Q.bww = s.bww; Q.boffw = s.boffw;
         Q.bn = s.bn; Q.boffn = s.boffn;
         Q.tickets = s.tickets; Q.ctick = s.ctick; Q.sum = s.sum;
-        Q.score = s.score; Q.lslot = s.lslot; Q.L = s.L; Q.LXY = s.LXY;
+        Q.score = s.score; Q.lslot = s.lslot; Q.L = s.L; Q.LXY = s.LXY; Q.hctx = s.hctx;
         return Q;
     }
 
@@ -750,8 +756,10 @@ struct rmc_ctx {
         // world_size == 1 with a unique id: a one-rank communicator; the sharded protocol then
         // runs through RCCL (self send/recv, one-rank all-reduce/all-to-all) -- its transport
         // exercised on a one-GPU machine
-        rccl = !virt && (ws > 1 || (cfg.world_size == 1 && cfg.comm_unique_id));
+        hostx = !virt && ws > 1 && !cfg.comm_unique_id && g_transport_set;
+        rccl = !virt && !hostx && (ws > 1 || (cfg.world_size == 1 && cfg.comm_unique_id));
         multi = W > 1 || rccl;
+        if (hostx) tx = g_transport;
         if (rank < 0 || rank >= W) throw Fail(RMC_E_ARG, "rank out of range");
         N = cfg.n_servers;
         V = cfg.n_vals;
@@ -792,7 +800,8 @@ struct rmc_ctx {
         stager.reset(new TraceStager());
         if (rccl) {
 #ifdef RMC_WITH_RCCL
-            if (!cfg.comm_unique_id) throw Fail(RMC_E_ARG, "world_size > 1 needs comm_unique_id (rmc_comm_unique_id)");
+            if (!cfg.comm_unique_id)
+                throw Fail(RMC_E_ARG, "world_size > 1 needs comm_unique_id (rmc_comm_unique_id) or a transport (rmc_set_transport)");
             ncclUniqueId id;
             std::memcpy(&id, cfg.comm_unique_id, sizeof id);
             if (ncclCommInitRank(&comm, W, id, rank) != ncclSuccess) throw Fail(RMC_E_COMM, "ncclCommInitRank failed");
@@ -809,28 +818,20 @@ struct rmc_ctx {
         HIPCHK(hipMemcpy(d_nat2id, U.nat2id.data(), U.nat2id.size() * 2, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(d_gmsg, U.gmsg.data(), U.gmsg.size() * 16, hipMemcpyHostToDevice));
 
-        // Permutations(Servers) (tla:21), or the identity without SYMMETRY
-        std::vector<uint8_t> perms;
-        std::vector<int> a(N);
-        for (int i = 0; i < N; i++) a[i] = i;
-        do {
-            for (int i = 0; i < MAXN; i++) perms.push_back(i < N ? (uint8_t)a[i] : 0);
-        } while (!cfg.no_symmetry && std::next_permutation(a.begin(), a.end()));
-        np = (int)(perms.size() / MAXN);
-        d_perms = dmalloc<uint8_t>(perms.size());
-        HIPCHK(hipMemcpy(d_perms, perms.data(), perms.size(), hipMemcpyHostToDevice));
-        std::vector<uint64_t> seeds(2 * (MAXN + MAXN * MAXN));
-        uint64_t x = SEED_SERVER;
-        for (int i = 0; i < MAXN; i++) { seeds[i] = splitmix(x); seeds[MAXN + MAXN * MAXN + i] = splitmix(x); }
-        x = SEED_PAIR;
-        for (int i = 0; i < MAXN * MAXN; i++) {
-            seeds[MAXN + i] = splitmix(x);
-            seeds[2 * MAXN + MAXN * MAXN + i] = splitmix(x);
-        }
+        // |Permutations(Servers)| (tla:21); 1 without SYMMETRY (the fingerprint's coset is the identity)
+        np = 1;
+        if (!cfg.no_symmetry)
+            for (int i = 2; i <= N; i++) np *= i;
+        // position constants K_f[a][b] of the fingerprint (rmc_spec.h), odd
+        std::vector<uint64_t> seeds(2 * SEEDS_PER_F);
+        uint64_t x = SEED_PAIR;
+        for (uint64_t &v : seeds) v = splitmix(x) | 1ull;
         d_seeds = dmalloc<uint64_t>(seeds.size());
         HIPCHK(hipMemcpy(d_seeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
         // fingerprint scheme identity (checkpoints): seeds, message hashes, record codec, slot hash
-        scheme_hash = 0x5eed5c4e3e000006ull;  // 4: signature-coset minimum for n >= 4; 5: positional slot keys; 6: codec of (N, V)
+        // (4: signature-coset minimum for n >= 4; 5: positional slot keys; 6: codec of (N, V); 7: content
+        // matrix x position constants, signature coset for every n)
+        scheme_hash = 0x5eed5c4e3e000007ull;
         auto mixin = [&](uint64_t v) { scheme_hash = mix64(scheme_hash ^ (v + 0x9e3779b97f4a7c15ull)); };
         for (uint64_t s : seeds) mixin(s);
         for (const ulonglong2 &g : U.gmsg) { mixin(g.x); mixin(g.y); }
@@ -886,6 +887,13 @@ struct rmc_ctx {
         s.fp = dmalloc<ulonglong2>(g);
         s.lslot = dmalloc<uint32_t>(g);
         s.score = dmalloc<uint4>(g * (uint64_t)sw4());
+        // chunks of split_min parents or more are split (M_SPLIT + k_hash_probe): their parents' hash contexts
+        const uint64_t hp = g / (uint64_t)ks.maxsucc + 1;
+        if (split_min && hp >= split_min) {
+            dfree(s.hctx);
+            s.hctx = nullptr;
+            s.hctx = dmalloc<uint32_t>(hp * (uint64_t)ks.ctxw);
+        }
         s.gslots = g;
         if (lc > s.lcap) {
             dfree(s.L); dfree(s.LXY);
@@ -967,7 +975,7 @@ struct rmc_ctx {
         dfree(s.err); dfree(s.sum); dfree(s.flags);
         dfree(s.score); dfree(s.wcnt); dfree(s.wacc); dfree(s.pnm); dfree(s.wposw); dfree(s.ctick);
         dfree(s.bw); dfree(s.bg); dfree(s.boff); dfree(s.bww); dfree(s.boffw); dfree(s.tickets);
-        dfree(s.bn); dfree(s.boffn); dfree(s.plist);
+        dfree(s.bn); dfree(s.boffn); dfree(s.plist); dfree(s.hctx);
         dfree(s.ctl); dfree(s.lrec);
         if (s.hsum) (void)hipHostFree(s.hsum);
         if (s.hctl) (void)hipHostFree(s.hctl);
@@ -986,7 +994,7 @@ struct rmc_ctx {
         stager.reset();  // (its thread finishes the pieces already copied: before the blocks go)
         for (Shard &s : sh) free_shard(s);
         sh.clear();
-        dfree(d_info); dfree(d_nat2id); dfree(d_gmsg); dfree(d_perms); dfree(d_seeds);
+        dfree(d_info); dfree(d_nat2id); dfree(d_gmsg); dfree(d_seeds);
         dfree(d_one); dfree(d_init_rec); dfree(d_init_fp); dfree(d_out); dfree(d_keys); dfree(d_cnt1); dfree(d_fp1); dfree(d_inv); dfree(d_err1);
         dfree(d_flags1); dfree(d_red);
         if (h_red) (void)hipHostFree(h_red);
@@ -1281,6 +1289,10 @@ struct rmc_ctx {
     // Every host value handed to these is this process's contribution (virtual mode: the
     // sum/max over all local shards already IS the global value).
     void allreduce(uint64_t *v, int n, bool is_max) {
+        if (hostx) {
+            if (tx.allreduce_u64(tx.user, v, n, is_max ? 1 : 0) != 0) throw Fail(RMC_E_COMM, "transport allreduce failed");
+            return;
+        }
         if (!rccl) return;
 #ifdef RMC_WITH_RCCL
         for (int i = 0; i < n; i++) h_red[i] = v[i];
@@ -1297,6 +1309,10 @@ struct rmc_ctx {
     // (row t = shard t) out.  One ncclAllGather through RCCL; virtual shards are all local.
     std::vector<uint64_t> gather_rows(const std::vector<std::vector<uint64_t>> &rows, int K) {
         std::vector<uint64_t> M((size_t)W * K, 0);
+        if (hostx) {
+            if (tx.allgather_u64(tx.user, rows[0].data(), K, M.data()) != 0) throw Fail(RMC_E_COMM, "transport allgather failed");
+            return M;
+        }
         if (!rccl) {
             for (size_t li = 0; li < sh.size(); li++)
                 std::copy(rows[li].begin(), rows[li].end(), M.begin() + (size_t)sh[li].id * K);
@@ -1329,8 +1345,48 @@ struct rmc_ctx {
         size_t elem;
         bool self_in_place = false;  // a shard's items to itself are already in its receive buffer
     };
+    // The host-staged transport: a rank's part for itself is a device copy (or nothing), every peer's
+    // part of every payload goes to host memory in one packed buffer, the transport's
+    // all-to-all-v moves the bytes, and the received parts go back to the device.
+    std::vector<char> hx_send, hx_recv;
+    void exchange_host(const std::vector<Payload> &P) {
+        for (const Payload &p : P) {
+            const XPlan &x = (*p.plans)[0];
+            const uint64_t own = x.send_cnt[rank];
+            if (own && !p.self_in_place)
+                HIPCHK(hipMemcpyAsync((char *)p.recv[0] + x.recv_off[rank] * p.elem,
+                                      (const char *)p.send[0] + x.send_off[rank] * p.elem, own * p.elem,
+                                      hipMemcpyDeviceToDevice, stream));
+            std::vector<uint64_t> so(W, 0), sb(W, 0), ro(W, 0), rb(W, 0);
+            uint64_t ts = 0, tr = 0;
+            for (int q = 0; q < W; q++) {
+                if (q == rank) continue;
+                so[q] = ts; sb[q] = x.send_cnt[q] * p.elem; ts += sb[q];
+                ro[q] = tr; rb[q] = x.recv_cnt[q] * p.elem; tr += rb[q];
+            }
+            hx_send.resize(std::max<size_t>(ts, 1));
+            hx_recv.resize(std::max<size_t>(tr, 1));
+            for (int q = 0; q < W; q++)
+                if (sb[q])
+                    HIPCHK(hipMemcpyAsync(hx_send.data() + so[q], (const char *)p.send[0] + x.send_off[q] * p.elem, sb[q],
+                                          hipMemcpyDeviceToHost, stream));
+            HIPCHK(hipStreamSynchronize(stream));
+            if (tx.alltoallv(tx.user, hx_send.data(), so.data(), sb.data(), hx_recv.data(), ro.data(), rb.data()) != 0)
+                throw Fail(RMC_E_COMM, "transport alltoallv failed");
+            for (int q = 0; q < W; q++)
+                if (rb[q])
+                    HIPCHK(hipMemcpyAsync((char *)p.recv[0] + x.recv_off[q] * p.elem, hx_recv.data() + ro[q], rb[q],
+                                          hipMemcpyHostToDevice, stream));
+            HIPCHK(hipStreamSynchronize(stream));
+        }
+    }
+
     // A shard's part for itself never goes through RCCL: a device copy (or nothing, self_in_place).
     void exchange(const std::vector<Payload> &P) {
+        if (hostx) {
+            exchange_host(P);
+            return;
+        }
         if (!rccl) {
             for (const Payload &p : P)
                 for (const Xfer &x : transfers(*p.plans))
@@ -1754,9 +1810,13 @@ struct rmc_ctx {
                 Q.plist = split && nzlist ? s.plist : nullptr;
                 return Q;
             };
-            // expand + fingerprint + seen-set probe + staging, one evaluation per parent
-            timed(PH_HASH, [&] { ks.fused(params(), stream); });
-            if (split) timed(PH_OTHER, [&] { ks.probe(params(), np_, stream); });
+            // expand + fingerprint + seen-set probe + staging, one evaluation per parent (a split
+            // chunk: expand + staging + hash context, then fingerprint + probe + election a lane per successor)
+            timed(PH_HASH, [&] {
+                if (split) ks.split(params(), stream);
+                else ks.fused(params(), stream);
+            });
+            if (split) timed(PH_OTHER, [&] { ks.hash_probe(params(), np_, stream); });
             timed(PH_DEDUP, [&] {
                 ks.wincount(params(), np_, stream);
                 if (split && nzlist) launch_nzlist(params(), np_, stream);
@@ -2024,8 +2084,9 @@ struct rmc_ctx {
         s.epoch = c.epoch;
         s.peak_words = std::max(s.peak_words, s.cur_words);
         if (s.T_count != c.T_count) throw Fail(RMC_E_STATE, "device level loop: seen-set count mismatch");
-        // a run that ended without an error never reads its trace (no counterexample): no flush
-        if (!(finished && status == RMC_DONE)) flush_trace(s, c.gid_cur + c.cur_n);
+        // a run that ended without an error reads its trace only for rmc_state_path: no flush now
+        s.trace_end = c.gid_cur + c.cur_n;
+        if (!(finished && status == RMC_DONE)) flush_trace(s, s.trace_end);
         seconds += el;
         if (c.stop == CTL_ERROR) {
             // the level the loop stopped in is intact: report its error as the host path does
@@ -2153,7 +2214,6 @@ struct rmc_ctx {
         Q.gid_next_base = 0;
         // a round of many parents: the commit visits only those with winners (k_nzlist, as a split
         // chunk of the single-GPU path; same switches)
-        const uint64_t split_min = (uint64_t)env_int("RMC_SPLIT_MIN", 1 << 16, 0, 1 << 30);
         if (split_min && s.np >= split_min && env_int("RMC_NZLIST", 1, 0, 1)) Q.plist = s.plist;
         Q.trace_base = 0;
         return Q;
@@ -2278,7 +2338,15 @@ struct rmc_ctx {
                 HIPCHK(hipMemsetAsync(s.ocnt, 0, 64 * 4, stream));
                 HIPCHK(hipMemsetAsync(s.sum + 9, 0, 8, stream));
                 if (!s.np || fail[li]) continue;
-                timed(PH_HASH, [&] { ks.fused(round_params(s, gbase), stream); });
+                timed(PH_HASH, [&] {
+                    const KParams Q = round_params(s, gbase);
+                    if (split_min && s.np >= split_min) {  // fingerprints a lane per successor (route: no probe)
+                        ks.split(Q, stream);
+                        ks.hash_probe(Q, s.np, stream);
+                    } else {
+                        ks.fused(Q, stream);
+                    }
+                });
                 launch_route_count(s.fp, s.cnt, s.np, (uint32_t)MS, (uint32_t)W, s.ocnt, stream);
             }
             // gathered row per shard: its successors per owner, its receive capacity, its failure
@@ -2726,12 +2794,15 @@ struct rmc_ctx {
     }
 
     // Walk parent pointers from err_ref to Init, then replay the slots from Init.
-    void build_trace() {
+    // The slot keys from Init down to the state with global id g (and, with gids, the global ids of
+    // the states on the path, Init's 0 first).
+    std::vector<uint16_t> path_slots(uint64_t g, std::vector<uint64_t> *gids) {
+        // (a run that ended without an error left its last device-loop levels' entries on the device)
+        for (Shard &s : sh) flush_trace(s, s.trace_end);
         sync_trace();
         HIPCHK(hipStreamSynchronize(stream));  // pending trace copies
         std::vector<uint16_t> slots;
-        if (err_last_slot != KEY_NONE) slots.push_back((uint16_t)err_last_slot);
-        uint64_t g = err_ref;
+        if (gids) gids->assign(1, g);
         for (;;) {
             uint64_t par;
             uint16_t sl;
@@ -2739,9 +2810,17 @@ struct rmc_ctx {
             if (par == ~0ull) break;
             slots.push_back(sl);
             g = par;
+            if (gids) gids->push_back(g);
             if (slots.size() > 100000) throw Fail(RMC_E_STATE, "corrupt parent chain");
         }
         std::reverse(slots.begin(), slots.end());
+        if (gids) std::reverse(gids->begin(), gids->end());
+        return slots;
+    }
+
+    void build_trace() {
+        std::vector<uint16_t> slots = path_slots(err_ref, nullptr);
+        if (err_last_slot != KEY_NONE) slots.push_back((uint16_t)err_last_slot);
         trace.clear();
         std::vector<uint32_t> rec = init_record();
         trace.push_back({unpack(rec.data()), -1, -1, -1});
@@ -2829,7 +2908,7 @@ struct rmc_ctx {
         }
     };
     std::string ckpt_path(const char *path) const {
-        return (rccl && W > 1) ? std::string(path) + ".rank" + std::to_string(rank) : std::string(path);
+        return ((rccl || hostx) && W > 1) ? std::string(path) + ".rank" + std::to_string(rank) : std::string(path);
     }
 
     // device <-> file in bounded pieces through one host buffer
@@ -3040,7 +3119,7 @@ struct rmc_ctx {
             Shard &s = sh[i];
             const CkptShard &c = sc[i];
             s.hpar.n = s.hslot.n = c.trace_n;
-            s.tflushed = s.tdev = c.trace_n;
+            s.tflushed = s.tdev = s.trace_end = c.trace_n;
             s.level_start = lss[i];
             s.cur_n = c.cur_n;
             s.nxt_n = 0;
@@ -3081,7 +3160,7 @@ struct rmc_ctx {
             s.T_count = 0;
             s.cur_n = s.nxt_n = 0;
             s.cur_wbase = s.cur_words = s.nxt_words = 0;
-            s.tflushed = 0;
+            s.tflushed = s.trace_end = 0;
             s.hpar.n = s.hslot.n = 0;
             s.level_start.clear();
         }
@@ -3142,13 +3221,20 @@ extern "C" {
 
 int rmc_abi_version(void) { return RMC_ABI_VERSION; }
 
+int rmc_set_transport(const rmc_transport *t) {
+    if (t && (!t->allreduce_u64 || !t->allgather_u64 || !t->alltoallv)) return RMC_E_ARG;
+    g_transport_set = t != nullptr;
+    g_transport = t ? *t : rmc_transport{};
+    return RMC_OK;
+}
+
 int rmc_comm_unique_id(void *out128) {
     if (!out128) return RMC_E_ARG;
 #ifdef RMC_WITH_RCCL
     ncclUniqueId id;
     if (ncclGetUniqueId(&id) != ncclSuccess) return RMC_E_COMM;
     static_assert(sizeof(id) <= 128, "ncclUniqueId larger than 128 bytes");
-    static_assert(sizeof(rmc_config) == 120, "rmc_config layout (ABI 3) changed: update INTEGRATION.md and raftmc");
+    static_assert(sizeof(rmc_config) == 120, "rmc_config layout (ABI 3/4) changed: update INTEGRATION.md and raftmc");
     std::memset(out128, 0, 128);
     std::memcpy(out128, &id, sizeof id);
     return RMC_OK;
@@ -3368,6 +3454,81 @@ int rmc_fingerprint(void *ctx, const int32_t *unpacked, uint64_t fp[2]) {
         ulonglong2 f = c->d2h(c->d_fp1);
         fp[0] = f.x;
         fp[1] = f.y;
+        return RMC_OK;
+    });
+}
+
+int rmc_state_path(void *ctx, uint64_t gid, uint32_t *keys, uint64_t *gids, uint32_t cap, uint32_t *len) {
+    rmc_ctx *c = (rmc_ctx *)ctx;
+    return guarded(c, [&] {
+        if (!c->inited) throw Fail(RMC_E_STATE, "state_path: no run");
+        if (gid >= c->total_distinct) throw Fail(RMC_E_ARG, "state_path: no state with that id");
+        std::vector<uint64_t> g;
+        const std::vector<uint16_t> sl = c->path_slots(gid, &g);
+        if (len) *len = (uint32_t)g.size();
+        if (g.size() > cap) throw Fail(RMC_E_ARG, "state_path: buffer too small");
+        for (size_t i = 0; i < g.size(); i++) {
+            if (gids) gids[i] = g[i];
+            if (keys) {
+                const uint32_t k = i ? sl[i - 1] : 0u;
+                keys[i] = i ? (key_server(k) << 24) | (key_action(k) << 16) | key_witness(k) : 0u;
+            }
+        }
+        return RMC_OK;
+    });
+}
+
+int rmc_fingerprints(void *ctx, const int32_t *unpacked, size_t stride, uint64_t n, uint64_t *fps) {
+    rmc_ctx *c = (rmc_ctx *)ctx;
+    return guarded(c, [&] {
+        if (!unpacked || !fps) throw Fail(RMC_E_ARG, "fingerprints: null buffer");
+        std::vector<uint32_t> rec((size_t)c->RECW * (n ? n : 1), 0u);
+        for (uint64_t i = 0; i < n; i++) c->pack(unpacked + i * stride, rec.data() + i * c->RECW);
+        uint32_t *d_rec = dmalloc<uint32_t>(rec.size());
+        ulonglong2 *d_fp = dmalloc<ulonglong2>(n ? n : 1);
+        try {
+            HIPCHK(hipMemcpy(d_rec, rec.data(), rec.size() * 4, hipMemcpyHostToDevice));
+            KParams P = c->base(c->sh[0]);
+            P.front = d_rec;
+            P.fp = d_fp;
+            if (n) c->ks.fp_states(P, n, c->stream);
+            HIPCHK(hipMemcpyAsync(fps, d_fp, n * 16, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+        } catch (...) {
+            dfree(d_rec);
+            dfree(d_fp);
+            throw;
+        }
+        dfree(d_rec);
+        dfree(d_fp);
+        return RMC_OK;
+    });
+}
+
+int rmc_seen_contains(void *ctx, const uint64_t *fps, uint64_t n, uint8_t *out) {
+    rmc_ctx *c = (rmc_ctx *)ctx;
+    return guarded(c, [&] {
+        if (!fps || !out) throw Fail(RMC_E_ARG, "seen_contains: null buffer");
+        if (c->rccl || c->hostx) throw Fail(RMC_E_STATE, "seen_contains: the seen set is spread over the ranks");
+        HIPCHK(hipStreamSynchronize(c->stream));
+        ulonglong2 *d_fp = dmalloc<ulonglong2>(n ? n : 1);
+        uint8_t *d_out = dmalloc<uint8_t>(n ? n : 1);
+        try {
+            HIPCHK(hipMemcpy(d_fp, fps, n * 16, hipMemcpyHostToDevice));
+            std::vector<Seen> seens;
+            for (const Shard &sh : c->sh) seens.push_back(sh.seen());
+            // a fingerprint lives in its owner's shard (fp_owner); one shard: every fingerprint
+            for (size_t i = 0; i < seens.size(); i++)
+                launch_seen_query(d_fp, n, seens[i], (uint32_t)c->sh.size(), (uint32_t)c->sh[i].id, d_out, c->stream);
+            HIPCHK(hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+        } catch (...) {
+            dfree(d_fp);
+            dfree(d_out);
+            throw;
+        }
+        dfree(d_fp);
+        dfree(d_out);
         return RMC_OK;
     });
 }

@@ -12,9 +12,8 @@ struct Tables {
     const uint32_t *info;     // [U]        message info word by id (TLC order)
     const uint16_t *nat2id;   // [nat_total] natural index -> id
     const ulonglong2 *gmsg;   // [U]        per-message hash, families 0/1 (no src/dst)
-    const uint8_t *perms;     // [np][MAXN] server permutations (pi[i] = image of i)
-    const uint64_t *seeds;    // [2][MAXN + MAXN*MAXN] position seeds of the structured hash
-    int np;
+    const uint64_t *seeds;    // [2][MAXN*MAXN] odd position constants K_f[a][b] of the fingerprint (rmc_spec.h)
+    int np;                   // |Permutations(Servers)| (1: no SYMMETRY)
     uint32_t bmw;             // 32-bit words of a bitmap over the universe's ids: ceil(U / 32)
 };
 
@@ -115,11 +114,13 @@ struct KParams {
     // xside[i] = {parent global id lo, hi, slot key, record words} instead of par / pslot
     int route;
     uint4 *xside;
-    // split probe (host-driven chunks of many parents): expand writes each successor's fingerprint and
-    // its extra record words (lslot = e) and k_probe gives every successor a lane of its own for the
-    // seen-set probe and the election (bit 0); bit 1: k_insert_winners puts the winners into the seen
-    // set, not the commit; bit 2: ... and leaves its verdicts in lslot (LS_WIN / LS_SEEN) for the commit
+    // split chunk (host-driven chunks of many parents): the expansion (M_SPLIT) stages the successors
+    // and writes each parent's hash context (hctx, ctx_words per parent), and k_hash_probe gives every
+    // successor a lane of its own for its fingerprint, the seen-set probe and the election (bit 0);
+    // bit 1: k_insert_winners puts the winners into the seen set, not the commit; bit 2: ... and leaves
+    // its verdicts in lslot (LS_WIN / LS_SEEN) for the commit
     int split;
+    uint32_t *hctx;
     // test variants: bit 0 RaftSplitBrain (BecomeLeader's quorum 1), bit 1 RaftCommitPastLog
     // (FollowerAcceptEntry's newCommitIndex without Min(., Len(newLog)))
     uint32_t quirks;
@@ -161,9 +162,12 @@ struct KParams {
 
 struct KernelSet {
     int N, V, MR, MCAP, CCW, RECW_MAX, maxsucc;
+    int ctxw;                                                 // hash-context words per parent (split chunks)
     void (*single)(const KParams &, hipStream_t);           // all successors of front[0] -> next, fp, out_keys
     void (*fused)(const KParams &, hipStream_t);            // expand + hash + probe + election + staging
-    void (*probe)(const KParams &, uint64_t np, hipStream_t);     // split probe: seen set + election per successor
+    void (*split)(const KParams &, hipStream_t);            // split chunk: expand + staging + hash context
+    void (*hash_probe)(const KParams &, uint64_t np, hipStream_t);  // split chunk: fingerprint + seen set + election
+                                                                   // per successor (P.route: fingerprint only)
     void (*insert)(const KParams &, uint64_t np, hipStream_t);    // split chunk: winners into the seen set
     void (*wincount)(const KParams &, uint64_t np, hipStream_t);  // winners per parent + their scan, successors generated
     void (*commit)(const KParams &, hipStream_t);           // winners -> next level, seen set, trace, invariants;
@@ -213,5 +217,8 @@ void launch_side_sizes(const uint4 *side, uint64_t n, uint32_t *sz, hipStream_t 
 void launch_accept_side(const uint4 *side, const uint32_t *off, uint64_t n, uint64_t rel0, uint64_t *noff,
                         uint64_t *par, uint16_t *pslot, hipStream_t s);
 void launch_owner_of(const ulonglong2 *fp, uint32_t W, uint32_t *out, hipStream_t s);
+// out[i] = 1 if fp[i] is in `seen` -- for the fingerprints the shard `self` of W owns (W = 1: all)
+void launch_seen_query(const ulonglong2 *fp, uint64_t n, Seen seen, uint32_t W, uint32_t self, uint8_t *out,
+                       hipStream_t s);
 
 }  // namespace rmc

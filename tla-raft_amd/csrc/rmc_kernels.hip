@@ -60,30 +60,19 @@ extern "C" int rmc_debug_phases(unsigned long long *out, int reset) {
 #ifndef RMC_GRID_PER_CU  // one-wave blocks per CU in the expansion / commit grids
 #define RMC_GRID_PER_CU 32
 #endif
-#ifndef RMC_COMMIT_EARLY  // k_commit: the seen-set insert's first CAS overlaps the record writes.
-// Measured off: it takes k_commit to 133 VGPRs (3 waves / SIMD: Raft.cfg commit 16.5 s) or, held
-// at 4 waves, to spills (14.4 s) against 14.2 s without (profiles/r03_ab1_raftcfg_*.txt)
-#define RMC_COMMIT_EARLY 0
-#endif
-#ifndef RMC_COMMIT_PREFETCH  // k_commit: the next parent's header loads go out with this parent's record
-#define RMC_COMMIT_PREFETCH 1
-#endif
-#ifndef RMC_EXPAND_PREFETCH_MSGS  // k_expand: the next parent's message-table words fetched ahead
-#define RMC_EXPAND_PREFETCH_MSGS 1
-#endif
-#ifndef RMC_MSG_BITMAP  // k_expand: m \in msgs by an LDS bitmap of the parent's ids (0: binary search)
-#define RMC_MSG_BITMAP 1
-#endif
-#ifndef RMC_HASH_COMPACT  // k_expand (n <= 3): successor hash rows in one pass over compacted successors
-#define RMC_HASH_COMPACT 1
-#endif
 #ifndef RMC_WIDE_WAVES
 #define RMC_WIDE_WAVES 2
+#endif
+#ifndef RMC_SPLIT_WAVES  // the split expansion (no fingerprints): waves per SIMD its registers are cut for
+#define RMC_SPLIT_WAVES 6
 #endif
 
 namespace rmc {
 
-enum Mode { M_SINGLE = 3, M_FUSED = 4 };
+// SINGLE: every successor of one state (parity hook); FUSED: expand + fingerprint + seen-set probe +
+// election + staging (device loop, small chunks, sharded rounds); SPLIT: expand + staging + the
+// parent's hash context only -- k_hash_probe fingerprints, probes and elects a lane per successor
+enum Mode { M_SINGLE = 3, M_FUSED = 4, M_SPLIT = 5 };
 
 template <int N>
 __device__ __forceinline__ uint32_t sel(const uint32_t *a, int i) {
@@ -182,20 +171,10 @@ __device__ __forceinline__ uint32_t lw_byte(uint32_t lw, uint32_t x) {  // x >= 
     return (lw >> (8 * (x - 2))) & 0xFFu;
 }
 
-// membership in the parent's sorted id list (LDS)
 // m \in msgs for the parent of the wave: one LDS read of the wave's bitmap over the universe's ids
 // (k_expand builds it with the parent: msg_bitmap); replaced a binary search over the sorted ids --
 // a chain of up to 7 dependent LDS reads per test, several tests per successor kind
 __device__ __forceinline__ bool in_msgs(const uint32_t *bm, uint32_t id) { return (bm[id >> 5] >> (id & 31u)) & 1u; }
-
-__device__ __forceinline__ bool has_id(const uint16_t *ids, uint32_t nm, uint32_t id) {
-    uint32_t lo = 0, hi = nm;
-    while (lo < hi) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (ids[mid] < id) lo = mid + 1; else hi = mid;
-    }
-    return lo < nm && ids[lo] == id;
-}
 
 // Median(F) (tla:70-75): smallest F[s] with |{p : F[p] <= F[s]}| >= k.
 template <int N>
@@ -381,18 +360,15 @@ __device__ __forceinline__ int check_invs(const uint32_t *c, uint32_t order, int
     return 1;
 }
 
-// ---- signature pre-sort (n >= 4) ----------------------------------------------------------
-// The fingerprint is min over permutations pi of H(pi), H = sum_s Z(pi(s), U[s]) +
-// sum_{s != j} Z(pi(s), pi(j), X[s][j]).  Any permutation-equivariant signature of a server
-// (a function of its data that does not name other servers) orders the servers; taking the
-// minimum only over the permutations that send the servers to their signature-sorted
-// positions (the coset fixed by the signature ties) is still constant on every symmetry class
-// (Raft.tla:21 SYMMETRY): for y = sigma(x) the allowed set of y is that of x composed with
-// sigma^-1.  The signature is the server's own word plus the sum of its outgoing pair inputs
-// (its message hashes to each peer, matchIndex / nextIndex / vote for that peer), mixed.
-constexpr uint64_t SIG_KU = 0x2545f4914f6cdd1dull, SIG_KX = 0x9fb21c651e98df25ull;
-__device__ __forceinline__ uint64_t sig_part_u(uint64_t u) { return mix64(u ^ SIG_KU); }
-__device__ __forceinline__ uint64_t sig_part_x(uint64_t x) { return mix64(x ^ SIG_KX); }
+// ---- symmetry fingerprint (rmc_spec.h: content matrix, position constants, signature coset) -----
+// The fingerprint is the minimum over permutations pi of H(pi) = sum_{t,j} C[t][j] K[pi(t)][pi(j)].
+// Any permutation-equivariant signature of a server (a function of its data that does not name
+// other servers) orders the servers; taking the minimum only over the permutations that send the
+// servers to their signature-sorted positions (the coset fixed by the signature ties) is still
+// constant on every symmetry class (Raft.tla:21 SYMMETRY): for y = sigma(x) the allowed set of y is
+// that of x composed with sigma^-1.  The signature is the server's row sum of C_1 -- its own word and
+// its outgoing pair contents (message hashes to each peer, matchIndex / nextIndex / vote for it).
+// Without SYMMETRY the identity is the only permutation (coset_ident).
 
 // per server t, 6 bits: lo_t (servers with a smaller signature) | (ties_t - 1) << 3
 template <int N>
@@ -408,6 +384,14 @@ __device__ __forceinline__ uint32_t coset_ranks(const uint64_t *sig) {
         }
         rk |= (lo | (eq << 3)) << (6 * t);
     }
+    return rk;
+}
+// no symmetry: server t at position t, no ties
+template <int N>
+__device__ __forceinline__ uint32_t coset_ident() {
+    uint32_t rk = 0;
+#pragma unroll
+    for (int t = 0; t < N; t++) rk |= (uint32_t)t << (6 * t);
     return rk;
 }
 __device__ __forceinline__ uint32_t small_fact(uint32_t g) {
@@ -427,14 +411,21 @@ __device__ __forceinline__ uint32_t coset_size(uint32_t rk) {
     }
     return K;
 }
-// the k-th allowed permutation (k < coset_size): tie groups in server order, each group's
-// members (in server order) take the positions [lo, lo + g) in the k-th arrangement
-// (factorial number system, group by group)
+// the k-th allowed permutation (k < coset_size), packed: server t goes to position (img >> 3t) & 7.
+// Tie groups in server order, each group's members (in server order) take the positions
+// [lo, lo + g) in the k-th arrangement (factorial number system, group by group).  (Packed, not an
+// array: the group members' positions are computed at run time, and an array written that way
+// lives in scratch.)
 template <int N>
-__device__ __forceinline__ void coset_img(uint32_t rk, uint32_t k, uint32_t *img) {
+__device__ __forceinline__ uint32_t coset_img(uint32_t rk, uint32_t k) {
+    uint32_t img = 0;
 #pragma unroll
     for (int t = 0; t < N; t++) {
         const uint32_t lo = (rk >> (6 * t)) & 7u, g = ((rk >> (6 * t + 3)) & 7u) + 1u;
+        if (g == 1u) {  // untied: its position is its rank
+            img |= lo << (3 * t);
+            continue;
+        }
         bool head = true;
 #pragma unroll
         for (int u = 0; u < t; u++) head &= ((rk >> (6 * u)) & 7u) != lo;
@@ -453,25 +444,25 @@ __device__ __forceinline__ void coset_img(uint32_t rk, uint32_t k, uint32_t *img
             for (; d; d--) m &= m - 1u;
             const uint32_t pos = (uint32_t)__builtin_ctz(m);
             avail &= ~(1u << pos);
-            img[u] = lo + pos;
+            img |= (lo + pos) << (3 * u);
             i++;
         }
     }
+    return img;
 }
-// H_f at one permutation from per-server inputs: u(t), x(f, t, j), seeds sS(f, a), sP(f, a, b)
-template <int N, class FU, class FX, class FS, class FP>
-__device__ __forceinline__ ulonglong2 hash_at(const uint32_t *img, FU u, FX x, FS sS, FP sP) {
+// H_f at one permutation (packed as coset_img): sum over the content matrix C(f, t, j) (diagonal:
+// own word) of the position constant K(f, pi(t), pi(j))
+template <int N, class FC, class FK>
+__device__ __forceinline__ ulonglong2 hash_at(uint32_t img, FC C, FK K) {
     uint64_t h0 = 0, h1 = 0;
 #pragma unroll
     for (int t = 0; t < N; t++) {
-        const uint64_t ut = u(t);
-        h0 += mix64(ut ^ sS(0, img[t]));
-        h1 += mix64(ut ^ sS(1, img[t]));
+        const uint32_t it = (img >> (3 * t)) & 7u;
 #pragma unroll
         for (int j = 0; j < N; j++) {
-            if (j == t) continue;
-            h0 += mix64(x(0, t, j) ^ sP(0, img[t], img[j]));
-            h1 += mix64(x(1, t, j) ^ sP(1, img[t], img[j]));
+            const uint32_t ij = (img >> (3 * j)) & 7u;
+            h0 += C(0, t, j) * K(0, it, ij);
+            h1 += C(1, t, j) * K(1, it, ij);
         }
     }
     return make_ulonglong2(h0, h1);
@@ -480,83 +471,7 @@ __device__ __forceinline__ bool lex_less(ulonglong2 a, ulonglong2 b) {  // (h1, 
     return a.y < b.y || (a.y == b.y && a.x < b.x);
 }
 
-// ---- structured symmetry fingerprint --------------------------------------------------
-// seeds layout: [f][0..MAXN) server position seeds, [f][MAXN + k*MAXN + l] pair seeds
-template <int N, int V>
-__device__ __forceinline__ ulonglong2 fingerprint(const uint32_t *c, int srow, const uint64_t *row0, const uint64_t *row1,
-                                  const uint64_t *M0, const uint64_t *M1, const Tables &t) {
-    using Lo = Layout<N, V>;
-    uint64_t U[N];
-    uint64_t X0[N * N], X1[N * N];
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-        const uint32_t vf = nib(c[Lo::W_VF], i);
-        const uint32_t vrel = vf == VF_NONE ? 0u : (vf == (uint32_t)i ? 1u : 2u);
-        const uint32_t own = vrel | (nib(c[Lo::W_CT], i) << 2) | (nib(c[Lo::W_ROLE], i) << 6) |
-                             (nib(c[Lo::W_CI], i) << 10) | (nib(c[Lo::W_LL], i) << 14) |
-                             (nib(c[Lo::W_MI + i], i) << 18) | (nib(c[Lo::W_NI + i], i) << 22);
-        U[i] = ((uint64_t)c[Lo::W_LOG + i] << 32) | own;
-#pragma unroll
-        for (int j = 0; j < N; j++) {
-            if (i == j) continue;
-            const uint64_t small = (uint64_t)(nib(c[Lo::W_MI + i], j) | (nib(c[Lo::W_NI + i], j) << 4) |
-                                              ((vf == (uint32_t)j) ? 256u : 0u));
-            const uint64_t m0 = (i == srow) ? row0[j] : M0[i * N + j];
-            const uint64_t m1 = (i == srow) ? row1[j] : M1[i * N + j];
-            X0[i * N + j] = m0 ^ (small * PAIR_K0);
-            X1[i * N + j] = m1 ^ (small * PAIR_K1);
-        }
-    }
-    uint64_t b0 = ~0ull, b1 = ~0ull;
-    const uint64_t *S0 = t.seeds, *S1 = t.seeds + (MAXN + MAXN * MAXN);
-    if (N >= 4) {
-        uint64_t sig[N];
-#pragma unroll
-        for (int i = 0; i < N; i++) {
-            sig[i] = sig_part_u(U[i]);
-#pragma unroll
-            for (int j = 0; j < N; j++)
-                if (j != i) sig[i] += sig_part_x(X0[i * N + j]);
-        }
-        const uint32_t rk = coset_ranks<N>(sig), K = coset_size<N>(rk);
-        ulonglong2 best = make_ulonglong2(~0ull, ~0ull);
-        for (uint32_t k = 0; k < K; k++) {
-            uint32_t img[N];
-            coset_img<N>(rk, k, img);
-            const ulonglong2 h = hash_at<N>(
-                img, [&](int i) { return U[i]; },
-                [&](int f, int i, int j) { return f ? X1[i * N + j] : X0[i * N + j]; },
-                [&](int f, uint32_t a) { return (f ? S1 : S0)[a]; },
-                [&](int f, uint32_t a, uint32_t b) { return (f ? S1 : S0)[MAXN + a * MAXN + b]; });
-            if (lex_less(h, best)) best = h;
-        }
-        return make_ulonglong2(best.x | 1ull, best.y);
-    }
-    for (int p = 0; p < t.np; p++) {
-        const uint8_t *pi = t.perms + p * MAXN;
-        uint32_t img[N];
-#pragma unroll
-        for (int i = 0; i < N; i++) img[i] = pi[i];
-        uint64_t h0 = 0, h1 = 0;
-#pragma unroll
-        for (int i = 0; i < N; i++) {
-            h0 += mix64(U[i] ^ S0[img[i]]);
-            h1 += mix64(U[i] ^ S1[img[i]]);
-#pragma unroll
-            for (int j = 0; j < N; j++) {
-                if (i == j) continue;
-                const uint32_t q = MAXN + img[i] * MAXN + img[j];
-                h0 += mix64(X0[i * N + j] ^ S0[q]);
-                h1 += mix64(X1[i * N + j] ^ S1[q]);
-            }
-        }
-        if (h1 < b1 || (h1 == b1 && h0 < b0)) { b1 = h1; b0 = h0; }
-    }
-    return make_ulonglong2(b0 | 1ull, b1);
-}
-
-// Per-server and per-pair inputs of the structured hash, from the words of one row
-// (identical to what fingerprint() computes for row i).
+// Per-server and per-pair inputs of the content matrix, from the words of one row.
 template <int N>
 __device__ __forceinline__ uint64_t own_word(uint32_t vfw, uint32_t ctw, uint32_t rolew, uint32_t ciw, uint32_t llw,
                                              uint32_t lw, uint32_t mirow, uint32_t nirow, uint32_t i) {
@@ -569,7 +484,45 @@ __device__ __forceinline__ uint64_t own_word(uint32_t vfw, uint32_t ctw, uint32_
 __device__ __forceinline__ uint64_t pair_small(uint32_t mirow, uint32_t nirow, uint32_t vf_i, uint32_t j) {
     return (uint64_t)(nib(mirow, j) | (nib(nirow, j) << 4) | ((vf_i == j) ? 256u : 0u));
 }
+// content C_f[t][j] of row t from its words and its message-hash sums toward j (Ms0/Ms1)
+template <int N>
+__device__ __forceinline__ uint64_t content(int f, uint32_t t, uint32_t j, const uint32_t *c, uint32_t lw_t,
+                                            uint32_t mirow, uint32_t nirow, uint64_t Ms) {
+    using Lo = Layout<N, 1>;
+    if (t == j)
+        return cmix_own(own_word<N>(c[Lo::W_VF], c[Lo::W_CT], c[Lo::W_ROLE], c[Lo::W_CI], c[Lo::W_LL], lw_t, mirow,
+                                    nirow, t),
+                        f);
+    const uint64_t sm = pair_small(mirow, nirow, nib(c[Lo::W_VF], t), j);
+    return cmix_pair(Ms ^ (sm * (f ? PAIR_K1 : PAIR_K0)), f);
+}
 
+// The fingerprint of a whole state: nibble core c, message-hash sums M_f[t * N + j] (src t, dst j).
+template <int N, int V>
+__device__ __forceinline__ ulonglong2 fingerprint(const uint32_t *c, const uint64_t *M0, const uint64_t *M1,
+                                                  const Tables &t) {
+    using Lo = Layout<N, V>;
+    uint64_t C0[N * N], C1[N * N], sig[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        sig[i] = 0;
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            C0[i * N + j] = content<N>(0, i, j, c, c[Lo::W_LOG + i], c[Lo::W_MI + i], c[Lo::W_NI + i], M0[i * N + j]);
+            C1[i * N + j] = content<N>(1, i, j, c, c[Lo::W_LOG + i], c[Lo::W_MI + i], c[Lo::W_NI + i], M1[i * N + j]);
+            sig[i] += C1[i * N + j];
+        }
+    }
+    const uint32_t rk = t.np > 1 ? coset_ranks<N>(sig) : coset_ident<N>(), K = coset_size<N>(rk);
+    ulonglong2 best = make_ulonglong2(~0ull, ~0ull);
+    for (uint32_t k = 0; k < K; k++) {
+        const ulonglong2 h = hash_at<N>(
+            coset_img<N>(rk, k), [&](int f, int a, int b) { return f ? C1[a * N + b] : C0[a * N + b]; },
+            [&](int f, uint32_t a, uint32_t b) { return t.seeds[f * SEEDS_PER_F + a * MAXN + b]; });
+        if (lex_less(h, best)) best = h;
+    }
+    return make_ulonglong2(best.x | 1ull, best.y);
+}
 constexpr int factorial(int n) { return n <= 1 ? 1 : n * factorial(n - 1); }
 
 // ---- expansion of one parent per wavefront ------------------------------------------------
@@ -583,14 +536,8 @@ struct Wave {
     uint64_t idw;        // ring position of the parent's first message-id word
     uint32_t id[MR];     // message id owned by this lane per round (0xFFFF = none)
     uint32_t inf[MR];
-    const uint32_t *bm;  // LDS bitmap of the parent's message ids (msg_bitmap), or nullptr: binary search
+    const uint32_t *bm;  // LDS bitmap of the parent's message ids (msg_bitmap)
 };
-
-// membership test of the evaluation: the bitmap when the kernel built one, else the sorted ids
-template <int N, int V, int MR>
-__device__ __forceinline__ bool msg_in(const Wave<N, V, MR> &W, const uint16_t *ids, uint32_t id) {
-    return W.bm ? in_msgs(W.bm, id) : has_id(ids, W.nm, id);
-}
 
 // The wave's parent's ids as a bitmap in LDS (bmw words): cleared, then one LDS OR per message.
 template <int N, int V, int MR>
@@ -672,7 +619,7 @@ __device__ __forceinline__ uint32_t nat_lookup(const KParams &P, uint32_t nat) {
 // BFV (the tla:420 variant): ob gets the lane's BecomeFollower successor (tla:190-229) -- a second
 // candidate per message; with BFV false ob is not touched.
 template <int N, int V, int MR, bool BFV = false>
-__device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> &W, const uint16_t *ids, int r, int lane,
+__device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> &W, int r, int lane,
                          Succ<N, V, MR> &o, Succ<N, V, MR> &ob, uint32_t &assert_key, uint32_t *ainf, uint32_t pid) {
     // pid: the id msg_nat looked up for this lane (the only one its action may send)
     using Lo = Layout<N, V>;
@@ -740,10 +687,10 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
         const uint32_t llt = lw_term(lw, ll), mlli = mi_x1(m), mllt = mi_x2(m);
         if (!(mllt > llt || (mllt == llt && mlli >= ll))) return;
         const uint32_t g = pid;  // nat2id[nat_vresp(s, src, mt)]
-        if (msg_in(W, ids, g)) return;
+        if (in_msgs(W.bm, g)) return;
         o.c[Lo::W_VF] = setnib(o.c[Lo::W_VF], s, src);
         o.add[0] = g; o.nadd = 1;
-        ainf[0] = minfo(VRESP, s, src, mt, 0, 0, 0, 0, 0, 0);
+        if (ainf) ainf[0] = minfo(VRESP, s, src, mt, 0, 0, 0, 0, 0, 0);
         o.key = slot_key(s, RV, k);
         return;
     }
@@ -770,16 +717,16 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
                 o.lw = nlw;
                 o.c[Lo::W_LL] = setnib(o.c[Lo::W_LL], s, nl);
             }
-            if (!msg_in(W, ids, resp)) {
+            if (!in_msgs(W.bm, resp)) {
                 o.add[0] = resp; o.nadd = 1;
-                ainf[0] = minfo(ARESP, s, src, mt, pli + ent, 1, 0, 0, 0, 0);
+                if (ainf) ainf[0] = minfo(ARESP, s, src, mt, pli + ent, 1, 0, 0, 0, 0);
             }
             o.key = slot_key(s, FAE, k);
         } else {
             const uint32_t resp = pid;  // nat2id[nat_aresp(s, src, mt, pli, FALSE)]
-            if (msg_in(W, ids, resp)) return;
+            if (in_msgs(W.bm, resp)) return;
             o.add[0] = resp; o.nadd = 1;
-            ainf[0] = minfo(ARESP, s, src, mt, pli, 0, 0, 0, 0, 0);
+            if (ainf) ainf[0] = minfo(ARESP, s, src, mt, pli, 0, 0, 0, 0, 0);
             o.key = slot_key(s, FRE, k);
         }
         return;
@@ -816,7 +763,7 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
 
 // Evaluate the non-message slot owned by this lane (last round).
 template <int N, int V, int MR>
-__device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR> &W, const uint16_t *ids, int lane,
+__device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR> &W, int lane,
                           Succ<N, V, MR> &o, uint32_t *ainf, const uint32_t (&sid)[N - 1]) {
     // sid: the ids slot_nats looked up for this lane
     using Lo = Layout<N, V>;
@@ -856,10 +803,10 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
             uint32_t id = 0;
 #pragma unroll
             for (int i = 0; i < N - 1; i++) id = i == ix ? sid[i] : id;
-            if (!msg_in(W, ids, id)) {
+            if (!in_msgs(W.bm, id)) {
 #pragma unroll
                 for (int a = 0; a < S::NADD; a++) o.add[a] = ((uint32_t)a == na) ? id : o.add[a];
-                ainf[na] = minfo(VREQ, s, (uint32_t)p, term, ll, llt, 0, 0, 0, 0);
+                if (ainf) ainf[na] = minfo(VREQ, s, (uint32_t)p, term, ll, llt, 0, 0, 0, 0);
                 na++;
             }
         }
@@ -919,11 +866,11 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
         const uint32_t ent = ni <= ll ? 1u : 0u;
         const uint32_t eb = ent ? lw_byte(lw, ni) : 0u;
         const uint32_t id = sid[0];  // nat2id[nat_areq(s, dst, ct, pli, plt, ent, eb, ci)]
-        if (msg_in(W, ids, id)) return;  // m \notin msgs
+        if (in_msgs(W.bm, id)) return;  // m \notin msgs
         o.c[Lo::W_PEND] = W.c[Lo::W_PEND] | (1u << pb);
         o.add[0] = id;
         o.nadd = 1;
-        ainf[0] = minfo(AREQ, s, dst, ct, pli, plt, ci, ent, eb & 15u, eb >> 4);
+        if (ainf) ainf[0] = minfo(AREQ, s, dst, ct, pli, plt, ci, ent, eb & 15u, eb >> 4);
         o.key = slot_key(s, LAE, dst);
         return;
     }
@@ -956,8 +903,8 @@ __device__ __forceinline__ void load_core(const uint32_t *ring, uint64_t start, 
     decode_core<N, V>(packed, c);
 }
 
-// Load a state record into the wave: uniform core, per-lane message ids, LDS copy of
-// the sorted ids and the per-(src,dst) message hash sums.
+// Load a state record into the wave: uniform core (+ an LDS copy), per-lane message ids and info
+// words, the per-(src,dst) message hash sums.
 // The whole record in one round trip: lane k holds record word k (and 64 + k); the core is read
 // across lanes, each lane's message ids are shuffled to it by load_parent -- no second dependent
 // load for the ids (words past the record's end are read but never used).  k_expand issues this
@@ -971,8 +918,7 @@ __device__ __forceinline__ void fetch_record(const KParams &P, uint64_t start, i
 // load_parent on a record already fetched (fetch_record)
 template <int N, int V, int MR, bool SUMS>
 __device__ __forceinline__ void load_parent_words(const KParams &P, uint64_t start, uint32_t rw0, uint32_t rw1, int lane,
-                                                  Wave<N, V, MR> &W, uint16_t *ids, uint64_t *M0, uint64_t *M1,
-                                                  uint32_t *pcore) {
+                                                  Wave<N, V, MR> &W, uint64_t *M0, uint64_t *M1, uint32_t *pcore) {
     using Lo = Layout<N, V>;
     using S = Spec<N, V, MR>;
     uint32_t packed[S::CCW];
@@ -1006,7 +952,6 @@ __device__ __forceinline__ void load_parent_words(const KParams &P, uint64_t sta
                 atomicAdd((unsigned long long *)&M1[pr], (unsigned long long)g.y);
             }
         }
-        ids[k] = (uint16_t)id;
         W.id[r] = id;
         W.inf[r] = inf;
     }
@@ -1027,8 +972,8 @@ __device__ __forceinline__ void load_parent_words(const KParams &P, uint64_t sta
 }
 
 // The message-table words of a fetched record (info word + hash pair per message), issued ahead of
-// use: k_expand loads them for its next parent while it hashes the current one (RMC_EXPAND_PREFETCH_MSGS),
-// which takes the table round trip off the start of every parent.
+// use: k_expand loads them for its next parent while it hashes the current one, which takes the
+// table round trip off the start of every parent.
 template <int MR>
 struct MsgPre {
     uint32_t id[MR], inf[MR];
@@ -1067,8 +1012,8 @@ __device__ __forceinline__ void fetch_msgs(const KParams &P, uint32_t rw0, uint3
 // load_parent_words with the message-table words already fetched (fetch_msgs)
 template <int N, int V, int MR>
 __device__ __forceinline__ void load_parent_pre(const KParams &P, uint64_t start, uint32_t rw0, int lane,
-                                                Wave<N, V, MR> &W, uint16_t *ids, uint64_t *M0, uint64_t *M1,
-                                                uint32_t *pcore, const MsgPre<MR> &pm) {
+                                                Wave<N, V, MR> &W, uint64_t *M0, uint64_t *M1, uint32_t *pcore,
+                                                const MsgPre<MR> &pm) {
     using Lo = Layout<N, V>;
     using S = Spec<N, V, MR>;
     uint32_t packed[S::CCW];
@@ -1092,7 +1037,6 @@ __device__ __forceinline__ void load_parent_pre(const KParams &P, uint64_t start
             atomicAdd((unsigned long long *)&M0[pr], (unsigned long long)pm.g[r].x);
             atomicAdd((unsigned long long *)&M1[pr], (unsigned long long)pm.g[r].y);
         }
-        ids[k] = (uint16_t)pm.id[r];
         W.id[r] = pm.id[r];
         W.inf[r] = pm.inf[r];
     }
@@ -1113,12 +1057,12 @@ __device__ __forceinline__ void load_parent_pre(const KParams &P, uint64_t start
 }
 
 template <int N, int V, int MR, bool SUMS>
-__device__ __forceinline__ void load_parent(const KParams &P, uint64_t start, int lane, Wave<N, V, MR> &W, uint16_t *ids,
-                            uint64_t *M0, uint64_t *M1, uint32_t *pcore) {
+__device__ __forceinline__ void load_parent(const KParams &P, uint64_t start, int lane, Wave<N, V, MR> &W, uint64_t *M0,
+                                            uint64_t *M1, uint32_t *pcore) {
     using S = Spec<N, V, MR>;
     uint32_t rw0, rw1;
     fetch_record<MR, S::RECW_MAX>(P, start, lane, rw0, rw1);
-    load_parent_words<N, V, MR, SUMS>(P, start, rw0, rw1, lane, W, ids, M0, M1, pcore);
+    load_parent_words<N, V, MR, SUMS>(P, start, rw0, rw1, lane, W, M0, M1, pcore);
 }
 
 // hash row of the acting server: parent sums + the messages this successor adds
@@ -1141,11 +1085,6 @@ __device__ __forceinline__ void succ_row_at(uint32_t s, uint32_t nadd, const uin
             row1[j] += ((uint32_t)j == dst) ? g.y : 0ull;
         }
     }
-}
-template <int N, int V, int MR>
-__device__ __forceinline__ void succ_row(const Succ<N, V, MR> &o, const uint64_t *M0, const uint64_t *M1,
-                                         const uint32_t *ainf, uint64_t *row0, uint64_t *row1) {
-    succ_row_at<N, V, MR>(o.s, o.nadd, M0, M1, ainf, row0, row1);
 }
 
 // Merge the parent's sorted ids (per lane: id[r] = id r*64+lane, 0xFFFF past nm) with a
@@ -1247,34 +1186,6 @@ __device__ __forceinline__ void seen_insert(const Seen &S, ulonglong2 f) {
         if (prev == 0ull) { S.T[h].y = f.y; return; }
         h = (h + 1) & S.mask;
     }
-}
-
-// An insert split in two: the first slot's CAS goes out as soon as the fingerprint is known and its
-// result is taken only once the caller's other work is issued (k_commit: the state's record, trace
-// entry and invariants), so the round trip overlaps that work instead of preceding it.
-__device__ __forceinline__ uint64_t seen_insert_begin(const Seen &S, ulonglong2 f, unsigned long long *prev) {
-    if (S.Tc) {
-        const uint64_t h = t_home_c(f, S.cap);
-        *prev = atomicCAS(&S.Tc[h], 0ull, (unsigned long long)f.x);
-        return h;
-    }
-    const uint64_t h = t_index(f, S.mask);
-    *prev = atomicCAS((unsigned long long *)&S.T[h].x, 0ull, (unsigned long long)f.x);
-    return h;
-}
-__device__ __forceinline__ void seen_insert_end(const Seen &S, ulonglong2 f, uint64_t h, unsigned long long prev) {
-    if (S.Tc) {
-        while (prev != 0ull) {
-            h = (h + 1 == S.cap) ? 0 : h + 1;
-            prev = atomicCAS(&S.Tc[h], 0ull, (unsigned long long)f.x);
-        }
-        return;
-    }
-    while (prev != 0ull) {
-        h = (h + 1) & S.mask;
-        prev = atomicCAS((unsigned long long *)&S.T[h].x, 0ull, (unsigned long long)f.x);
-    }
-    S.T[h].y = f.y;
 }
 
 __device__ __forceinline__ uint64_t l_index(const ulonglong2 f, uint64_t mask) {
@@ -1383,48 +1294,55 @@ __device__ __forceinline__ void unstage_core(const uint32_t *pc, const uint4 a, 
     c[Lo::W_MISC] = b.y;
 }
 
+// Words of a split chunk's hash context per parent (M_SPLIT -> k_hash_probe): the packed core
+// (padded to 16 B), then per ordered server pair (t, j), t != j, its message-hash sums
+// {M_0 lo, hi, M_1 lo, hi}.
+template <int N, int V>
+constexpr int ctx_words() { return ((Codec<N, V>::CCW + 3) / 4) * 4 + 4 * N * (N - 1); }
+constexpr int pair_index(int N, int t, int j) { return t * (N - 1) + (j < t ? j : j - 1); }
+
+// one family's half of msg_hash (rmc_spec.h)
+__device__ __forceinline__ uint64_t msg_hash_half(uint32_t info, int f) {
+    const uint64_t body = (uint64_t)info & ~0xFCull;
+    return f ? mix64(body * 0xc2b2ae3d27d4eb4fULL + (SEED_MSG + 0x632be59bd9b4e019ULL))
+             : mix64(body * 0x9e3779b97f4a7c15ULL + SEED_MSG);
+}
+
+template <int N, int MR, int MODE, bool BFV>
+constexpr int expand_waves() {
+    return MODE == M_SPLIT ? ((MR == 1 && !BFV) ? RMC_SPLIT_WAVES : RMC_WIDE_WAVES)
+                           : ((N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((BFV && N >= 4) ? 1 : RMC_WIDE_WAVES));
+}
+
 // BFV: the BecomeFollower variant (tla:420) -- MR more candidates (one per message lane) and MR * 64
 // more successor slots per parent (MX)
 template <int N, int V, int MR, int MODE, bool BFV = false>
-__global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((BFV && N >= 4) ? 1 : RMC_WIDE_WAVES)) void k_expand(KParams P) {
+__global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expand(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
-    constexpr bool SUMS = true;
+    constexpr bool HASH = MODE != M_SPLIT;              // fingerprints in this kernel
     constexpr int MX = S::MAXS + (BFV ? S::MCAP : 0);   // successor slots per parent
     constexpr int NC = MR + 1 + (BFV ? MR : 0);         // candidates per lane: messages, slot, BecomeFollower
-    __shared__ uint16_t ids[S::MCAP];
-    __shared__ ulonglong2 sPart[SUMS ? 64 : 1];         // partial minima per (successor, permutation block)
-    __shared__ uint64_t M0[N * N], M1[N * N];
+    constexpr int HX = HASH ? MX : 1;                   // per-successor hash inputs, by TLC rank
+    constexpr int HB = !HASH ? 1 : (N <= 3 ? 32 : 64);  // successors hashed per batch
+    constexpr int FH = HASH ? 64 / HB : 1;              // lanes per batch successor: one per half when 2
+    __shared__ uint64_t M0[N * N], M1[N * N];           // the parent's message-hash sums per (src, dst)
     __shared__ uint32_t pcore[Lo::NW + N];
-    constexpr bool SIG = SUMS && N >= 4;                // signature pre-sort (coset minimum)
-    constexpr int NPM = (SUMS && !SIG) ? factorial(N) : 1;  // |Permutations(Servers)| (tla:21)
-    constexpr int MAXS = SUMS ? MX : 1;
-    // n >= 4 (signature path): the successors are hashed in batches of 64 (by TLC rank), so the row
-    // arrays hold one batch -- the LDS of a block no longer caps the 2 waves / SIMD the registers allow
-    // (25.8 -> ~15 KB for 5 servers); a parent has more than 64 successors only rarely
-    constexpr int SBAT = SIG ? 64 : MAXS;
-    constexpr int MAXG = SIG ? SBAT : 1;
-    __shared__ uint64_t Rt[2][NPM * N], Tt[2][NPM];     // parent row terms / totals per permutation
-    __shared__ uint64_t sdS[2][N], sdP[2][N * N];       // position seeds
-    __shared__ uint8_t pimg[NPM * N];                   // permutation images
-    __shared__ uint64_t sU[SBAT], sX[2][SBAT * N];      // compacted successor rows (of one batch when SIG)
-    // SIG: every successor's row inputs by TLC rank (own word; matchIndex row | votedFor << 20;
-    // nextIndex row; its added messages' info words in sAinf: sCa)
-    __shared__ uint64_t sUg[SIG ? MAXS : 1];
-    __shared__ uint32_t sW1[SIG ? MAXS : 1], sW2[SIG ? MAXS : 1];
-    __shared__ uint8_t sS[MAXS], sNa[MAXS];             // acting server, |added ids| per successor
-    // CPT (n <= 3): the successors' hash rows are built in one pass over the compacted successors (a
-    // lane each) instead of once per candidate kind -- per successor its rows and votedFor (sCp) and
-    // where its added messages' info words are (sCa)
-    constexpr bool CPT = RMC_HASH_COMPACT && !SIG && N <= 3;
-    __shared__ uint32_t sCp[CPT ? MAXS : 1];
-    __shared__ uint16_t sCa[(CPT || SIG) ? MAXS : 1];
-    // signature pre-sort: parent rows / signatures, per successor the tie ranks, the first task
-    // of its coset (exclusive scan of coset sizes) and its running minimum; per task its successor
-    __shared__ uint64_t pU[SIG ? N : 1], pX[2][SIG ? N * N : 1], psig[SIG ? N : 1];
-    __shared__ uint32_t sRk[MAXG], sKoff[MAXG], sTl[SIG ? 64 : 1];
-    __shared__ ulonglong2 sBest[MAXG];
-    __shared__ uint32_t sAinf[(MR + 1) * 64 * S::NADD];  // info words of the messages each candidate adds
+    __shared__ uint64_t sK[2][HASH ? N * N : 1];        // position constants K_f[a][b]
+    __shared__ uint64_t pC[2][HASH ? N * N : 1];        // the parent's content matrix C_f[t][j]
+    __shared__ uint64_t psig[HASH ? N : 1];             // ... and its servers' signatures
+    // every successor's row inputs at its TLC rank: own word; matchIndex row | votedFor << 20;
+    // nextIndex row; where its added messages' info words are (sAinf); acting server; |added|
+    __shared__ uint64_t sUg[HX];
+    __shared__ uint32_t sW1[HX], sW2[HX];
+    __shared__ uint16_t sCa[HX];
+    __shared__ uint8_t sS[HX], sNa[HX];
+    // per batch successor: its acting row's contents, tie ranks, first task, running minimum;
+    // per task lane: its partial minimum and successor
+    __shared__ uint64_t sC[2][HASH ? HB * N : 1];
+    __shared__ uint32_t sRk[HB], sKoff[HB], sTl[HASH ? 64 : 1];
+    __shared__ ulonglong2 sBest[HB], sPart[HASH ? 64 : 1];
+    __shared__ uint32_t sAinf[HASH ? (MR + 1) * 64 * S::NADD : 1];  // info words of the messages each candidate adds
     extern __shared__ uint32_t sBM[];                    // bitmap of the parent's message ids (P.t.bmw words)
     if (MODE == M_FUSED && !level_args(P)) return;
     // device loop: the levels committed so far go to the host as this level starts (the write to
@@ -1434,30 +1352,20 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
     // device-loop grids are sized on a bound of the level: blocks past it leave before the LDS setup
     if (MODE == M_FUSED && P.p_begin + blockIdx.x >= P.p_end) return;
     const int lane = threadIdx.x;
-    if (SUMS) {
-        if (!SIG)
-            for (int i = lane; i < P.t.np * N; i += 64) pimg[i] = P.t.perms[(i / N) * MAXN + (i % N)];
-        if (lane < N) {
-            sdS[0][lane] = P.t.seeds[lane];
-            sdS[1][lane] = P.t.seeds[MAXN + MAXN * MAXN + lane];
-        }
-        if (lane < N * N) {
-            const int k = lane / N, l = lane % N;
-            sdP[0][lane] = P.t.seeds[MAXN + k * MAXN + l];
-            sdP[1][lane] = P.t.seeds[2 * MAXN + MAXN * MAXN + k * MAXN + l];
-        }
+    if (HASH && lane < 2 * N * N) {
+        const int f = lane / (N * N), a = (lane / N) % N, b = lane % N;
+        sK[f][a * N + b] = P.t.seeds[f * SEEDS_PER_F + a * MAXN + b];
     }
     PHASE_DECL
     // software pipeline over the block's parents: the next parent's record offset goes out at the
-    // top of an iteration and its record once this one's actions are evaluated, so a block's
-    // second and later parents start with their record in registers
-    // (offsets two parents ahead: an offset has a whole iteration to land before its record is fetched)
+    // top of an iteration and its record once this one's is consumed, so a block's second and later
+    // parents start with their record in registers (offsets two parents ahead: an offset has a
+    // whole iteration to land before its record is fetched).  One-round kernels also fetch the next
+    // parent's message-table words once this one's actions are evaluated (the two-round n >= 4
+    // expansion is at its register limit already).
     uint64_t p = P.p_begin + blockIdx.x, nstart = 0, nnstart = 0;
     uint32_t nrw0 = 0, nrw1 = 0;
-    // PREM: the next parent's record goes out as soon as this one's is consumed, its message-table
-    // words once this one's actions are evaluated -- both land while this parent is hashed (one-round
-    // kernels: the two-round n >= 4 expansion is at its register limit already)
-    constexpr bool PREM = RMC_EXPAND_PREFETCH_MSGS && MR == 1;
+    constexpr bool PREM = MR == 1;
     MsgPre<MR> pm;
     if (p < P.p_end) {
         nstart = rec_start<S::RECW_MAX>(P, p);
@@ -1471,36 +1379,37 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
         nstart = nnstart;
         if (p + 2ull * gridDim.x < P.p_end) nnstart = rec_start<S::RECW_MAX>(P, p + 2ull * gridDim.x);
         Wave<N, V, MR> W;
+        const uint32_t rec0 = nrw0;  // this parent's record words (lane k: word k; the split context keeps the core)
         if constexpr (PREM) {
-            load_parent_pre<N, V, MR>(P, start, nrw0, lane, W, ids, M0, M1, pcore, pm);
+            load_parent_pre<N, V, MR>(P, start, nrw0, lane, W, M0, M1, pcore, pm);
             if (more) fetch_record<MR, S::RECW_MAX>(P, nstart, lane, nrw0, nrw1);
         } else {
-            load_parent_words<N, V, MR, SUMS>(P, start, nrw0, nrw1, lane, W, ids, M0, M1, pcore);
+            load_parent_words<N, V, MR, true>(P, start, nrw0, nrw1, lane, W, M0, M1, pcore);
         }
-#if RMC_MSG_BITMAP
         msg_bitmap<N, V, MR>(sBM, P.t.bmw, W, lane);
         W.bm = sBM;
-#else
-        W.bm = nullptr;
-#endif
         PHASE(0);
         Succ<N, V, MR> cand[NC];
         uint32_t akey = KEY_NONE;
+        // the lane index, opaque to the compiler here: what the evaluation derives from it is
+        // recomputed per parent instead of hoisted out of the loop (and spilled)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
         // every id lookup of the actions in one round trip (msg_nat / slot_nats)
         uint32_t mid[MR], sid[N - 1];
         {
             uint32_t snat[N - 1];
-            slot_nats<N, V, MR>(P, W, lane, snat);
+            slot_nats<N, V, MR>(P, W, ln, snat);
 #pragma unroll
-            for (int r = 0; r < MR; r++) mid[r] = nat_lookup(P, msg_nat<N, V, MR>(P, W, r, lane));
+            for (int r = 0; r < MR; r++) mid[r] = nat_lookup(P, msg_nat<N, V, MR>(P, W, r, ln));
 #pragma unroll
             for (int i = 0; i < N - 1; i++) sid[i] = nat_lookup(P, snat[i]);
         }
 #pragma unroll
         for (int r = 0; r < MR; r++)
-            eval_msg<N, V, MR, BFV>(P, W, ids, r, lane, cand[r], cand[BFV ? MR + 1 + r : r], akey,
-                                    &sAinf[(r * 64 + lane) * S::NADD], mid[r]);
-        eval_slot<N, V, MR>(P, W, ids, lane, cand[MR], &sAinf[(MR * 64 + lane) * S::NADD], sid);
+            eval_msg<N, V, MR, BFV>(P, W, r, ln, cand[r], cand[BFV ? MR + 1 + r : r], akey,
+                                    HASH ? &sAinf[(r * 64 + ln) * S::NADD] : nullptr, mid[r]);
+        eval_slot<N, V, MR>(P, W, ln, cand[MR], HASH ? &sAinf[(MR * 64 + ln) * S::NADD] : nullptr, sid);
         if constexpr (PREM) {
             if (more) fetch_msgs<N, V, MR>(P, nrw0, nrw1, lane, pm);
         } else {
@@ -1544,15 +1453,13 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
                 if (lane == 0) atomicMin(&P.err[ERR_ASSERT], (((unsigned long long)p << 16) | best) << 8);
             }
         }
-        if (MODE == M_FUSED) {
-            if (lane == 0) {
-                P.cnt[pl] = total;
-                if (MODE == M_FUSED) P.pnm[pl] = W.nm;
-                if (total == 0 && !am && P.check_deadlock) atomicMin(&P.err[ERR_DEADLOCK], ((unsigned long long)p << 16) << 8);
-            }
+        if (MODE != M_SINGLE && lane == 0) {
+            P.cnt[pl] = total;
+            P.pnm[pl] = W.nm;
+            if (total == 0 && !am && P.check_deadlock) atomicMin(&P.err[ERR_DEADLOCK], ((unsigned long long)p << 16) << 8);
         }
         PHASE(2);
-        if (MODE == M_FUSED) {
+        if (MODE != M_SINGLE) {
             // stage every enabled successor at its slot q: the acting row and the added message ids
             // -- commit rebuilds the state from the parent's core and merges the ids
 #pragma unroll
@@ -1563,294 +1470,183 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
             }
         }
         PHASE(3);
-        if (SUMS) {
-            const int np = P.t.np;
-            if (!SIG) {
-                // (a) parent row terms Rt[f][p][s] = Z_f(pi(s), U[s]) + sum_j Z_f(pi(s), pi(j), X_f[s][j])
-                //     and their per-permutation totals Tt[f][p]  (structured hash, rmc_spec.h)
-                for (int idx = lane; idx < np * N; idx += 64) {
-                    const int pp = idx / N;
-                    const uint32_t sv = (uint32_t)(idx - pp * N);
-                    const uint32_t imgs = pimg[idx];
-                    const uint32_t mirow = pcore[Lo::W_MI + sv], nirow = pcore[Lo::W_NI + sv];
-                    const uint64_t u = own_word<N>(W.c[Lo::W_VF], W.c[Lo::W_CT], W.c[Lo::W_ROLE], W.c[Lo::W_CI],
-                                                   W.c[Lo::W_LL], pcore[Lo::W_LOG + sv], mirow, nirow, sv);
-                    uint64_t r0 = mix64(u ^ sdS[0][imgs]), r1 = mix64(u ^ sdS[1][imgs]);
-                    const uint32_t vfs = nib(W.c[Lo::W_VF], sv);
-#pragma unroll
-                    for (int j = 0; j < N; j++) {
-                        if ((uint32_t)j == sv) continue;
-                        const uint64_t sm = pair_small(mirow, nirow, vfs, j);
-                        const uint32_t q = imgs * N + pimg[pp * N + j];
-                        r0 += mix64((M0[sv * N + j] ^ (sm * PAIR_K0)) ^ sdP[0][q]);
-                        r1 += mix64((M1[sv * N + j] ^ (sm * PAIR_K1)) ^ sdP[1][q]);
-                    }
-                    Rt[0][idx] = r0;
-                    Rt[1][idx] = r1;
-                }
-            } else {
-                // (a') the parent's per-server inputs and signatures (lane t = server t)
-                if (lane < N) {
-                    const uint32_t t = (uint32_t)lane;
-                    const uint32_t mirow = pcore[Lo::W_MI + t], nirow = pcore[Lo::W_NI + t];
-                    const uint64_t u = own_word<N>(W.c[Lo::W_VF], W.c[Lo::W_CT], W.c[Lo::W_ROLE], W.c[Lo::W_CI],
-                                                   W.c[Lo::W_LL], pcore[Lo::W_LOG + t], mirow, nirow, t);
-                    const uint32_t vft = nib(W.c[Lo::W_VF], t);
-                    pU[t] = u;
-                    uint64_t sg = sig_part_u(u);
-#pragma unroll
-                    for (int j = 0; j < N; j++) {
-                        const uint64_t sm = pair_small(mirow, nirow, vft, j);
-                        const uint64_t x0 = M0[t * N + j] ^ (sm * PAIR_K0);
-                        pX[0][t * N + j] = x0;
-                        pX[1][t * N + j] = M1[t * N + j] ^ (sm * PAIR_K1);
-                        if ((uint32_t)j != t) sg += sig_part_x(x0);
-                    }
-                    psig[t] = sg;
-                }
-                __syncthreads();
-            }
-            // (b) every enabled successor writes its acting row to LDS slot rank
-            if constexpr (CPT) {
-#pragma unroll
-                for (int r = 0; r < NC; r++) {
-                    if (cand[r].key == KEY_NONE) continue;
-                    const Succ<N, V, MR> &o = cand[r];
-                    const uint32_t sl = rank[r];
-                    const uint32_t vfs = nib(o.c[Lo::W_VF], o.s);
-                    sU[sl] = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI], o.c[Lo::W_LL],
-                                         o.lw, o.mirow, o.nirow, o.s);
-                    sS[sl] = (uint8_t)o.s;
-                    sNa[sl] = (uint8_t)o.nadd;
-                    sCp[sl] = o.mirow | (o.nirow << 12) | (vfs << 24);  // rows of N <= 3 nibbles
-                    sCa[sl] = (uint16_t)(((r <= MR ? r : 0) * 64 + lane) * S::NADD);
-                }
-                __syncthreads();
-                for (uint32_t l = (uint32_t)lane; l < total; l += 64) {
-                    const uint32_t sv = sS[l], cp = sCp[l];
-                    const uint32_t mirow = cp & 0xFFFu, nirow = (cp >> 12) & 0xFFFu, vfs = cp >> 24;
-                    uint64_t row0[N], row1[N];
-                    succ_row_at<N, V, MR>(sv, sNa[l], M0, M1, &sAinf[sCa[l]], row0, row1);
-#pragma unroll
-                    for (int j = 0; j < N; j++) {
-                        const uint64_t sm = pair_small(mirow, nirow, vfs, j);
-                        sX[0][l * N + j] = row0[j] ^ (sm * PAIR_K0);
-                        sX[1][l * N + j] = row1[j] ^ (sm * PAIR_K1);
-                    }
-                }
-            }
-            if constexpr (SIG) {
-                // stage each successor's row inputs by its TLC rank; the batches below build its hash rows
-                // and signature ranks a lane per successor, 64 successors at a time
-#pragma unroll
-                for (int r = 0; r < NC; r++) {
-                    if (cand[r].key == KEY_NONE) continue;
-                    const Succ<N, V, MR> &o = cand[r];
-                    const uint32_t g = rank[r];
-                    const uint32_t vfs = nib(o.c[Lo::W_VF], o.s);
-                    sUg[g] = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI], o.c[Lo::W_LL],
-                                         o.lw, o.mirow, o.nirow, o.s);
-                    sW1[g] = o.mirow | (vfs << 20);  // rows of N <= 5 nibbles
-                    sW2[g] = o.nirow;
-                    sCa[g] = (uint16_t)(((r <= MR ? r : 0) * 64 + lane) * S::NADD);
-                    sS[g] = (uint8_t)o.s;
-                    sNa[g] = (uint8_t)o.nadd;
-                }
-            } else if constexpr (!CPT) {
-#pragma unroll
-            for (int r = 0; r < NC; r++) {
-                if (cand[r].key == KEY_NONE) continue;
-                const Succ<N, V, MR> &o = cand[r];
-                const uint32_t sl = rank[r];
-                uint64_t row0[N], row1[N];
-                // BecomeFollower candidates (r > MR) add no messages: their info words are never read
-                succ_row<N, V, MR>(o, M0, M1, &sAinf[((r <= MR ? r : 0) * 64 + lane) * S::NADD], row0, row1);
-                const uint32_t vfs = nib(o.c[Lo::W_VF], o.s);
-                const uint64_t u = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI],
-                                               o.c[Lo::W_LL], o.lw, o.mirow, o.nirow, o.s);
-                sU[sl] = u;
-#pragma unroll
-                for (int j = 0; j < N; j++) {
-                    const uint64_t sm = pair_small(o.mirow, o.nirow, vfs, j);
-                    sX[0][sl * N + j] = row0[j] ^ (sm * PAIR_K0);
-                    sX[1][sl * N + j] = row1[j] ^ (sm * PAIR_K1);
-                }
-                sS[sl] = (uint8_t)o.s;
-                sNa[sl] = (uint8_t)o.nadd;
-            }
-            }
-            __syncthreads();
-            // the successor's fingerprint: seen-set probe + election (fused), or the hash pass output
-            PHASE(4);
-            auto emit = [&](uint32_t lo, ulonglong2 best) {
-                const ulonglong2 f = make_ulonglong2(best.x | 1ull, best.y);
-                if (MODE == M_FUSED) {
-                    // the seen set is read-only in this launch (commit inserts)
-                    const uint64_t q = pl * (uint64_t)MX + lo;
-                    P.fp[q] = f;
-                    if (P.route) return;  // sharded round: the fingerprint's owner probes and elects
-                    const uint32_t e = ((uint32_t)sNa[lo] + (W.nm & 1u) + 1u) >> 1;
-                    if (P.split) {  // k_probe probes and elects, a lane per successor
-                        P.lslot[q] = e;
-                        return;
-                    }
-                    // the election slot's first word goes out with the seen-set probe: one
-                    // round trip fewer for a new fingerprint
-                    const uint64_t g0 = l_index(f, P.Lmask);
-                    const unsigned long long v0 =
-                        __hip_atomic_load(&P.LXY[g0].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    P.lslot[q] = seen_contains(P.seen, f)
-                                     ? LS_SEEN
-                                     : elect_slot<MX>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g0, v0);
+        if constexpr (MODE == M_SPLIT) {
+            // the parent's hash context for k_hash_probe: record words 0 .. CCW - 1 are in lanes
+            // 0 .. CCW - 1 (rec0), the message-hash sums in LDS
+            constexpr int CTXW = ctx_words<N, V>(), CC = ((S::CCW + 3) / 4) * 4;
+            uint32_t *cx = P.hctx + pl * (uint64_t)CTXW;
+            for (int k = lane; k < CTXW; k += 64) {
+                uint32_t v = 0u;
+                if (k < CC) {
+                    v = k < S::CCW ? rec0 : 0u;
                 } else {
-                    P.fp[lo] = f;
+                    const int pi = (k - CC) >> 2, part = k & 3;
+                    const int t = pi / (N - 1), jj = pi % (N - 1), j = jj < t ? jj : jj + 1;
+                    const uint64_t m = part < 2 ? M0[t * N + j] : M1[t * N + j];
+                    v = (part & 1) ? (uint32_t)(m >> 32) : (uint32_t)m;
                 }
-            };
-            if (SIG) {
-                // (c') per batch of 64 successors: one task per (successor, allowed permutation) --
-                //      exclusive scan of the coset sizes, then 64 tasks per round; a successor's tasks
-                //      are consecutive, so the first lane of each run folds the run into its minimum
-                for (uint32_t b0 = 0; b0 < total; b0 += (uint32_t)SBAT) {
-                    const uint32_t nb = total - b0 < (uint32_t)SBAT ? total - b0 : (uint32_t)SBAT;
-                    if ((uint32_t)lane < nb) {  // successor b0 + lane: hash rows, signature, coset
-                        const uint32_t l = (uint32_t)lane, g = b0 + l;
-                        const uint32_t sv = sS[g], w1 = sW1[g];
-                        const uint32_t mirow = w1 & 0xFFFFFu, vfs = w1 >> 20, nirow = sW2[g];
-                        const uint64_t u = sUg[g];
-                        uint64_t row0[N], row1[N];
-                        succ_row_at<N, V, MR>(sv, sNa[g], M0, M1, &sAinf[sCa[g]], row0, row1);
-                        sU[l] = u;
-                        uint64_t sg = sig_part_u(u);
+                cx[k] = v;
+            }
+            __syncthreads();  // M0 / M1 are cleared for the next parent
+            continue;
+        }
+        // ---- fingerprints (rmc_spec.h): content matrix, signature coset, minimum -----------------
+        // (a) the parent's content matrix, a lane per (half, row, column)
+        if (lane < 2 * N * N) {
+            const int f = lane / (N * N), t = (lane / N) % N, j = lane % N;
+            pC[f][t * N + j] = content<N>(f, (uint32_t)t, (uint32_t)j, W.c, pcore[Lo::W_LOG + t], pcore[Lo::W_MI + t],
+                                          pcore[Lo::W_NI + t], f ? M1[t * N + j] : M0[t * N + j]);
+        }
+        // (b) every enabled successor's row inputs at its TLC rank
+#pragma unroll
+        for (int r = 0; r < NC; r++) {
+            if (cand[r].key == KEY_NONE) continue;
+            const Succ<N, V, MR> &o = cand[r];
+            const uint32_t g = rank[r];
+            const uint32_t vfs = nib(o.c[Lo::W_VF], o.s);
+            sUg[g] = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI], o.c[Lo::W_LL], o.lw,
+                                 o.mirow, o.nirow, o.s);
+            sW1[g] = o.mirow | (vfs << 20);  // rows of N <= 5 nibbles
+            sW2[g] = o.nirow;
+            // (BecomeFollower candidates, r > MR, add no messages: their info words are never read)
+            sCa[g] = (uint16_t)(((r <= MR ? r : 0) * 64 + lane) * S::NADD);
+            sS[g] = (uint8_t)o.s;
+            sNa[g] = (uint8_t)o.nadd;
+        }
+        __syncthreads();
+        if (lane < N) {
+            uint64_t sg = 0;
+#pragma unroll
+            for (int j = 0; j < N; j++) sg += pC[1][lane * N + j];
+            psig[lane] = sg;
+        }
+        PHASE(4);
+        auto emit = [&](uint32_t lo, ulonglong2 best) {
+            const ulonglong2 f = make_ulonglong2(best.x | 1ull, best.y);
+            if (MODE == M_FUSED) {
+                // the seen set is read-only in this launch (commit inserts)
+                const uint64_t q = pl * (uint64_t)MX + lo;
+                P.fp[q] = f;
+                if (P.route) return;  // sharded round: the fingerprint's owner probes and elects
+                const uint32_t e = ((uint32_t)sNa[lo] + (W.nm & 1u) + 1u) >> 1;
+                // the election slot's first word goes out with the seen-set probe: one round trip
+                // fewer for a new fingerprint
+                const uint64_t g0 = l_index(f, P.Lmask);
+                const unsigned long long v0 = __hip_atomic_load(&P.LXY[g0].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                P.lslot[q] = seen_contains(P.seen, f) ? LS_SEEN
+                                                      : elect_slot<MX>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g0, v0);
+            } else {
+                P.fp[lo] = f;
+            }
+        };
+        // (c) per batch of HB successors (by TLC rank)
+        for (uint32_t b0 = 0; b0 < total; b0 += (uint32_t)HB) {
+            const uint32_t nb = total - b0 < (uint32_t)HB ? total - b0 : (uint32_t)HB;
+            {  // (c1) the acting row's contents: lane (half, successor) when FH == 2, else both halves
+                const uint32_t l = (uint32_t)lane % HB, g = b0 + l;
+                if (l < nb) {
+                    const uint32_t sv = sS[g], w1 = sW1[g], na = sNa[g];
+                    const uint32_t mirow = w1 & 0xFFFFFu, vfs = w1 >> 20, nirow = sW2[g];
+                    const uint64_t u = sUg[g];
+                    const uint32_t *ai = &sAinf[sCa[g]];
+#pragma unroll
+                    for (int fi = 0; fi < 3 - FH; fi++) {
+                        const int f = FH == 2 ? lane / HB : fi;
+                        uint64_t row[N];
+#pragma unroll
+                        for (int j = 0; j < N; j++) row[j] = f ? M1[sv * N + j] : M0[sv * N + j];
+#pragma unroll
+                        for (int a = 0; a < S::NADD; a++) {
+                            if ((uint32_t)a >= na) break;
+                            const uint32_t inf = ai[a];
+                            const uint32_t dst = mi_dst(inf);
+                            const uint64_t h = msg_hash_half(inf, f);
+#pragma unroll
+                            for (int j = 0; j < N; j++) row[j] += ((uint32_t)j == dst) ? h : 0ull;
+                        }
+                        sC[f][l * N + sv] = cmix_own(u, f);
 #pragma unroll
                         for (int j = 0; j < N; j++) {
-                            const uint64_t sm = pair_small(mirow, nirow, vfs, j);
-                            const uint64_t x0 = row0[j] ^ (sm * PAIR_K0);
-                            sX[0][l * N + j] = x0;
-                            sX[1][l * N + j] = row1[j] ^ (sm * PAIR_K1);
-                            if ((uint32_t)j != sv) sg += sig_part_x(x0);
-                        }
-                        // only the acting server's row changes (every message it adds is its own)
-                        uint64_t sig[N];
-#pragma unroll
-                        for (int t = 0; t < N; t++) sig[t] = (uint32_t)t == sv ? sg : psig[t];
-                        const uint32_t rk = coset_ranks<N>(sig);
-                        sRk[l] = rk;
-                        sKoff[l] = coset_size<N>(rk);
-                        sBest[l] = make_ulonglong2(~0ull, ~0ull);
-                    }
-                    __syncthreads();
-                    uint32_t ntask = 0;
-                    {
-                        const uint32_t l = (uint32_t)lane;
-                        uint32_t rt;
-                        const uint32_t ex = wave_excl_scan(l < nb ? sKoff[l] : 0u, lane, &rt);
-                        if (l < nb) sKoff[l] = ex;
-                        ntask = rt;
-                    }
-                    __syncthreads();
-                    for (uint32_t tb = 0; tb < ntask; tb += 64) {
-                        const uint32_t ti = tb + (uint32_t)lane;
-                        uint32_t l = 0xFFFFFFFFu;
-                        ulonglong2 h = make_ulonglong2(~0ull, ~0ull);
-                        if (ti < ntask) {
-                            uint32_t a = 0, b = nb;  // sKoff[a] <= ti < sKoff[b]
-                            while (b - a > 1) {
-                                const uint32_t m = (a + b) >> 1;
-                                if (sKoff[m] <= ti) a = m; else b = m;
-                            }
-                            l = a;
-                            uint32_t img[N];
-                            coset_img<N>(sRk[l], ti - sKoff[l], img);
-                            const uint32_t sv = sS[b0 + l];
-                            const uint64_t su = sU[l];
-                            h = hash_at<N>(
-                                img, [&](int t) { return (uint32_t)t == sv ? su : pU[t]; },
-                                [&](int f, int t, int j) {
-                                    return (uint32_t)t == sv ? sX[f][l * N + j] : pX[f][t * N + j];
-                                },
-                                [&](int f, uint32_t x) { return sdS[f][x]; },
-                                [&](int f, uint32_t x, uint32_t y) { return sdP[f][x * N + y]; });
-                        }
-                        sPart[lane] = h;
-                        sTl[lane] = l;
-                        __syncthreads();
-                        if (ti < ntask && (lane == 0 || sTl[lane - 1] != l)) {
-                            ulonglong2 best = sBest[l];
-                            for (int j = lane; j < 64 && sTl[j] == l; j++)
-                                if (lex_less(sPart[j], best)) best = sPart[j];
-                            sBest[l] = best;
-                        }
-                        __syncthreads();
-                    }
-                    PHASE(5);
-                    if ((uint32_t)lane < nb) emit(b0 + (uint32_t)lane, sBest[lane]);
-                    __syncthreads();
-                    PHASE(6);
-                }
-            } else {
-                for (int pp = lane; pp < np; pp += 64) {
-                    uint64_t t0 = 0, t1 = 0;
-#pragma unroll
-                    for (int q = 0; q < N; q++) { t0 += Rt[0][pp * N + q]; t1 += Rt[1][pp * N + q]; }
-                    Tt[0][pp] = t0;
-                    Tt[1][pp] = t1;
-                }
-                __syncthreads();
-                // (c) one (successor l, permutation block b) task per lane: the lane takes the minimum
-                //     over permutations b, b + PB, ... of (parent total - old row + new row), and the PB
-                //     partial minima of a successor meet in LDS.  PB = 64 / total (at most |perms|)
-                //     keeps all 64 lanes busy when a parent has few successors -- the common case.
-                const uint32_t npu = (uint32_t)np;
-                uint32_t PB = 1;
-                if (total > 0 && total < 64) PB = min(64u / total, npu);
-                const uint32_t SB = 64u / PB;  // successors per round
-                const uint32_t li = (uint32_t)lane / PB, blk = (uint32_t)lane - li * PB;
-                for (uint32_t b0 = 0; b0 < total; b0 += SB) {
-                    const uint32_t l = b0 + li;
-                    uint64_t m0 = ~0ull, m1 = ~0ull;
-                    if (li < SB && l < total) {
-                        const uint32_t sv = sS[l];
-                        const uint64_t u = sU[l];
-                        uint64_t x0[N], x1[N];
-#pragma unroll
-                        for (int j = 0; j < N; j++) { x0[j] = sX[0][l * N + j]; x1[j] = sX[1][l * N + j]; }
-                        for (uint32_t pp = blk; pp < npu; pp += PB) {
-                            uint32_t img[N];
-#pragma unroll
-                            for (int j = 0; j < N; j++) img[j] = pimg[pp * N + j];
-                            uint32_t imgs = img[0];
-#pragma unroll
-                            for (int j = 1; j < N; j++) imgs = ((uint32_t)j == sv) ? img[j] : imgs;
-                            uint64_t h0 = Tt[0][pp] - Rt[0][pp * N + sv] + mix64(u ^ sdS[0][imgs]);
-                            uint64_t h1 = Tt[1][pp] - Rt[1][pp * N + sv] + mix64(u ^ sdS[1][imgs]);
-#pragma unroll
-                            for (int j = 0; j < N; j++) {
-                                if ((uint32_t)j == sv) continue;
-                                const uint32_t q = imgs * N + img[j];
-                                h0 += mix64(x0[j] ^ sdP[0][q]);
-                                h1 += mix64(x1[j] ^ sdP[1][q]);
-                            }
-                            if (h1 < m1 || (h1 == m1 && h0 < m0)) { m1 = h1; m0 = h0; }
+                            if ((uint32_t)j == sv) continue;
+                            const uint64_t sm = pair_small(mirow, nirow, vfs, (uint32_t)j);
+                            sC[f][l * N + j] = cmix_pair(row[j] ^ (sm * (f ? PAIR_K1 : PAIR_K0)), f);
                         }
                     }
-                    sPart[lane] = make_ulonglong2(m0, m1);
-                    __syncthreads();
-                    PHASE(5);
-                    const uint32_t lo = b0 + (uint32_t)lane;
-                    if ((uint32_t)lane < SB && lo < total) {
-                        ulonglong2 best = sPart[lane * PB];
-                        for (uint32_t k = 1; k < PB; k++) {
-                            const ulonglong2 v = sPart[lane * PB + k];
-                            if (lex_less(v, best)) best = v;
-                        }
-                        emit(lo, best);
-                    }
-                    __syncthreads();
-                    PHASE(6);
                 }
             }
+            __syncthreads();
+            if ((uint32_t)lane < nb) {  // (c2) signatures, tie ranks and coset size per successor
+                const uint32_t l = (uint32_t)lane, sv = sS[b0 + l];
+                uint64_t rs = 0;
+#pragma unroll
+                for (int j = 0; j < N; j++) rs += sC[1][l * N + j];
+                uint64_t sig[N];
+#pragma unroll
+                for (int t = 0; t < N; t++) sig[t] = (uint32_t)t == sv ? rs : psig[t];
+                const uint32_t rk = P.t.np > 1 ? coset_ranks<N>(sig) : coset_ident<N>();
+                sRk[l] = rk;
+                sKoff[l] = coset_size<N>(rk);
+                sBest[l] = make_ulonglong2(~0ull, ~0ull);
+            }
+            __syncthreads();
+            uint32_t ntask = 0;
+            {
+                const uint32_t l = (uint32_t)lane;
+                uint32_t rt;
+                const uint32_t ex = wave_excl_scan(l < nb ? sKoff[l] : 0u, lane, &rt);
+                if (l < nb) sKoff[l] = ex;
+                ntask = rt;
+            }
+            __syncthreads();
+            PHASE(5);
+            // (c3) one task per (successor, allowed permutation), 64 per round; a successor's tasks
+            //      are consecutive, so the first lane of each run folds the run into its minimum
+            for (uint32_t tb = 0; tb < ntask; tb += 64) {
+                const uint32_t ti = tb + (uint32_t)lane;
+                uint32_t l = 0xFFFFFFFFu;
+                ulonglong2 h = make_ulonglong2(~0ull, ~0ull);
+                if (ti < ntask) {
+                    uint32_t a = 0, b = nb;  // sKoff[a] <= ti < sKoff[b]
+                    while (b - a > 1) {
+                        const uint32_t m = (a + b) >> 1;
+                        if (sKoff[m] <= ti) a = m; else b = m;
+                    }
+                    l = a;
+                    const uint32_t imgw = coset_img<N>(sRk[l], ti - sKoff[l]);
+                    const uint32_t sv = sS[b0 + l];
+                    // a row per iteration (not unrolled: the LDS operands of every row at once
+                    // would spill); the acting row from the batch, the others from the parent
+                    uint64_t h0 = 0, h1 = 0;
+#pragma unroll 1
+                    for (uint32_t t = 0; t < (uint32_t)N; t++) {
+                        const uint32_t it = (imgw >> (3 * t)) & 7u;
+                        const uint64_t *r0 = t == sv ? &sC[0][l * N] : &pC[0][t * N];
+                        const uint64_t *r1 = t == sv ? &sC[1][l * N] : &pC[1][t * N];
+#pragma unroll
+                        for (int j = 0; j < N; j++) {
+                            const uint32_t ij = (imgw >> (3 * j)) & 7u;
+                            h0 += r0[j] * sK[0][it * N + ij];
+                            h1 += r1[j] * sK[1][it * N + ij];
+                        }
+                    }
+                    h = make_ulonglong2(h0, h1);
+                }
+                sPart[lane] = h;
+                sTl[lane] = l;
+                __syncthreads();
+                if (ti < ntask && (lane == 0 || sTl[lane - 1] != l)) {
+                    ulonglong2 best = sBest[l];
+                    for (int j = lane; j < 64 && sTl[j] == l; j++)
+                        if (lex_less(sPart[j], best)) best = sPart[j];
+                    sBest[l] = best;
+                }
+                __syncthreads();
+            }
+            PHASE(6);
+            if ((uint32_t)lane < nb) emit(b0 + (uint32_t)lane, sBest[lane]);
+            __syncthreads();
+            PHASE(5);
         }
-        PHASE(5);
         asm volatile("" ::"v"(nnstart));  // the offset two parents ahead is in by now: keep its load up top
         if (MODE == M_FUSED) continue;
         // SINGLE: every successor, in TLC order
@@ -1870,15 +1666,9 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((
     PHASE_FLUSH;
 }
 
-// Split probe of a host-driven chunk: the expansion (P.split) wrote every successor's fingerprint
-// fp[q] and its extra record words e in lslot[q]; here each successor gets a lane of its own for the
-// seen-set probe and the election (elect_slot, the same protocol as the fused pass), so a wave keeps
-// 64 independent probe chains in flight instead of the ~5 of one parent.  A wave takes 64
-// consecutive parents: their successor counts are scanned across the wave and successor i of the
-// group goes to lane i % 64 of round i / 64 (its parent found by a binary search over the scan).
-// Successor slot q of every successor of the chunk, a lane each: a wave takes 64 consecutive
-// parents, their successor counts are scanned across the wave and successor i of the group goes to
-// lane i % 64 of round i / 64 (its parent found by a binary search over the scan).
+// Every successor slot of a split chunk, a lane each: a wave takes 64 consecutive parents, their
+// successor counts are scanned across the wave and successor i of the group goes to lane i % 64 of
+// round i / 64 (its parent found by a binary search over the scan); f(parent pl, rank r).
 template <int MX, class F>
 __device__ __forceinline__ void each_successor(const KParams &P, F &&f) {
     const int lane = threadIdx.x & 63;
@@ -1900,20 +1690,96 @@ __device__ __forceinline__ void each_successor(const KParams &P, F &&f) {
                 j = v <= i ? j + st : j;
             }
             const uint32_t exj = (uint32_t)__shfl(ex, j, 64);
-            if (i < tot) f((g0 + (uint64_t)j) * (uint64_t)MX + (i - exj));
+            if (i < tot) f(g0 + (uint64_t)j, i - exj);
         }
     }
 }
 
-// Split probe of a host-driven chunk: the expansion (P.split) wrote every successor's fingerprint
-// fp[q] and its extra record words e in lslot[q]; here each successor gets a lane of its own for the
-// seen-set probe and the election (elect_slot, the same protocol as the fused pass), so a wave keeps
-// 64 independent probe chains in flight instead of the ~5 of one parent.
-template <int MX>
-__global__ __launch_bounds__(256) void k_probe(KParams P) {
-    each_successor<MX>(P, [&](uint64_t q) {
-        const ulonglong2 f = P.fp[q];
-        const uint32_t e = P.lslot[q];
+// Split chunk: every successor's fingerprint, seen-set probe and election, a lane per successor.
+// The expansion (M_SPLIT) left each parent's hash context (its packed core and its message-hash
+// sums per server pair, ctx_words) and each successor's staged row; the successor's content
+// matrix is rebuilt from those (rmc_spec.h), its coset minimum taken, and the fingerprint probed
+// and elected with the fused pass's protocol (elect_slot) -- 64 independent chains per wave instead
+// of the ~5 of one parent, and the hash at full lane occupancy.  A sharded round (P.route) only
+// needs the fingerprints: its owners probe and elect.
+template <int N, int V, int MR, int MX>
+__global__ __launch_bounds__(256) void k_hash_probe(KParams P) {
+    using S = Spec<N, V, MR>;
+    using Lo = Layout<N, V>;
+    constexpr int CTXW = ctx_words<N, V>(), CC4 = (S::CCW + 3) / 4;
+    __shared__ uint64_t sK[2][N * N];
+    if (threadIdx.x < 2 * N * N) {
+        const int f = threadIdx.x / (N * N), a = (threadIdx.x / N) % N, b = threadIdx.x % N;
+        sK[f][a * N + b] = P.t.seeds[f * SEEDS_PER_F + a * MAXN + b];
+    }
+    __syncthreads();
+    each_successor<MX>(P, [&](uint64_t pl, uint32_t r) {
+        const uint64_t q = pl * (uint64_t)MX + r;
+        const uint4 *cx = reinterpret_cast<const uint4 *>(P.hctx + pl * (uint64_t)CTXW);
+        const uint4 *st = P.score + q * (uint64_t)S::SW4;
+        const uint4 sa = st[0], sb = st[1];
+        const uint4 sc = S::SW4 > 2 ? st[2] : make_uint4(0u, 0u, 0u, 0u);
+        uint32_t pk[CC4 * 4];
+#pragma unroll
+        for (int k = 0; k < CC4; k++) {
+            const uint4 v = cx[k];
+            pk[4 * k] = v.x; pk[4 * k + 1] = v.y; pk[4 * k + 2] = v.z; pk[4 * k + 3] = v.w;
+        }
+        uint4 mp[N * (N - 1)];
+#pragma unroll
+        for (int k = 0; k < N * (N - 1); k++) mp[k] = cx[CC4 + k];
+        uint32_t pc[Lo::NW], c[Lo::NW];
+        decode_core<N, V>(pk, pc);
+        unstage_core<N, V>(pc, sa, sb, c);
+        const uint32_t sv = sa.x >> 20, nadd = sb.z >> 16;
+        // the added messages' hashes toward each destination (all from the acting server)
+        uint64_t ad0[N], ad1[N];
+#pragma unroll
+        for (int j = 0; j < N; j++) { ad0[j] = 0; ad1[j] = 0; }
+        const uint32_t aid[4] = {sb.w & 0xFFFFu, sb.w >> 16, sc.x & 0xFFFFu, sc.x >> 16};
+#pragma unroll
+        for (int a = 0; a < S::NADD; a++) {
+            if ((uint32_t)a >= nadd) break;
+            const uint32_t inf = P.t.info[aid[a]];
+            const ulonglong2 g = P.t.gmsg[aid[a]];
+            const uint32_t d = mi_dst(inf);
+#pragma unroll
+            for (int j = 0; j < N; j++) {
+                ad0[j] += (uint32_t)j == d ? g.x : 0ull;
+                ad1[j] += (uint32_t)j == d ? g.y : 0ull;
+            }
+        }
+        // the successor's content matrix and its servers' signatures
+        uint64_t C0[N * N], C1[N * N], sig[N];
+#pragma unroll
+        for (int t = 0; t < N; t++) {
+            sig[t] = 0;
+#pragma unroll
+            for (int j = 0; j < N; j++) {
+                uint64_t m0 = 0, m1 = 0;
+                if (t != j) {
+                    const uint4 m = mp[pair_index(N, t, j)];
+                    m0 = ((uint64_t)m.y << 32 | m.x) + ((uint32_t)t == sv ? ad0[j] : 0ull);
+                    m1 = ((uint64_t)m.w << 32 | m.z) + ((uint32_t)t == sv ? ad1[j] : 0ull);
+                }
+                C0[t * N + j] = content<N>(0, t, j, c, c[Lo::W_LOG + t], c[Lo::W_MI + t], c[Lo::W_NI + t], m0);
+                C1[t * N + j] = content<N>(1, t, j, c, c[Lo::W_LOG + t], c[Lo::W_MI + t], c[Lo::W_NI + t], m1);
+                sig[t] += C1[t * N + j];
+            }
+        }
+        const uint32_t rk = P.t.np > 1 ? coset_ranks<N>(sig) : coset_ident<N>(), K = coset_size<N>(rk);
+        ulonglong2 best = make_ulonglong2(~0ull, ~0ull);
+        for (uint32_t k = 0; k < K; k++) {
+            const ulonglong2 h = hash_at<N>(
+                coset_img<N>(rk, k), [&](int f, int a, int b) { return f ? C1[a * N + b] : C0[a * N + b]; },
+                [&](int f, uint32_t a, uint32_t b) { return sK[f][a * N + b]; });
+            if (lex_less(h, best)) best = h;
+        }
+        const ulonglong2 f = make_ulonglong2(best.x | 1ull, best.y);
+        P.fp[q] = f;
+        if (P.route) return;
+        const uint32_t nm = (pc[Lo::W_MISC] >> 16) & 0xFFu;
+        const uint32_t e = (nadd + (nm & 1u) + 1u) >> 1;  // record words a winner adds (elect_key)
         const uint64_t g = l_index(f, P.Lmask);
         const unsigned long long v0 = __hip_atomic_load(&P.LXY[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         P.lslot[q] = seen_contains(P.seen, f) ? LS_SEEN
@@ -1927,7 +1793,8 @@ __global__ __launch_bounds__(256) void k_probe(KParams P) {
 // dependent round trips per parent with winners
 template <int MX>
 __global__ __launch_bounds__(256) void k_insert_winners(KParams P) {
-    each_successor<MX>(P, [&](uint64_t q) {
+    each_successor<MX>(P, [&](uint64_t pl, uint32_t r) {
+        const uint64_t q = pl * (uint64_t)MX + r;
         const uint32_t g = P.lslot[q];
         if (g >= LS_ELECT) return;
         const bool w = elect_q(P.L[g]) == (uint32_t)q;
@@ -1940,17 +1807,13 @@ __global__ __launch_bounds__(256) void k_insert_winners(KParams P) {
 template <int N, int V, int MR>
 __global__ __launch_bounds__(64) void k_fp_states(KParams P, uint64_t n) {
     using S = Spec<N, V, MR>;
-    __shared__ uint16_t ids[S::MCAP];
     __shared__ uint64_t M0[N * N], M1[N * N];
     __shared__ uint32_t pcore[Layout<N, V>::NW + N];
     const int lane = threadIdx.x;
     for (uint64_t p = blockIdx.x; p < n; p += gridDim.x) {
         Wave<N, V, MR> W;
-        load_parent<N, V, MR, true>(P, rec_start<S::RECW_MAX>(P, p), lane, W, ids, M0, M1, pcore);
-        uint64_t row0[N], row1[N];
-#pragma unroll
-        for (int j = 0; j < N; j++) { row0[j] = 0; row1[j] = 0; }
-        const ulonglong2 f = fingerprint<N, V>(W.c, -1, row0, row1, M0, M1, P.t);
+        load_parent<N, V, MR, true>(P, rec_start<S::RECW_MAX>(P, p), lane, W, M0, M1, pcore);
+        const ulonglong2 f = fingerprint<N, V>(W.c, M0, M1, P.t);
         if (lane == 0) P.fp[p] = f;
     }
 }
@@ -2250,9 +2113,9 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
     // offsets, successor count and first 64 election slots (read ahead of knowing whether they are
     // needed; all in bounds; commit always reads a ring level: foff is set).  The header's uniform
     // words travel in one VGPR: lane k loads word k (one load instruction for all of them, two
-    // registers per header in flight instead of ten).  RMC_COMMIT_PREFETCH: software pipeline --
-    // the next parent's header goes out with this parent's record, so its round trip overlaps this
-    // one's instead of starting the next iteration.
+    // registers per header in flight instead of ten).  Software pipeline: the next parent's header
+    // goes out with this parent's record, so its round trip overlaps this one's instead of starting
+    // the next iteration.
     struct Hdr {
         uint32_t hw, g0;
     };
@@ -2277,38 +2140,22 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
     // the parents this pass visits: k-th -> level-local index (a split chunk: only those with winners)
     const uint64_t nvis = P.plist ? (uint64_t)P.sum[SUM_NZ] : P.p_end - P.p_begin;
     auto parent_at = [&](uint64_t k) -> uint64_t { return P.p_begin + (P.plist ? (uint64_t)P.plist[k] : k); };
-#if RMC_COMMIT_PREFETCH
-    // (RMC_COMMIT_PREFETCH 2: two headers ahead, so a run of parents without winners -- each only a
-    // header wait -- pays half a round trip per parent).  pq: the parents of k, k + grid, k + 2 grid
-    Hdr nh{}, nnh{};
+    // pq: the parents of k, k + grid, k + 2 grid
+    Hdr nh{};
     uint64_t pq[3] = {0, 0, 0};
 #pragma unroll
     for (int j = 0; j < 3; j++)
         if (blockIdx.x + (uint64_t)j * gridDim.x < nvis) pq[j] = parent_at(blockIdx.x + (uint64_t)j * gridDim.x);
     if (blockIdx.x < nvis) nh = header(pq[0]);
-    if (RMC_COMMIT_PREFETCH > 1 && blockIdx.x + gridDim.x < nvis) nnh = header(pq[1]);
-#endif
     PHASE_DECL
     for (uint64_t k = blockIdx.x; k < nvis; k += gridDim.x) {
-#if RMC_COMMIT_PREFETCH
         const uint64_t p = pq[0];
         pq[0] = pq[1];
         pq[1] = pq[2];
         pq[2] = k + 3ull * gridDim.x < nvis ? parent_at(k + 3ull * gridDim.x) : 0ull;
-#else
-        const uint64_t p = parent_at(k);
-#endif
         const uint64_t pl = p - P.p_begin;
-#if RMC_COMMIT_PREFETCH > 1
-        const Hdr h = nh;
-        nh = nnh;
-        if (k + 2ull * gridDim.x < nvis) nnh = header(pq[1]);
-#elif RMC_COMMIT_PREFETCH
         const Hdr h = nh;
         if (k + gridDim.x < nvis) nh = header(pq[0]);
-#else
-        const Hdr h = header(p);
-#endif
         const uint32_t g0 = h.g0;
         const uint32_t wc = rdlane(h.hw, 2);
         PHASE(0);
@@ -2330,17 +2177,11 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
         // round the owner's verdict is already known): a speculative read instead of a third round
         // trip once the election words are in
         uint4 xa = make_uint4(0u, 0u, 0u, 0u), xb = xa, xc = xa;
-#if RMC_COMMIT_EARLY
-        ulonglong2 xf = make_ulonglong2(0ull, 0ull);  // and their fingerprints (the seen-set insert)
-#endif
         if ((uint32_t)lane < t && (verdict ? g0 == LS_WIN : g0 < LS_ELECT)) {
             const uint4 *src = P.score + (pl * (uint64_t)MX + (uint32_t)lane) * (uint64_t)S::SW4;
             xa = src[0];
             xb = src[1];
             if (S::SW4 > 2) xc = src[2];
-#if RMC_COMMIT_EARLY
-            if (!P.route) xf = P.fp[pl * (uint64_t)MX + (uint32_t)lane];
-#endif
         }
         uint32_t pc[Lo::NW], ppk[S::CCW];
 #pragma unroll
@@ -2378,11 +2219,6 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
             uint32_t pk[S::CCW];
             uint4 sa = make_uint4(0u, 0u, 0u, 0u), sb = sa, sc = sa;
             uint32_t size = 0;
-#if RMC_COMMIT_EARLY
-            ulonglong2 fi = make_ulonglong2(0ull, 0ull);
-            uint64_t hi = 0;
-            unsigned long long prev = 0ull;
-#endif
 #pragma unroll
             for (int w = 0; w < S::CCW; w++) pk[w] = 0u;
             if (win) {
@@ -2409,12 +2245,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
                     P.xside[out] = make_uint4((uint32_t)pref, (uint32_t)(pref >> 32), key, size);
                 } else {
                     const uint64_t gid = P.gid_next_base + out;
-#if RMC_COMMIT_EARLY
-                    fi = r0 == 0 ? xf : P.fp[q];
-                    hi = seen_insert_begin(P.seen, fi, &prev);  // resolved after the record is out
-#else
                     if (!(P.split & 2)) seen_insert(P.seen, P.fp[q]);  // (split chunk: k_insert_winners)
-#endif
                     P.par[gid - P.trace_base] = P.gid_parent_base + p;
                     P.pslot[gid - P.trace_base] = (uint16_t)key;
                 }
@@ -2449,9 +2280,6 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
                 const uint32_t add[4] = {ay & 0xFFFFu, ay >> 16, az & 0xFFFFu, az >> 16};
                 write_ids<N, V, MR>(P.next, ring_wrap(rstart + S::CCW, P.rcap), P.rcap, id, nm, add, nadd, lane);
             }
-#if RMC_COMMIT_EARLY
-            if (win && !P.route) seen_insert_end(P.seen, fi, hi, prev);
-#endif
             done += (uint32_t)__popcll(m);
             done_w += wtot;
             PHASE(5);
@@ -2471,7 +2299,8 @@ static inline unsigned grid_for(uint64_t n) {
 
 template <int N, int V, int MR, bool BFV = false>
 struct Launch {
-    static size_t bm_bytes(const KParams &P) { return RMC_MSG_BITMAP ? (size_t)P.t.bmw * 4 : 0; }
+    static constexpr int MX = Spec<N, V, MR>::MAXS + (BFV ? Spec<N, V, MR>::MCAP : 0);
+    static size_t bm_bytes(const KParams &P) { return (size_t)P.t.bmw * 4; }
     static void single(const KParams &P, hipStream_t s) {
         hipLaunchKernelGGL((k_expand<N, V, MR, M_SINGLE, BFV>), dim3(1), dim3(64), bm_bytes(P), s, P);
     }
@@ -2479,14 +2308,16 @@ struct Launch {
         hipLaunchKernelGGL((k_expand<N, V, MR, M_FUSED, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64),
                            bm_bytes(P), s, P);
     }
-    static void probe(const KParams &P, uint64_t np, hipStream_t s) {
-        constexpr int MX = Spec<N, V, MR>::MAXS + (BFV ? Spec<N, V, MR>::MCAP : 0);
+    static void split(const KParams &P, hipStream_t s) {
+        hipLaunchKernelGGL((k_expand<N, V, MR, M_SPLIT, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64),
+                           bm_bytes(P), s, P);
+    }
+    static void hash_probe(const KParams &P, uint64_t np, hipStream_t s) {
         const uint64_t blocks = (np + 255) / 256;  // four one-group waves per block
-        hipLaunchKernelGGL((k_probe<MX>), dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u), dim3(256),
-                           0, s, P);
+        hipLaunchKernelGGL((k_hash_probe<N, V, MR, MX>), dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u),
+                           dim3(256), 0, s, P);
     }
     static void insert(const KParams &P, uint64_t np, hipStream_t s) {
-        constexpr int MX = Spec<N, V, MR>::MAXS + (BFV ? Spec<N, V, MR>::MCAP : 0);
         const uint64_t blocks = (np + 255) / 256;
         hipLaunchKernelGGL((k_insert_winners<MX>), dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u),
                            dim3(256), 0, s, P);
@@ -2515,7 +2346,9 @@ static void fill(KernelSet *ks) {
     ks->maxsucc = S::MAXS + (BFV ? S::MCAP : 0);
     ks->single = &Launch<N, V, MR, BFV>::single;
     ks->fused = &Launch<N, V, MR, BFV>::fused;
-    ks->probe = &Launch<N, V, MR, BFV>::probe;
+    ks->split = &Launch<N, V, MR, BFV>::split;
+    ks->hash_probe = &Launch<N, V, MR, BFV>::hash_probe;
+    ks->ctxw = ctx_words<N, V>();
     ks->insert = &Launch<N, V, MR, BFV>::insert;
     ks->wincount = &Launch<N, V, MR>::wincount;
     ks->commit = &Launch<N, V, MR, BFV>::commit;
@@ -2533,11 +2366,15 @@ bool get_kernels(int N, int V, int msg_cap, bool become_follower, KernelSet *ks)
         else fill<n, v, mr, false>(ks);                           \
         return true;                                              \
     }
+#ifdef RMC_QUICK  // kernel experiments: Raft.cfg's instance only (compile time)
+    RMC_CASE(3, 2, 1)
+#else
     RMC_CASE(2, 1, 1) RMC_CASE(2, 2, 1)
     RMC_CASE(3, 1, 1) RMC_CASE(3, 2, 1) RMC_CASE(3, 3, 1)
     RMC_CASE(3, 1, 2) RMC_CASE(3, 2, 2)
     RMC_CASE(4, 1, 2) RMC_CASE(4, 2, 2)
     RMC_CASE(5, 1, 2) RMC_CASE(5, 2, 2)
+#endif
 #undef RMC_CASE
     return false;
 }
@@ -2813,6 +2650,15 @@ void launch_side_sizes(const uint4 *side, uint64_t n, uint32_t *sz, hipStream_t 
 void launch_accept_side(const uint4 *side, const uint32_t *off, uint64_t n, uint64_t rel0, uint64_t *noff,
                         uint64_t *par, uint16_t *pslot, hipStream_t s) {
     if (n) hipLaunchKernelGGL(k_accept_side, dim3(grid256(n)), dim3(256), 0, s, side, off, n, rel0, noff, par, pslot);
+}
+__global__ __launch_bounds__(256) void k_seen_query(const ulonglong2 *__restrict__ fp, uint64_t n, Seen seen, uint32_t W,
+                                                    uint32_t self, uint8_t *__restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        if (W <= 1 || fp_owner(fp[i], W) == self) out[i] = seen_contains(seen, fp[i]) ? 1u : 0u;
+}
+void launch_seen_query(const ulonglong2 *fp, uint64_t n, Seen seen, uint32_t W, uint32_t self, uint8_t *out,
+                       hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_seen_query, dim3(grid256(n)), dim3(256), 0, s, fp, n, seen, W, self, out);
 }
 void launch_owner_of(const ulonglong2 *fp, uint32_t W, uint32_t *out, hipStream_t s) {
     hipLaunchKernelGGL(k_owner_of, dim3(1), dim3(64), 0, s, fp, W, out);

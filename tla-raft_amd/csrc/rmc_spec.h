@@ -250,15 +250,20 @@ RMC_HD uint32_t nat_aresp(const Dims &d, uint32_t src, uint32_t dst, uint32_t te
 }
 
 // ---- hashing --------------------------------------------------------------------------
-// Symmetry+VIEW fingerprint (tla:21,38): fp(s) = min over permutations pi of the
-// 128-bit structured hash H(pi(view(s))), with
-//   H_f(w) = sum_k Z_f(k, U_w[k]) + sum_{k != l} Z_f(k, l, P_w[k][l])     (mod 2^64, f = 0,1)
-// where U_w[k] is the exact packed own-state of server k (votedFor as None/self/
-// other, term, role, commitIndex, log, matchIndex[k][k], nextIndex[k][k]) and
-// P_w[k][l] combines matchIndex[k][l], nextIndex[k][l], votedFor[k] = l and the sum
-// of per-message hashes of msgs with src = k, dst = l.  Every term is a strong mix
-// of (position, content), so H is a Zobrist-style hash of the whole view; all
-// states in one orbit produce the same multiset {H(pi(s))} and hence the same min.
+// Symmetry+VIEW fingerprint (tla:21,38).  Per server k, its exact own-state U[k] (votedFor as
+// None/self/other, term, role, commitIndex, log, matchIndex[k][k], nextIndex[k][k]) and, per peer l,
+// its pair state X_f[k][l] (matchIndex[k][l], nextIndex[k][l], votedFor[k] = l, and the sum of the
+// per-message hashes of msgs with src = k, dst = l) -- server-relative, no server ids.  Each is
+// mixed once into a content matrix
+//   C_f[k][k] = mix64(U[k] ^ CK_U_f),   C_f[k][l] = mix64(X_f[k][l] ^ CK_X_f)        (f = 0, 1)
+// and a permutation pi, which puts server k at position pi(k), is priced by position constants:
+//   H_f(pi) = sum_{k,l} C_f[k][l] * K_f[pi(k)][pi(l)]       (mod 2^64, K_f odd, host seeds)
+// so a state costs its N^2 content mixes once (a successor: its acting server's row) and each
+// permutation only N^2 multiply-adds.  The fingerprint is the minimum of (H_1, H_0) over the
+// permutations consistent with the servers' signatures sig[k] = sum_l C_1[k][l] (sorted; ties
+// enumerated): states of one orbit have permuted signatures, so they take the minimum over the
+// same multiset of H values -- a class invariant; distinct contents sum to distinct values except
+// with probability ~2^-64 per half.
 RMC_HD uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
@@ -269,10 +274,15 @@ RMC_HD uint64_t splitmix(uint64_t &x) {
     return mix64(x);
 }
 
-constexpr uint64_t SEED_SERVER = 0x5ee1d5e5a7c0ffeeULL;
-constexpr uint64_t SEED_PAIR = 0x9a1b2c3d4e5f6071ULL;
+constexpr uint64_t SEED_PAIR = 0x9a1b2c3d4e5f6071ULL;  // position constants (host)
 constexpr uint64_t SEED_MSG = 0x0123456789abcdefULL;
 constexpr uint64_t PAIR_K0 = 0x9e3779b97f4a7c15ULL, PAIR_K1 = 0xc2b2ae3d27d4eb4fULL;
+constexpr uint64_t CK_U0 = 0x2545f4914f6cdd1dULL, CK_U1 = 0x8cb92ba72f3d8dd7ULL;
+constexpr uint64_t CK_X0 = 0x9fb21c651e98df25ULL, CK_X1 = 0xd6e8feb86659fd93ULL;
+RMC_HD uint64_t cmix_own(uint64_t u, int f) { return mix64(u ^ (f ? CK_U1 : CK_U0)); }
+RMC_HD uint64_t cmix_pair(uint64_t x, int f) { return mix64(x ^ (f ? CK_X1 : CK_X0)); }
+// position constants: K_f[a][b] = seeds[f * MAXN * MAXN + a * MAXN + b] (odd)
+constexpr int SEEDS_PER_F = MAXN * MAXN;
 
 // per-message hash pair of everything but src/dst (those are positions in the pair sums),
 // from the message's info word: the host's table (Universe::gmsg) and the expansion kernel's

@@ -76,6 +76,18 @@ class _Result(ctypes.Structure):
     ]
 
 
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+_ALLREDUCE = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, _U64P, ctypes.c_int32, ctypes.c_int32)
+_ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, _U64P, ctypes.c_int32, _U64P)
+_ALLTOALLV = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, _U64P, _U64P, ctypes.c_void_p,
+                              _U64P, _U64P)
+
+
+class _Transport(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("allreduce_u64", _ALLREDUCE), ("allgather_u64", _ALLGATHER),
+                ("alltoallv", _ALLTOALLV)]
+
+
 _lib = None
 
 
@@ -113,6 +125,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.rmc_successors.argtypes = [vp, P(i32), P(i32), ctypes.c_size_t, u32, P(u32), P(u64), P(u32)]
     lib.rmc_fingerprint.argtypes = [vp, P(i32), P(u64)]
     lib.rmc_eval_invariant.argtypes = [vp, P(i32), u32, P(i32)]
+    lib.rmc_set_transport.argtypes = [P(_Transport)]
+    lib.rmc_state_path.argtypes = [vp, u64, P(u32), P(u64), u32, P(u32)]
+    lib.rmc_fingerprints.argtypes = [vp, P(i32), ctypes.c_size_t, u64, P(u64)]
+    lib.rmc_seen_contains.argtypes = [vp, P(u64), u64, P(ctypes.c_uint8)]
     _lib = lib
     return lib
 
@@ -215,6 +231,87 @@ def comm_unique_id() -> bytes:
     if rc != RMC_OK:
         raise RmcError(f"rmc_comm_unique_id failed: {ERRORS.get(rc, rc)}")
     return buf.raw
+
+
+class HostTransport:
+    """The sharded protocol's collectives through host memory and a torch.distributed process group
+    (include/rmc.h rmc_transport) instead of RCCL: every rank of a world_size > 1 run installs one
+    before creating its ModelChecker (without comm_unique_id).  With a gloo group the ranks may share
+    one device -- the multi-rank path of SURVEY 8(e) as separate processes on a one-GPU box (tests) --
+    since RCCL refuses two ranks on one device.  A callback that raises fails the step (RMC_E_COMM)."""
+
+    def __init__(self, group=None):
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        self._np, self._torch, self._dist, self._group = np, torch, dist, group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self._c = _Transport(None, _ALLREDUCE(self._allreduce), _ALLGATHER(self._allgather),
+                             _ALLTOALLV(self._alltoallv))
+
+    @staticmethod
+    def _failed():
+        import sys
+        import traceback
+        traceback.print_exc(file=sys.stderr)
+        return 1
+
+    def _u64(self, ptr, n):
+        return self._np.ctypeslib.as_array(ptr, shape=(n,))
+
+    def _allreduce(self, _user, v, n, is_max):
+        try:
+            a = self._u64(v, n)
+            t = self._torch.from_numpy(a.astype(self._np.int64))  # values < 2^63 (counts, keys, codes)
+            self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX if is_max else self._dist.ReduceOp.SUM,
+                                  group=self._group)
+            a[:] = t.numpy().astype(self._np.uint64)
+            return 0
+        except Exception:  # noqa: BLE001 -- the library raises RMC_E_COMM
+            return self._failed()
+
+    def _allgather(self, _user, row, k, out):
+        try:
+            t = self._torch.from_numpy(self._u64(row, k).astype(self._np.int64))
+            parts = [self._torch.empty_like(t) for _ in range(self.world)]
+            self._dist.all_gather(parts, t, group=self._group)
+            self._u64(out, self.world * k)[:] = self._torch.cat(parts).numpy().astype(self._np.uint64)
+            return 0
+        except Exception:  # noqa: BLE001
+            return self._failed()
+
+    def _alltoallv(self, _user, send, send_off, send_bytes, recv, recv_off, recv_bytes):
+        try:
+            W = self.world
+            sb, rb = self._u64(send_bytes, W).tolist(), self._u64(recv_bytes, W).tolist()
+            so, ro = self._u64(send_off, W).tolist(), self._u64(recv_off, W).tolist()
+            send_end = max([int(o + b) for o, b in zip(so, sb)] + [1])
+            recv_end = max([int(o + b) for o, b in zip(ro, rb)] + [1])
+            src = self._np.ctypeslib.as_array(ctypes.cast(send, ctypes.POINTER(ctypes.c_uint8)), shape=(send_end,))
+            dst = self._np.ctypeslib.as_array(ctypes.cast(recv, ctypes.POINTER(ctypes.c_uint8)), shape=(recv_end,))
+            # all_to_all_single takes the parts in rank order, contiguous
+            ti = self._torch.from_numpy(self._np.concatenate([src[int(so[q]):int(so[q] + sb[q])] for q in range(W)]))
+            to = self._torch.empty(int(sum(rb)), dtype=self._torch.uint8)
+            self._dist.all_to_all_single(to, ti, [int(x) for x in rb], [int(x) for x in sb], group=self._group)
+            got, at = to.numpy(), 0
+            for q in range(W):
+                dst[int(ro[q]):int(ro[q] + rb[q])] = got[at:at + int(rb[q])]
+                at += int(rb[q])
+            return 0
+        except Exception:  # noqa: BLE001
+            return self._failed()
+
+    def install(self):
+        """Route the collectives of every ModelChecker created from now on in this process through this group."""
+        rc = load_library().rmc_set_transport(ctypes.byref(self._c))
+        if rc != RMC_OK:
+            raise RmcError(f"rmc_set_transport failed: {ERRORS.get(rc, rc)}")
+        return self
+
+    @staticmethod
+    def uninstall():
+        load_library().rmc_set_transport(None)
 
 
 # ------------------------------------------------------------------------------ unpacked states
@@ -518,6 +615,31 @@ class ModelChecker:
         fp = (ctypes.c_uint64 * 2)()
         self._check(self.lib.rmc_fingerprint(self.h, self._unpacked(state), fp))
         return fp[0], fp[1]
+
+    # ---- checks of a finished run's deep levels (tests/test_gpu_deep.py) -----------------
+    def state_path(self, gid: int):
+        """(keys, gids): how each state on the path from Init to the explored state `gid` was reached
+        ((server, action, witness) per step) and the global ids of the path's states (Init's 0 first)."""
+        cap = 4096
+        keys, gids, n = (ctypes.c_uint32 * cap)(), (ctypes.c_uint64 * cap)(), ctypes.c_uint32()
+        self._check(self.lib.rmc_state_path(self.h, gid, keys, gids, cap, ctypes.byref(n)))
+        return ([(k >> 24, (k >> 16) & 0xFF, k & 0xFFFF) for k in keys[1:n.value]], list(gids[:n.value]))
+
+    def fingerprints_unpacked(self, unpacked, stride: int, n: int):
+        """Fingerprints of n unpacked states (a contiguous int32 buffer, `stride` ints apart), one launch."""
+        fps = (ctypes.c_uint64 * (2 * max(n, 1)))()
+        buf = ctypes.cast(unpacked.ctypes.data if hasattr(unpacked, "ctypes") else unpacked,
+                          ctypes.POINTER(ctypes.c_int32))
+        self._check(self.lib.rmc_fingerprints(self.h, buf, stride, n, fps))
+        return [(fps[2 * i], fps[2 * i + 1]) for i in range(n)]
+
+    def seen_contains(self, fps: Sequence[Tuple[int, int]]) -> List[bool]:
+        """Membership of each fingerprint in the seen set (TLC's FPSet)."""
+        n = len(fps)
+        arr = (ctypes.c_uint64 * (2 * max(n, 1)))(*[w for f in fps for w in f])
+        out = (ctypes.c_uint8 * max(n, 1))()
+        self._check(self.lib.rmc_seen_contains(self.h, arr, n, out))
+        return [bool(out[i]) for i in range(n)]
 
     def eval_invariant(self, state: dict, name: str) -> Optional[bool]:
         """True / False, or None for a TLC evaluation error."""

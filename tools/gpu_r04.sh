@@ -1,0 +1,39 @@
+#!/bin/bash
+# Round-4 GPU session steps on one box, each under its own time limit, stopping at the first
+# failure.  usage: tools/gpu_r04.sh OUTDIR step [step ...]
+#   tests        pytest -m gpu (whole suite)        tests:K  pytest -m gpu -k K
+#   raftcfg      Raft.cfg exhausted level by level (tools/explore.py)
+#   prof_raftcfg rocprofv3 kernel stats of the same
+#   bench        bench.py default line              prof_bench  rocprofv3 kernel stats of bench (configs[1])
+#   c4           configs[3] as deep as one GPU goes  rccl1       Raft.cfg through a one-rank RCCL communicator
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+cd "$R" || exit 1
+O=gpurun_out/$1
+shift
+mkdir -p "$O"
+export TMPDIR=/tmp
+step() { echo "== $1 ($(date +%T))"; }
+for s in "$@"; do
+  step "$s"
+  case "$s" in
+    tests) timeout -k 10 900 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1 || { tail -30 "$O/tests.log"; exit 1; }
+           tail -2 "$O/tests.log" ;;
+    tests:*) k=${s#tests:}; timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread -k "$k" > "$O/tests_$k.log" 2>&1 || { tail -30 "$O/tests_$k.log"; exit 1; }
+           tail -2 "$O/tests_$k.log" ;;
+    raftcfg) timeout -k 10 300 python -u tools/explore.py 3 2 3 3 --budget 200 > "$O/raftcfg.log" 2>&1 || { tail -20 "$O/raftcfg.log"; exit 1; }
+           tail -4 "$O/raftcfg.log" ;;
+    prof_raftcfg) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof_raftcfg" -o run -- python3 "$R/tools/explore.py" 3 2 3 3 --budget 200 > "$O/prof_raftcfg.log" 2>&1 || { tail -20 "$O/prof_raftcfg.log"; exit 1; }
+           grep RESULT "$O/prof_raftcfg.log"; find "$O/prof_raftcfg" -name '*kernel_stats.csv' -exec head -12 {} \; ;;
+    bench) timeout -k 10 600 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" || { tail "$O/bench.err"; exit 1; }
+           cut -c1-600 "$O/bench.json" ;;
+    prof_bench) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof_c2" -o bench -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-probe-peak --no-scale > "$O/prof_c2.log" 2>&1 || { tail -20 "$O/prof_c2.log"; exit 1; }
+           find "$O/prof_c2" -name '*kernel_stats.csv' -exec head -12 {} \; ;;
+    c4) timeout -k 10 300 python -u tools/explore.py 5 1 3 3 --budget 150 > "$O/c4.log" 2>&1 || { tail -20 "$O/c4.log"; exit 1; }
+           tail -4 "$O/c4.log" ;;
+    rccl1) timeout -k 10 300 python -u tools/explore.py 3 2 3 3 --rccl1 --budget 200 > "$O/rccl1.log" 2>&1 || { tail -5 "$O/rccl1.log"; exit 1; }
+           tail -4 "$O/rccl1.log" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== done ($(date +%T))"
