@@ -55,20 +55,23 @@ TIMED_PHASES = 1 << PHASES.index("expand_hash")  # HIP-event timing of the domin
 TIMING_EVERY = 4
 
 
-def alg_bytes(phase, F, G, N, S, CCWB, slot_bytes=16, SWB=32, split=False):
+def alg_bytes(phase, F, G, N, S, CCWB, slot_bytes=16, SWB=32, split=False, CTXB=112):
     """Algorithmic HBM bytes of one phase of the fused single-GPU level (DESIGN.md "Kernels"):
     F parents of S-byte records (S = the run's average packed record: CCWB core bytes + message
     ids), G generated successors, N new states; SWB = staging bytes per successor (the acting row),
-    slot_bytes = seen-set slot (16 full, 8 compact).  split: the host-driven chunk's probe and
-    election run in k_probe ("probe"), not in the expansion."""
-    if phase == "expand_hash" and split:  # k_expand<FUSED>, split chunk: staged row + fp + extra-words word out
-        return F * S + F * 8 + G * (SWB + 16 + 4)
+    slot_bytes = seen-set slot (16 full, 8 compact), CTXB = a split chunk's hash context per parent
+    (ctx_bytes).  split: the host-driven chunk's expansion only stages (k_expand<SPLIT>); the
+    fingerprints, probe and election run in k_hash_probe ("probe")."""
+    if phase == "expand_hash" and split:  # k_expand<SPLIT>: parents in, count + |msgs| + hash context out,
+        # the staged rows out
+        return F * S + F * 8 + F * CTXB + G * SWB
     if phase == "expand_hash":   # k_expand<FUSED>: parents in, count + |msgs| out; per successor: staged row +
         # fp + election slot, one seen-set probe; per new fingerprint at least one election (16-B slot, 8-B word, count)
         return F * S + F * 8 + G * (SWB + 16 + 4) + G * slot_bytes + N * (16 + 8 + 4)
-    if phase == "probe":         # k_probe: per parent its count; per successor fp + extra words in, verdict out,
-        # one seen-set probe; per new fingerprint at least one election (16-B slot, 8-B word, count)
-        return F * 4 + G * (16 + 4 + 4) + G * slot_bytes + N * (16 + 8 + 4)
+    if phase == "probe":         # k_hash_probe: per parent its count and hash context; per successor its staged
+        # row in, fingerprint + verdict out, one seen-set probe; per new fingerprint at least one election
+        # (16-B slot, 8-B word, count)
+        return F * (4 + CTXB) + G * (SWB + 16 + 4) + G * slot_bytes + N * (16 + 8 + 4)
     if phase == "insert":        # k_insert_winners: per parent its count; per successor its slot word; per new
         # state its election word, fingerprint, seen-set insert and verdict
         return F * 4 + G * 4 + N * (8 + 16 + slot_bytes + 4)
@@ -604,12 +607,13 @@ def at_scale(device, workload="raftcfg", probes_per_s=None):
         dt = time.perf_counter() - t0
     ms = sum(ls.kernel_ms[PHASES.index("expand_hash")] for ls in cold.levels)
     S, CCWB = record_bytes(cold, cfg)
-    # each level's expansion bytes: split (k_probe) levels of >= 2^16 parents without the probe and election
+    # each level's expansion bytes: split levels of >= 2^16 parents (k_expand<SPLIT>: no fingerprints, probe or
+    # election -- those are k_hash_probe's)
     alg = 0
     for i, ls in enumerate(cold.levels[:-1]):
         nxt = cold.levels[i + 1]
         alg += alg_bytes("expand_hash", nxt.expanded, nxt.generated, nxt.new_states, S, CCWB, cold.seen_slot_bytes,
-                         staging_bytes(cfg), split=nxt.expanded >= (1 << 16))
+                         staging_bytes(cfg), split=nxt.expanded >= (1 << 16), CTXB=ctx_bytes(w["n"], w["V"]))
     gbs = alg / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     gold = {}
     gpath = os.path.join(ROOT, "tests", "golden", "levels_prefix.json")
@@ -680,6 +684,12 @@ def codec_words(n, V):
     b_ix, b_ni, b_ent = bits_for(V + 1), bits_for(V + 2), 3 + bits_for(V - 1)
     bits = n * (bits_for(n) + 3 + 2 + 2 * b_ix) + n * V * b_ent + n * n * (b_ix + b_ni) + n * n + 3 + 4 + V + 8
     return (bits + 31) // 32
+
+
+def ctx_bytes(n, V):
+    """A split chunk's hash context per parent (rmc_kernels.hip ctx_words): the packed core padded to
+    16 B, then 16 B of message-hash sums per ordered server pair."""
+    return 4 * ((codec_words(n, V) + 3) // 4 * 4 + 4 * n * (n - 1))
 
 
 def staging_bytes(cfg):

@@ -769,6 +769,27 @@ def test_launcher_prints_tlc_counterexample(tmp_path):
            f"{g['queue_left']} states left on queue." in out
 
 
+@pytest.mark.parametrize("spec", ["seeded", "raft_e2"])
+def test_launcher_gpus_one_rank_prints_the_single_path_lines(spec, tmp_path):
+    """raftmc -gpus 1 -onerank: a rank process forked by the launcher, its RCCL id handed down a pipe,
+    the sharded protocol through a one-rank communicator from Init's level -- TLC's lines (counters,
+    depth or the violation and every State block) equal the single-GPU run's."""
+    import subprocess
+    from test_host import LAUNCHER, cfg_text
+    name = "RaftSeeded" if spec == "seeded" else "Raft"
+    (tmp_path / f"{name}.cfg").write_text(cfg_text(E=2, R=3, vals="v1"))
+    env = dict(os.environ, RMC_SKIP_SPEC_CHECK="1")
+    base = [LAUNCHER, "-deadlock", "-config", str(tmp_path / f"{name}.cfg"), str(tmp_path / f"{name}.tla")]
+    keep = lambda out: [ln for ln in out.splitlines() if not ln.startswith(("Starting", "Finished in", "Progress(",
+                                                                          "GPU:", "Running", "vm:"))]
+    one = subprocess.run(base, capture_output=True, text=True, env=env, timeout=180)
+    rk = subprocess.run(base[:1] + ["-gpus", "1", "-onerank", "-shardmin", "1"] + base[1:], capture_output=True,
+                        text=True, env=env, timeout=180)
+    assert one.returncode == rk.returncode == (12 if spec == "seeded" else 0), rk.stdout + rk.stderr
+    assert keep(rk.stdout) == keep(one.stdout)
+    assert "Running breadth-first search Model-Checking on 1 GPU" in rk.stdout
+
+
 # ---- the BecomeFollower variant (SURVEY 8(f) item 3; Raft.tla:190-231, 420) ---------------------
 # Next with `\/ BecomeFollower(s)` uncommented: FollowerUpdateTerm / CandidateToFollower /
 # LeaderToFollower right after UpdateTerm, a second candidate per message lane (k_expand<..., BFV>).

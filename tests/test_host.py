@@ -145,6 +145,24 @@ def test_launcher_rejects_unknown_flags(tmp_path):
     assert r.returncode == 150 and "unsupported option" in r.stderr
 
 
+def test_launcher_gpus_argument(tmp_path):
+    """-gpus N (one rank process per GPU, myrun.sh:3's -workers on the node): the count is checked;
+    without a GPU every rank fails to start, and the launcher still ends (no rank left waiting for
+    the RCCL id) with TLC's header and the error once, from rank 0."""
+    r = subprocess.run([LAUNCHER, "-gpus", "0", "Raft.tla"], capture_output=True, text=True)
+    assert r.returncode == 150 and "-gpus" in r.stderr
+    if has_gpu():
+        pytest.skip("the no-device path needs a machine without a GPU")
+    (tmp_path / "Raft.cfg").write_text(cfg_text(E=2, R=3, vals="v1"))
+    env = dict(os.environ, RMC_SKIP_SPEC_CHECK="1")
+    r = subprocess.run([LAUNCHER, "-gpus", "3", "-deadlock", "-config", str(tmp_path / "Raft.cfg"),
+                        str(tmp_path / "Raft.tla")], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 75, r.stdout + r.stderr
+    out = r.stdout.splitlines()
+    assert sum(1 for ln in out if ln.startswith("Running breadth-first search Model-Checking on 3 GPUs")) == 1
+    assert sum(1 for ln in out if ln.startswith("Error: could not start the GPU model checker")) == 1
+
+
 def test_launcher_reports_cfg_errors(tmp_path):
     (tmp_path / "Raft.cfg").write_text(cfg_text().replace("VIEW view", ""))
     env = dict(os.environ, RMC_SKIP_SPEC_CHECK="1")
@@ -241,14 +259,17 @@ def _bench():
 
 
 def test_bench_split_bytes_account_for_the_probe_pass():
-    """A split chunk's expansion + k_probe move the fused expansion's algorithmic bytes plus what the
-    split adds: each successor's fingerprint and extra-words word read back (20 B) and its verdict
-    written (4 B), and each parent's count read (4 B)."""
+    """A split chunk's expansion + k_hash_probe move the fused expansion's algorithmic bytes plus what
+    the split adds: each parent's hash context written and read back (2 x 112 B for 3 servers and 2
+    values) and its count read (4 B), and each successor's staged row read back (32 B)."""
     bench = _bench()
     F, G, N, S = 1000, 5200, 1000, 69.5
+    ctxb = bench.ctx_bytes(3, 2)
+    assert ctxb == 112
     fused = bench.alg_bytes("expand_hash", F, G, N, S, 16, 8, 32)
-    split = bench.alg_bytes("expand_hash", F, G, N, S, 16, 8, 32, split=True) + bench.alg_bytes("probe", F, G, N, S, 16, 8)
-    assert split == fused + F * 4 + G * 24
+    split = bench.alg_bytes("expand_hash", F, G, N, S, 16, 8, 32, split=True, CTXB=ctxb) + \
+        bench.alg_bytes("probe", F, G, N, S, 16, 8, 32, CTXB=ctxb)
+    assert split == fused + F * (4 + 2 * ctxb) + G * 32
 
 
 def test_bench_counters_at_scale_read_from_profiles():

@@ -1,14 +1,20 @@
 // raftmc -- TLC-compatible command line over librmc (the drop-in for myrun.sh:3).
 //
-//   raftmc [-deadlock] [-workers N] [-config Raft.cfg] [-device D] [-msgcap C] [-seenlog2 K] Raft.tla
+//   raftmc [-deadlock] [-workers N] [-config Raft.cfg] [-device D] [-gpus N] [-msgcap C] [-seenlog2 K] Raft.tla
 //
 // Accepts the flags myrun.sh passes to TLC (myrun.sh:3), reads the same Raft.tla /
 // Raft.cfg, and prints TLC's result lines (states generated, distinct states, depth,
 // the counterexample) so that parsers of raft.log keep working.  GPU-specific lines
 // are printed after TLC's block.  Exit codes follow TLC's (0 ok, 11 deadlock,
 // 12 safety violation, 14 Assert, 75 evaluation error, 150/151 spec/config errors).
+#include <fcntl.h>
+#include <signal.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <chrono>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -212,8 +218,120 @@ struct Printer {
 
 int usage(const char *msg) {
     std::fprintf(stderr, "raftmc: %s\nusage: raftmc [-deadlock] [-workers N] [-config FILE.cfg] [-device D] "
-                         "[-msgcap C] [-seenlog2 K] [-checkpoint MIN] [-metadir DIR] [-recover DIR] FILE.tla\n", msg);
+                         "[-gpus N [-onerank] [-shardmin K]] [-msgcap C] [-seenlog2 K] [-checkpoint MIN] [-metadir DIR] "
+                         "[-recover DIR] FILE.tla\n", msg);
     return 150;
+}
+
+bool io_all(int fd, void *buf, size_t n, bool wr) {
+    char *p = static_cast<char *>(buf);
+    while (n) {
+        const ssize_t k = wr ? ::write(fd, p, n) : ::read(fd, p, n);
+        if (k <= 0) return false;
+        p += k;
+        n -= (size_t)k;
+    }
+    return true;
+}
+
+// -gpus N: one rank process per GPU, forked before anything touches a GPU.  Rank 0
+// creates the RCCL unique id (its bootstrap root lives in that process) and sends it up a pipe;
+// this process hands it down to ranks 1 .. N-1.  Rank r runs the checker on device base + r with
+// world_size N (-onerank: one rank, world_size 1 with the id -- the sharded protocol through a
+// one-rank communicator); only rank 0 writes TLC's output, the others' stdout goes to /dev/null.
+// Returns rank 0's exit code.  A rank that dies, or ends with an error while rank 0 still runs,
+// takes the others down (they would wait in a collective); after rank 0 ends the others get 60 s.
+int run_ranks(int N, bool onerank, const rmc_config &base, const std::function<int(const rmc_config &)> &body) {
+    std::fflush(stdout);
+    std::fflush(stderr);
+    int up[2];
+    if (::pipe(up) != 0) { std::printf("Error: pipe failed\n"); return 75; }
+    std::vector<pid_t> pid(N, -1);
+    std::vector<int> down(N, -1);
+    for (int r = 0; r < N; r++) {
+        int p[2];
+        if (::pipe(p) != 0) { std::printf("Error: pipe failed\n"); return 75; }
+        const pid_t k = ::fork();
+        if (k < 0) { std::printf("Error: fork failed\n"); return 75; }
+        if (k == 0) {  // rank r
+            ::close(p[1]);
+            ::close(up[0]);
+            if (r != 0) ::close(up[1]);  // (only rank 0 writes up: the others must not hold it open)
+            for (int q = 0; q < r; q++) ::close(down[q]);
+            unsigned char id[128];
+            if (r == 0) {
+                const int rc = rmc_comm_unique_id(id);
+                if (rc != RMC_OK) {
+                    std::printf("Error: could not start the GPU model checker (RCCL unique id: code %d)\n", rc);
+                    std::fflush(stdout);
+                    std::_Exit(75);
+                }
+                if (!io_all(up[1], id, sizeof id, true)) std::_Exit(75);
+            } else if (!io_all(p[0], id, sizeof id, false)) {
+                std::_Exit(75);  // rank 0 could not start: nothing to join
+            }
+            if (r == 0) ::close(up[1]);
+            ::close(p[0]);
+            if (r != 0) {
+                const int dn = ::open("/dev/null", O_WRONLY);
+                if (dn >= 0) ::dup2(dn, 1);
+            }
+            rmc_config c = base;
+            c.rank = onerank ? 0 : r;
+            c.world_size = onerank ? 1 : N;
+            c.comm_unique_id = id;
+            c.device = (base.device >= 0 ? base.device : 0) + r;
+            const int code = body(c);
+            std::fflush(stdout);
+            std::fflush(stderr);
+            std::_Exit(code);
+        }
+        ::close(p[0]);
+        down[r] = p[1];
+        pid[r] = k;
+    }
+    ::close(up[1]);
+    unsigned char id[128];
+    const bool have = io_all(up[0], id, sizeof id, false);
+    ::close(up[0]);
+    for (int r = 1; r < N; r++) {
+        if (have) io_all(down[r], id, sizeof id, true);
+        ::close(down[r]);
+    }
+    ::close(down[0]);
+    int code0 = 75, alive = N;
+    bool rank0_done = false;
+    auto kill_all = [&] {
+        for (int r = 0; r < N; r++)
+            if (pid[r] > 0) ::kill(pid[r], SIGKILL);
+    };
+    auto t_done = std::chrono::steady_clock::now();
+    while (alive) {
+        int st = 0;
+        const pid_t w = ::waitpid(-1, &st, rank0_done ? WNOHANG : 0);
+        if (w < 0) break;
+        if (w == 0) {  // rank 0 has ended; the others finish their last collectives or are stopped
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t_done).count() > 60.0) kill_all();
+            ::usleep(100000);
+            continue;
+        }
+        const int r = (int)(std::find(pid.begin(), pid.end(), w) - pid.begin());
+        if (r >= N) continue;
+        pid[r] = -1;
+        alive--;
+        const bool clean = WIFEXITED(st);
+        const int code = clean ? WEXITSTATUS(st) : 75;
+        if (r == 0) {
+            code0 = code;
+            rank0_done = true;
+            t_done = std::chrono::steady_clock::now();
+        } else if (!clean || (!rank0_done && code != 0 && code != 11 && code != 12 && code != 14)) {
+            std::fprintf(stderr, "raftmc: rank %d ended (%s %d); stopping the other ranks\n", r,
+                         clean ? "exit" : "signal", clean ? code : WTERMSIG(st));
+            kill_all();
+        }
+    }
+    return code0;
 }
 
 }  // namespace
@@ -229,7 +347,9 @@ static void phase_time(const char *what) {
 
 int main(int argc, char **argv) {
     std::string tla_path, cfg_path;
-    int check_deadlock = 1, device = -1, msgcap = 0, seenlog2 = 0, workers = 1;
+    int check_deadlock = 1, device = -1, msgcap = 0, seenlog2 = 0, workers = 1, gpus = 1;
+    bool onerank = false;                // -gpus 1 through a one-rank RCCL communicator (tests)
+    unsigned long long shardmin = 0;     // -gpus: levels below this many states run replicated (0 = 2^20)
     bool print_locations = false;       // print each action's source range and exit (no GPU needed)
     double progress_s = 60.0;           // TLC reports Progress once a minute (and at the end)
     double ckpt_minutes = 30.0;         // TLC -checkpoint: minutes between checkpoints (0 = never)
@@ -244,6 +364,9 @@ int main(int argc, char **argv) {
         else if (a == "-workers") workers = std::atoi(need("-workers"));  // CPU threads in TLC; the GPU path ignores it
         else if (a == "-config") cfg_path = need("-config");
         else if (a == "-device") device = std::atoi(need("-device"));
+        else if (a == "-gpus") gpus = std::atoi(need("-gpus"));
+        else if (a == "-onerank") onerank = true;
+        else if (a == "-shardmin") shardmin = std::strtoull(need("-shardmin"), nullptr, 10);
         else if (a == "-msgcap") msgcap = std::atoi(need("-msgcap"));
         else if (a == "-seenlog2") seenlog2 = std::atoi(need("-seenlog2"));
         else if (a == "-checkpoint") ckpt_minutes = std::atof(need("-checkpoint"));
@@ -256,6 +379,7 @@ int main(int argc, char **argv) {
         else return usage(("unsupported option " + a).c_str());
     }
     if (tla_path.empty()) return usage("missing spec file");
+    if (gpus < 1 || gpus > 64) return usage("-gpus must be 1..64");
     if (cfg_path.empty()) cfg_path = tla_path.substr(0, tla_path.size() - 4) + ".cfg";
     std::string tla, cfgtxt;
     const bool skip_spec = std::getenv("RMC_SKIP_SPEC_CHECK") && std::string(std::getenv("RMC_SKIP_SPEC_CHECK")) == "1";
@@ -291,13 +415,16 @@ int main(int argc, char **argv) {
     cfg.device = device;
     cfg.msg_cap = msgcap;
     cfg.seen_log2 = seenlog2;
+    cfg.shard_min_states = shardmin;
 
     std::printf("raftmc (MI355X-native model checker for kikimo/tla-raft) -- TLC-compatible output\n");
-    std::printf("Running breadth-first search Model-Checking on the GPU (TLC -workers %d order: 1).\n", workers);
+    std::printf("Running breadth-first search Model-Checking on %d GPU%s (TLC -workers %d order: 1).\n", gpus,
+                gpus > 1 ? "s" : "", workers);
     std::printf("Parsing file %s\n", tla_path.c_str());
     std::printf("Semantic processing of module %s\n", pm.module.c_str());
     for (const auto &c : pm.ignored_constants) std::printf("(ignoring assignment to undeclared constant %s)\n", c.c_str());
     std::printf("Starting... (%s)\n", now_str().c_str());
+    auto check = [&](const rmc_config &cfg) -> int {
     const auto t0 = std::chrono::steady_clock::now();
     void *ctx = nullptr;
     phase_time("create");
@@ -429,8 +556,9 @@ int main(int argc, char **argv) {
     if (res.status == RMC_DONE)
         std::printf("The depth of the complete state graph search is %d.\n", res.depth);
     std::printf("Finished in %.2fs at (%s)\n", el, now_str().c_str());
-    std::printf("GPU: %.0f distinct states/s over %.3f s of BFS levels (MI355X, 1 device).\n",
-                gpu_seconds > 0 ? res.distinct / gpu_seconds : 0.0, gpu_seconds);
+    std::printf("GPU: %.0f distinct states/s over %.3f s of BFS levels (MI355X, %d device%s).\n",
+                gpu_seconds > 0 ? res.distinct / gpu_seconds : 0.0, gpu_seconds, cfg.world_size > 1 ? cfg.world_size : 1,
+                cfg.world_size > 1 ? "s" : "");
     // The process ends here: by default the device and host memory (~250 GB and ~110 GB of
     // trace at Raft.cfg) go back with the process instead of through rmc_destroy, whose frees took
     // ~16 s after a Raft.cfg exhaustion (RMC_FAST_EXIT=0 destroys the context first).
@@ -442,4 +570,7 @@ int main(int argc, char **argv) {
     rmc_destroy(ctx);
     phase_time("destroyed");
     return exit_code;
+    };
+    if (gpus > 1 || onerank) return run_ranks(gpus, onerank, cfg, check);
+    return check(cfg);
 }

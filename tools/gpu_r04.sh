@@ -6,6 +6,8 @@
 #   prof_raftcfg rocprofv3 kernel stats of the same
 #   bench        bench.py default line              prof_bench  rocprofv3 kernel stats of bench (configs[1])
 #   c4           configs[3] as deep as one GPU goes  rccl1       Raft.cfg through a one-rank RCCL communicator
+#   pmc_raftcfg  PMC passes over Raft.cfg's first 40 expansions + tools/pmc_scale_report.py
+#   myrun        tools/gpu_myrun.sh (the drop-in on scratch_myrun/)   smoke  __graft_entry__.smoke()
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd "$R" || exit 1
@@ -33,6 +35,11 @@ for s in "$@"; do
            tail -4 "$O/c4.log" ;;
     rccl1) timeout -k 10 300 python -u tools/explore.py 3 2 3 3 --rccl1 --budget 200 > "$O/rccl1.log" 2>&1 || { tail -5 "$O/rccl1.log"; exit 1; }
            tail -4 "$O/rccl1.log" ;;
+    pmc_raftcfg) OUT=$O/pmc_raftcfg CFG="3 2 3 3 --levels 40" LIMIT=150 bash tools/pmc_scale.sh || exit 1
+           python tools/pmc_scale_report.py "$O/pmc_raftcfg" "$O/pmc_scale_raftcfg_levels.json" --workload "Raft.cfg, first 40 expansions" ;;
+    myrun) bash tools/gpu_myrun.sh || exit 1 ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { cat "$O/smoke.log"; exit 1; }
+           tail -1 "$O/smoke.log" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

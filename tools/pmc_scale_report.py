@@ -5,8 +5,8 @@ tools/pmc_scale.sh runs tools/explore.py once per counter pass: by default 3 ser
 MaxElection 2 (18.5 M states), or Raft.cfg's first levels (CFG="3 2 3 3 --levels 44"); either way the
 compact seen set is ~140 GB -- far beyond the 256 MB Infinity Cache, so FETCH_SIZE / WRITE_SIZE are
 HBM traffic.  explore.py steps level by level on the host-driven path: a level of F parents is
-ceil(F / chunk_parents) chunks, one dispatch of each kernel per chunk (k_probe only for chunks of at
-least --split-min parents), in dispatch order.  The explore log of the same pass gives each level's
+ceil(F / chunk_parents) chunks, one dispatch of each kernel per chunk (k_hash_probe and k_insert_winners
+only for chunks of at least --split-min parents), in dispatch order.  The explore log of the same pass gives each level's
 parents F, successors G, new states N, average record bytes S and the HIP-event time of each kernel
 phase; each dispatch's duration is its own (start / end timestamps of the FETCH_SIZE pass's records).
 Per level (dispatches of a level summed) this records:
@@ -31,11 +31,11 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from bench import HBM_PEAK_GBS, VALU_PEAK, alg_bytes  # noqa: E402
+from bench import HBM_PEAK_GBS, VALU_PEAK, alg_bytes, ctx_bytes  # noqa: E402
 
 LEVEL = re.compile(r"^L\s*(\d+) F=\s*(\d+) G=\s*(\d+) N=\s*(\d+) tot=\s*\d+\s+[\d.]+ms \[([^\]]*)\].*rec=([\d.]+)B")
 # name -> (kernel name fragment, explore phase column of its HIP-event time, alg_bytes phase)
-KERNELS = {"expand": ("k_expand", 1, "expand_hash"), "probe": ("k_probe", 5, "probe"),
+KERNELS = {"expand": ("k_expand", 1, "expand_hash"), "probe": ("k_hash_probe", 5, "probe"),
            "insert": ("k_insert_winners", 5, "insert"), "commit": ("k_commit", 3, "materialize")}
 
 
@@ -104,7 +104,7 @@ def main():
             # HIP-event columns lump k_probe and k_insert_winners together)
             ms = sum(fetch[i]["_ms"] for i in range(d0, k))
             split = L["F"] >= a.split_min  # (every chunk of such a level is split at Raft.cfg's sizes)
-            alg = alg_bytes(phase, L["F"], L["G"], L["N"], L["rec"], 0, 8, swb, split=split)
+            alg = alg_bytes(phase, L["F"], L["G"], L["N"], L["rec"], 0, 8, swb, split=split, CTXB=ctx_bytes(a.n, a.V))
             rd = 1024 * sum(fetch[i]["FETCH_SIZE"] for i in range(d0, k))
             wr = 1024 * sum(write[i]["WRITE_SIZE"] for i in range(d0, k))
             hbm = 2 * rd + wr
