@@ -607,13 +607,18 @@ def at_scale(device, workload="raftcfg", probes_per_s=None):
         dt = time.perf_counter() - t0
     ms = sum(ls.kernel_ms[PHASES.index("expand_hash")] for ls in cold.levels)
     S, CCWB = record_bytes(cold, cfg)
-    # each level's expansion bytes: split levels of >= 2^16 parents (k_expand<SPLIT>: no fingerprints, probe or
-    # election -- those are k_hash_probe's)
+    # each expansion's bytes, chunk by chunk as the engine cuts the level (chunk_parents): a chunk of >= 2^16
+    # parents is split (k_expand<SPLIT>: no fingerprints, probe or election -- those are k_hash_probe's);
+    # a level's successors and new states are spread over its chunks in proportion to their parents
+    cp = chunk_parents(w["n"], w["V"])
     alg = 0
-    for i, ls in enumerate(cold.levels[:-1]):
-        nxt = cold.levels[i + 1]
-        alg += alg_bytes("expand_hash", nxt.expanded, nxt.generated, nxt.new_states, S, CCWB, cold.seen_slot_bytes,
-                         staging_bytes(cfg), split=nxt.expanded >= (1 << 16), CTXB=ctx_bytes(w["n"], w["V"]))
+    for ls in cold.levels[1:]:  # (levels[0] is Init's)
+        F = ls.expanded
+        for c0 in range(0, F, cp):
+            f = min(cp, F - c0)
+            alg += alg_bytes("expand_hash", f, ls.generated * f / F, ls.new_states * f / F, S, CCWB,
+                             cold.seen_slot_bytes, staging_bytes(cfg), split=f >= (1 << 16),
+                             CTXB=ctx_bytes(w["n"], w["V"]))
     gbs = alg / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     gold = {}
     gpath = os.path.join(ROOT, "tests", "golden", "levels_prefix.json")
@@ -684,6 +689,14 @@ def codec_words(n, V):
     b_ix, b_ni, b_ent = bits_for(V + 1), bits_for(V + 2), 3 + bits_for(V - 1)
     bits = n * (bits_for(n) + 3 + 2 + 2 * b_ix) + n * V * b_ent + n * n * (b_ix + b_ni) + n * n + 3 + 4 + V + 8
     return (bits + 31) // 32
+
+
+def chunk_parents(n, V, chunk_successors=1 << 28):
+    """Parents per host-driven chunk on one GPU (rmc_engine.hip: Gcap / maxsucc, at most the winner count's
+    1024 x 4096 tiles); maxsucc = Spec::MAXS of one message round (n <= 3) or two."""
+    mcap = 64 if n <= 3 else 128
+    maxsucc = mcap + n * (4 + V + n - 1)
+    return min(chunk_successors // maxsucc, 1024 * 4096)
 
 
 def ctx_bytes(n, V):

@@ -25,6 +25,8 @@ with open(os.path.join(GOLDEN, "levels.json")) as _f:
     LEVELS = json.load(_f)
 with open(os.path.join(GOLDEN, "traces.json")) as _f:
     TRACES = json.load(_f)
+with open(os.path.join(GOLDEN, "levels_bf.json")) as _f:
+    LEVELS.update(json.load(_f))  # the BecomeFollower variant (Raft.tla:420): keys bf_*
 SPEC = {False: 0, True: 1}
 
 
@@ -79,7 +81,7 @@ def check(g, r):
 
 @pytest.mark.parametrize("W,shard_min", [(2, 1), (2, 40), (3, 1)])
 @pytest.mark.parametrize("name", ["n3_v1_e2_r3", "seeded_n3_v2_e2_r3", "deadlock_n3_v1_e1_r3", "n4_v1_e1_r3",
-                                  "exist_lc_n3_v1_e2_r3"])
+                                  "exist_lc_n3_v1_e2_r3", "bf_n4_v1_e1_r3"])
 def test_ranks_identical_to_single(name, W, shard_min, tmp_path):
     """Golden levels, counters and counterexample at W ranks; every rank reports the same run."""
     g = LEVELS[name]

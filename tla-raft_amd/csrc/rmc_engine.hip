@@ -282,9 +282,21 @@ class TraceStager {
                 b = free_.back();
                 free_.pop_back();
             }
-            HIPCHK(hipMemcpyAsync(par_[b], dpar + i, k * 8, hipMemcpyDeviceToHost, cs));
-            HIPCHK(hipMemcpyAsync(slot_[b], dslot + i, k * 2, hipMemcpyDeviceToHost, cs));
-            HIPCHK(hipEventRecord(ev_[b], cs));
+            try {
+                HIPCHK(hipMemcpyAsync(par_[b], dpar + i, k * 8, hipMemcpyDeviceToHost, cs));
+                HIPCHK(hipMemcpyAsync(slot_[b], dslot + i, k * 2, hipMemcpyDeviceToHost, cs));
+                HIPCHK(hipEventRecord(ev_[b], cs));
+            } catch (...) {
+                // the buffer goes back and the stager is marked failed: drain() reports the error
+                // instead of waiting for a buffer that no job will return
+                {
+                    std::lock_guard<std::mutex> lk(m_);
+                    free_.push_back(b);
+                    failed_ = true;
+                }
+                cv_.notify_all();
+                throw;
+            }
             Job j;
             j.b = b;
             hpar.for_range(at + i, k, [&](uint64_t *p, uint64_t c) { j.pp[j.np] = p; j.pc[j.np++] = c; });
@@ -848,6 +860,16 @@ struct rmc_ctx {
         // on demand (ensure_chunk), so a small run does not pay for them; an RCCL rank allocates
         // them at create, its budgets may be explicit (bench's configs[3] leg).
         Gcap = cfg.chunk_successors ? cfg.chunk_successors : (virt ? (1ull << 23) : (1ull << 28));
+        if (!cfg.chunk_successors && (rccl || hostx) && (cfg.seen_mem_bytes || cfg.frontier_mem_bytes)) {
+            // a rank allocates its round buffers at create: with explicit seen-set / frontier budgets,
+            // halve the default round until those buffers fit beside the budgets in free memory
+            // (per slot: fingerprint, verdict, staging, item out and in, route and owner words, ~2 election slots)
+            size_t fr = 0, tot = 0;
+            HIPCHK(hipMemGetInfo(&fr, &tot));
+            const uint64_t per_slot = 16 + 4 + 16 * (uint64_t)sw4() + 4 + 4 + 4 + 2 * sizeof(XItem) + 8 + 2 * 24;
+            const uint64_t budgets = cfg.seen_mem_bytes + cfg.frontier_mem_bytes + (4ull << 30);
+            while (Gcap > (1ull << 24) && budgets + Gcap * per_slot > (uint64_t)fr) Gcap >>= 1;
+        }
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 30)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^30");
         chunk_parents = Gcap / ks.maxsucc;
@@ -1834,7 +1856,11 @@ struct rmc_ctx {
             trace_fence(s);
             // (timed with the winner count: PH_OTHER stays the probe pass alone)
             if (split && split_insert) timed(PH_DEDUP, [&] { ks.insert(params(), np_, stream); });
-            timed(PH_MAT, [&] { ks.commit(params(), stream); });  // + chunk summary
+            // + chunk summary; a split chunk's winners a lane per successor slot of its parents with winners
+            timed(PH_MAT, [&] {
+                if (split && nzlist && split_insert && split_flags == 7) ks.commit_split(params(), np_, stream);
+                else ks.commit(params(), stream);
+            });
             HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
             HIPCHK(hipGetLastError());
@@ -2475,7 +2501,11 @@ struct rmc_ctx {
                     inject(4, s.id, c, L);
                     grow_outbox(s, wwords[li], wnum[li]);
                     if (wwords[li] >= s.rcap) ensure_ring(s, wwords[li], 0);  // P.rcap also bounds the outbox
-                    timed(PH_MAT, [&] { ks.commit(round_params(s, gbase), stream); });
+                    timed(PH_MAT, [&] {
+                        const KParams Q = round_params(s, gbase);
+                        if (Q.plist) ks.commit_split(Q, s.np, stream);  // a lane per successor slot
+                        else ks.commit(Q, stream);
+                    });
                 });
             }
             for (size_t li = 0; li < NL; li++) {

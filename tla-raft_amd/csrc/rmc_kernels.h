@@ -172,6 +172,8 @@ struct KernelSet {
     void (*wincount)(const KParams &, uint64_t np, hipStream_t);  // winners per parent + their scan, successors generated
     void (*commit)(const KParams &, hipStream_t);           // winners -> next level, seen set, trace, invariants;
                                                             // chunk summary (and the device loop's next level)
+    void (*commit_split)(const KParams &, uint64_t np, hipStream_t);  // ... a lane per successor slot of the parents
+                                                            // with winners (plist; LS_WIN verdicts) + summary
     void (*fp_states)(const KParams &, uint64_t n, hipStream_t);  // fp of front[0..n) -> fp
     void (*inv_states)(const KParams &, uint64_t n, int32_t *out, hipStream_t); // per state: 1/0/-1 for inv_mask bits
     // host codec of the packed core (rmc_spec.h Codec)

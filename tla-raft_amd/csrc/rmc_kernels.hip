@@ -2292,6 +2292,159 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
     if (last_commit_block(P.ctick, nb)) finish_level<MX, S::RECW_MAX>(P);
 }
 
+// ---- split chunk / sharded round commit: a lane per successor slot ------------------------------
+// The wave-per-parent commit (k_commit) runs a parent's few winners on a few of its 64 lanes, and
+// most of its time waits on one parent's chain of round trips.  Here a wave takes 64 consecutive
+// parents with winners (plist), their successor counts scanned across the wave, and successor i of
+// the group goes to lane i % 64 of round i / 64 (as each_successor); every lane whose slot won
+// (lslot == LS_WIN: the split chunk's k_insert_winners verdict, or the owner's in a sharded round)
+// rebuilds its state from the parent's record core and its staged row, encodes it, writes its record
+// -- core words, then the parent's message ids merged with the ones its action added -- at its next-
+// level word offset, its trace entry (or sidecar) and checks the INVARIANTs.  A parent's winners are
+// consecutive lanes of a round (or run on into the next), so its winners' ordinals and word offsets
+// are segmented scans across the wave plus what the parent's part of the previous round carried.
+// The chunk summary follows in k_commit_finish.
+template <int N, int V, int MR, int MX>
+__global__ __launch_bounds__(256) void k_commit_split(KParams P) {
+    using S = Spec<N, V, MR>;
+    using Lo = Layout<N, V>;
+    constexpr int CCW = S::CCW;
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const uint64_t nvis = P.sum[SUM_NZ];
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t g0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; g0 < nvis;
+         g0 += nwaves * 64) {
+        const uint64_t k = g0 + (uint64_t)lane;
+        const uint32_t pl_l = k < nvis ? P.plist[k] : 0u;  // this lane's parent with winners (chunk-local)
+        const uint32_t t = k < nvis ? P.cnt[pl_l] : 0u;
+        uint32_t tot;
+        const uint32_t ex = wave_excl_scan(t, lane, &tot);
+        uint32_t cw = 0, cs = 0;  // winners / record words the previous round gave the group's parent cj
+        int cj = -1;
+        for (uint32_t b0 = 0; b0 < tot; b0 += 64) {
+            const uint32_t i = b0 + (uint32_t)lane;
+            int j = 0;  // the last group entry j with ex[j] <= i
+#pragma unroll
+            for (int st = 32; st; st >>= 1) {
+                const uint32_t v = (uint32_t)__shfl(ex, j + st, 64);
+                j = v <= i ? j + st : j;
+            }
+            const uint32_t r = i - (uint32_t)__shfl(ex, j, 64);
+            const uint32_t pl = (uint32_t)__shfl(pl_l, j, 64);
+            const uint64_t q = (uint64_t)pl * MX + r;
+            const bool win = i < tot && P.lslot[q] == LS_WIN;
+            const uint64_t p = P.p_begin + pl;
+            uint4 sa = make_uint4(0u, 0u, 0u, 0u), sb = sa, sc = sa;
+            uint32_t pk[CCW], c[Lo::NW];
+            uint32_t nm = 0, nadd = 0, size = 0;
+            uint64_t start = 0;
+            if (win) {
+                const uint4 *src = P.score + q * (uint64_t)S::SW4;
+                sa = src[0];
+                sb = src[1];
+                if (S::SW4 > 2) sc = src[2];
+                start = ring_wrap(P.fbase + P.foff[p], P.rcap);
+#pragma unroll
+                for (int w = 0; w < CCW; w++) pk[w] = ring_word(P.front, start, (uint32_t)w, P.rcap);
+                uint32_t pc[Lo::NW];
+                decode_core<N, V>(pk, pc);
+                unstage_core<N, V>(pc, sa, sb, c);
+                encode_core<N, V>(c, pk);
+                nm = (pc[Lo::W_MISC] >> 16) & 0xFFu;
+                nadd = sb.z >> 16;
+                size = (uint32_t)CCW + ((nm + nadd + 1u) >> 1);
+            }
+            // segmented (by parent) exclusive winner count and word offset, plus the carry
+            const uint64_t wm = __ballot(win);
+            const int j0 = __builtin_amdgcn_readfirstlane(j);
+            const uint32_t r0 = __builtin_amdgcn_readfirstlane(r);
+            const int seg = lane - (int)(j == j0 ? r - r0 : r);  // first lane of this lane's parent in the round
+            uint32_t ord = (uint32_t)__popcll(wm & lt_mask & ~((1ull << seg) - 1ull));
+            uint32_t szt;
+            const uint32_t szx = wave_excl_scan(size, lane, &szt);
+            uint32_t wofs = szx - (uint32_t)__shfl(szx, seg, 64);
+            if (j == cj) {
+                ord += cw;
+                wofs += cs;
+            }
+            {  // what the round's last parent carries into the next round
+                const int jl = __builtin_amdgcn_readlane(j, 63), sl = __builtin_amdgcn_readlane(seg, 63);
+                const uint32_t szl = __builtin_amdgcn_readlane(szx, sl);
+                const uint32_t w_in = (uint32_t)__popcll(wm & ~((1ull << sl) - 1ull));
+                const bool cont = jl == cj;
+                cw = w_in + (cont ? cw : 0u);
+                cs = (szt - szl) + (cont ? cs : 0u);
+                cj = jl;
+            }
+            if (!win) continue;
+            const uint32_t tile = pl / WTILE;
+            const uint64_t out = P.next_base + P.boff[tile] + P.wpos[pl] + ord;
+            const uint64_t wd = P.next_wbase + P.boffw[tile] + P.wposw[pl] + wofs;  // level-relative
+            const uint64_t rs = ring_wrap(P.nbase + wd, P.rcap);
+            P.noff[out] = wd;
+#pragma unroll
+            for (int w = 0; w < CCW; w++) P.next[ring_wrap(rs + (uint32_t)w, P.rcap)] = pk[w];
+            // the parent's sorted ids merged with the added ones (sorted here: BecomeCandidate adds
+            // its VoteReqs in peer order), written a word at a time, the last half-word padded
+            uint32_t add[4] = {sb.w & 0xFFFFu, sb.w >> 16, sc.x & 0xFFFFu, sc.x >> 16};
+#pragma unroll
+            for (int a = 0; a < S::NADD; a++)
+#pragma unroll
+                for (int b = 0; b + 1 < S::NADD - a; b++)
+                    if ((uint32_t)(b + 1) < nadd && add[b + 1] < add[b]) {
+                        const uint32_t x = add[b];
+                        add[b] = add[b + 1];
+                        add[b + 1] = x;
+                    }
+            const uint64_t pid = ring_wrap(start + CCW, P.rcap), oid = ring_wrap(rs + CCW, P.rcap);
+            uint32_t kk = 0, a = 0, word = 0, pw = 0;
+            const uint32_t tot_ids = nm + nadd;
+            for (uint32_t o = 0; o < tot_ids; o++) {
+                uint32_t next_add = 0xFFFFFFFFu;
+#pragma unroll
+                for (int b = 0; b < S::NADD; b++) next_add = (uint32_t)b == a ? add[b] : next_add;
+                if (kk < nm && (kk & 1u) == 0u) pw = ring_word(P.front, pid, kk >> 1, P.rcap);
+                const uint32_t pv = (pw >> ((kk & 1u) * 16u)) & 0xFFFFu;
+                uint32_t id;
+                if (a < nadd && (kk >= nm || next_add < pv)) {
+                    id = next_add;
+                    a++;
+                } else {
+                    id = pv;
+                    kk++;
+                }
+                if (o & 1u) P.next[ring_wrap(oid + (o >> 1), P.rcap)] = word | (id << 16);
+                else word = id;
+            }
+            if (tot_ids & 1u) P.next[ring_wrap(oid + (tot_ids >> 1), P.rcap)] = word;
+            const uint32_t key = sb.z & 0xFFFFu;
+            if (P.route) {
+                // sharded round: the trace entry travels with the record to the state's next-level owner
+                const uint64_t pref = P.gid_parent_base + p;
+                P.xside[out] = make_uint4((uint32_t)pref, (uint32_t)(pref >> 32), key, size);
+            } else {
+                const uint64_t gid = P.gid_next_base + out;
+                P.par[gid - P.trace_base] = P.gid_parent_base + p;
+                P.pslot[gid - P.trace_base] = (uint16_t)key;
+            }
+            int which = 0;
+            const MsgView mv{P.front, pid, P.rcap, nm, sb.w, sc.x, nadd, P.t.info};
+            const int iv = check_invs<N, V>(c, P.inv_order, &which, mv);
+            if (iv != 1) {
+                const unsigned long long ek = ((((unsigned long long)p << 16) | key) << 8) | (unsigned long long)which;
+                atomicMin(&P.err[iv == 0 ? ERR_INV : ERR_EVAL], ek);
+            }
+        }
+    }
+}
+
+// the chunk summary after k_commit_split (one wave): finish_level
+template <int MX, int RECW_MAX>
+__global__ __launch_bounds__(64) void k_commit_finish(KParams P) {
+    finish_level<MX, RECW_MAX>(P);
+}
+
 static inline unsigned grid_for(uint64_t n) {
     const uint64_t cap = 256ull * RMC_GRID_PER_CU;  // one-wave blocks per CU (default 32) on 256 CUs
     return (unsigned)(n < cap ? (n ? n : 1) : cap);
@@ -2329,6 +2482,12 @@ struct Launch {
     static void commit(const KParams &P, hipStream_t s) {
         hipLaunchKernelGGL((k_commit<N, V, MR, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
     }
+    static void commit_split(const KParams &P, uint64_t np, hipStream_t s) {
+        const uint64_t blocks = (np + 255) / 256;  // a wave per 64 parents with winners (at most np of them)
+        hipLaunchKernelGGL((k_commit_split<N, V, MR, MX>), dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u),
+                           dim3(256), 0, s, P);
+        hipLaunchKernelGGL((k_commit_finish<MX, Spec<N, V, MR>::RECW_MAX>), dim3(1), dim3(64), 0, s, P);
+    }
     static void fps(const KParams &P, uint64_t n, hipStream_t s) {
         hipLaunchKernelGGL((k_fp_states<N, V, MR>), dim3(grid_for(n)), dim3(64), 0, s, P, n);
     }
@@ -2352,6 +2511,7 @@ static void fill(KernelSet *ks) {
     ks->insert = &Launch<N, V, MR, BFV>::insert;
     ks->wincount = &Launch<N, V, MR>::wincount;
     ks->commit = &Launch<N, V, MR, BFV>::commit;
+    ks->commit_split = &Launch<N, V, MR, BFV>::commit_split;
     ks->fp_states = &Launch<N, V, MR>::fps;
     ks->inv_states = &Launch<N, V, MR>::invs;
     ks->encode = &Launch<N, V, MR>::enc;

@@ -258,6 +258,8 @@ int run_ranks(int N, bool onerank, const rmc_config &base, const std::function<i
             ::close(up[0]);
             if (r != 0) ::close(up[1]);  // (only rank 0 writes up: the others must not hold it open)
             for (int q = 0; q < r; q++) ::close(down[q]);
+            // RCCL's own messages (its version line, warnings) go to stderr: stdout is TLC's
+            ::setenv("NCCL_DEBUG_FILE", "/dev/stderr", 0);
             unsigned char id[128];
             if (r == 0) {
                 const int rc = rmc_comm_unique_id(id);
@@ -428,7 +430,18 @@ int main(int argc, char **argv) {
     const auto t0 = std::chrono::steady_clock::now();
     void *ctx = nullptr;
     phase_time("create");
+    // a rank's communicator set-up prints RCCL's banner on stdout: send it to stderr (stdout is TLC's)
+    const int saved_out = cfg.comm_unique_id ? ::dup(1) : -1;
+    if (saved_out >= 0) {
+        std::fflush(stdout);
+        ::dup2(2, 1);
+    }
     int rc = rmc_create(&cfg, &ctx);
+    if (saved_out >= 0) {
+        std::fflush(stdout);
+        ::dup2(saved_out, 1);
+        ::close(saved_out);
+    }
     phase_time("created");
     if (rc != RMC_OK) { std::printf("Error: could not start the GPU model checker (code %d)\n", rc); return 75; }
     rmc_level_stats st;
@@ -466,6 +479,7 @@ int main(int argc, char **argv) {
     };
     auto last_progress = std::chrono::steady_clock::now();
     bool reported = false, have_last = false;
+    int printed_level = -1;  // the level of the last Progress line
     rmc_level_stats last{};
     while (rc == RMC_OK) {
         uint32_t nl = 0;
@@ -479,6 +493,7 @@ int main(int argc, char **argv) {
         if (!reported || std::chrono::duration<double>(now - last_progress).count() >= progress_s) {
             progress(last);
             reported = true;
+            printed_level = last.level;
             last_progress = now;
         }
         const double since = std::chrono::duration<double>(std::chrono::steady_clock::now() - last_ckpt).count();
@@ -499,7 +514,7 @@ int main(int argc, char **argv) {
         rmc_destroy(ctx);
         return 75;
     }
-    if (have_last) progress(last);  // the closing report
+    if (have_last && last.level != printed_level) progress(last);  // the closing report (once)
     rmc_result res;
     rmc_get_result(ctx, &res);
     int exit_code = 0;
