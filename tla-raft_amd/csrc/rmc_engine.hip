@@ -860,14 +860,20 @@ struct rmc_ctx {
         // on demand (ensure_chunk), so a small run does not pay for them; an RCCL rank allocates
         // them at create, its budgets may be explicit (bench's configs[3] leg).
         Gcap = cfg.chunk_successors ? cfg.chunk_successors : (virt ? (1ull << 23) : (1ull << 28));
-        if (!cfg.chunk_successors && (rccl || hostx) && (cfg.seen_mem_bytes || cfg.frontier_mem_bytes)) {
-            // a rank allocates its round buffers at create: with explicit seen-set / frontier budgets,
-            // halve the default round until those buffers fit beside the budgets in free memory
+        if (!cfg.chunk_successors && !virt && (cfg.seen_mem_bytes || cfg.frontier_mem_bytes)) {
+            // with explicit seen-set / frontier budgets (an RCCL rank allocates its round buffers at
+            // create; one GPU grows them to this size), halve the default chunk until its buffers
+            // fit beside the budgets in free memory
             // (per slot: fingerprint, verdict, staging, item out and in, route and owner words, ~2 election slots)
             size_t fr = 0, tot = 0;
             HIPCHK(hipMemGetInfo(&fr, &tot));
-            const uint64_t per_slot = 16 + 4 + 16 * (uint64_t)sw4() + 4 + 4 + 4 + 2 * sizeof(XItem) + 8 + 2 * 24;
-            const uint64_t budgets = cfg.seen_mem_bytes + cfg.frontier_mem_bytes + (4ull << 30);
+            // (per slot: fingerprint, verdict, staging, scan word, ~2 election slots; an RCCL rank also its
+            // route / owner words and items out and in)
+            const uint64_t per_slot = 16 + 4 + 16 * (uint64_t)sw4() + 4 + 2 * 24 +
+                                      ((rccl || hostx) ? 4 + 4 + 2 * sizeof(XItem) + 8 : 0);
+            // beside the budgets: the live levels' record offsets (8 B a state; the two widest levels
+            // of configs[3] hold about a third of its seen set's states) and some slack
+            const uint64_t budgets = cfg.seen_mem_bytes + cfg.frontier_mem_bytes + cfg.seen_mem_bytes / 2 + (4ull << 30);
             while (Gcap > (1ull << 24) && budgets + Gcap * per_slot > (uint64_t)fr) Gcap >>= 1;
         }
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
@@ -1041,8 +1047,11 @@ struct rmc_ctx {
     // offsets array with `used` entries kept
     void ensure_off(uint64_t *&p, uint64_t &cap, uint64_t used, uint64_t need) {
         if (need <= cap) return;
-        const uint64_t nc = std::max<uint64_t>(need + need / 2, cap * 2);
-        uint64_t *nb = dmalloc<uint64_t>(nc);
+        // room to grow (x1.5) when the device has it; near the memory budgets, what the level needs
+        uint64_t nc = std::max<uint64_t>(need + need / 2, cap * 2);
+        uint64_t *nb = dmalloc_try<uint64_t>(nc);
+        if (!nb) nb = dmalloc_try<uint64_t>(nc = need + need / 16);
+        if (!nb) nb = dmalloc<uint64_t>(nc = need);
         if (used) HIPCHK(hipMemcpyAsync(nb, p, used * 8, hipMemcpyDeviceToDevice, stream));
         HIPCHK(hipStreamSynchronize(stream));
         dfree(p);

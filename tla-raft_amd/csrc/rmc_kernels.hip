@@ -1488,6 +1488,7 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
                 cx[k] = v;
             }
             __syncthreads();  // M0 / M1 are cleared for the next parent
+            PHASE(4);
             continue;
         }
         // ---- fingerprints (rmc_spec.h): content matrix, signature coset, minimum -----------------

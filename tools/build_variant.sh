@@ -2,22 +2,19 @@
 # Build an experimental variant of librmc.so next to the default one:
 #   tools/build_variant.sh prof   -> tla-raft_amd/build_prof/librmc.so  (-DRMC_PHASE_PROF, tools/phase_prof.py)
 #   tools/build_variant.sh w1     -> tla-raft_amd/build_w1/librmc.so    (n >= 4 expansion at 1 wave / SIMD)
+#   tools/build_variant.sh sw5    -> tla-raft_amd/build_sw5/librmc.so   (split expansion at 5 waves / SIMD)
 # Select it with RMC_LIBRARY=<path> (raftmc.load_library).  Needs the default build (make -C tla-raft_amd).
 set -e
 cd "$(dirname "$0")/../tla-raft_amd"
 case "$1" in
   prof) FLAGS="-DRMC_PHASE_PROF" ;;
   w1) FLAGS="-DRMC_WIDE_WAVES=1" ;;
-  bm0) FLAGS="-DRMC_MSG_BITMAP=0" ;;  # k_expand: m \in msgs by binary search over the sorted ids
-  pm0) FLAGS="-DRMC_EXPAND_PREFETCH_MSGS=0" ;;  # k_expand without the next parent's message-table prefetch
-  hc0) FLAGS="-DRMC_HASH_COMPACT=0" ;;  # k_expand: successor hash rows once per candidate kind
-  cp2) FLAGS="-DRMC_COMMIT_PREFETCH=2" ;;  # k_commit: two headers ahead
-  cp0) FLAGS="-DRMC_COMMIT_PREFETCH=0" ;;  # k_commit without the next parent's header prefetch
-  ce1) FLAGS="-DRMC_COMMIT_EARLY=1" ;;  # k_commit: early seen-set insert (measured slower, off by default)
+  # the split (no fingerprint) expansion: waves / SIMD its registers are cut for (e.g. sw5)
+  sw*) FLAGS="-DRMC_SPLIT_WAVES=${1#sw}" ;;
   # n = 3 occupancy: expansion waves / SIMD, commit waves / SIMD, grid blocks / CU (e.g. n3w6c4g32)
   n3w*) X=${1#n3w}; W=${X%%c*}; X=${X#*c}; C=${X%%g*}; G=${X#*g}
         FLAGS="-DRMC_N3_WAVES=$W -DRMC_N3_COMMIT_WAVES=$C -DRMC_GRID_PER_CU=$G" ;;
-  *) echo "usage: $0 prof|w1|ce1|cp0|cp2|pm0|bm0|hc0|n3w<W>c<C>g<G>" >&2; exit 2 ;;
+  *) echo "usage: $0 prof|w1|sw<W>|n3w<W>c<C>g<G>" >&2; exit 2 ;;
 esac
 OUT=build_$1
 mkdir -p "$OUT"

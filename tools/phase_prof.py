@@ -6,7 +6,7 @@ RMC_LIBRARY=.../librmc.so.  Runs one configuration for --levels BFS levels (or t
 prints each phase's share of the waves' time in k_expand:
   0 load parent record (+ message hash rows)   1 evaluate actions (one candidate per lane)
   2 TLC-order ranks, error keys               3 staging of the successor rows (fused level)
-  4 parent/successor hash inputs (rows, signatures)
+  4 parent/successor hash inputs (rows, signatures); a split chunk's hash context
   5 symmetry minimum (+ seen-set probe / election on the n = 3 path)
   6 seen-set probe + election (n >= 4 signature path)
 
@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tla-raft_amd"))
 import raftmc  # noqa: E402
 
-NAMES = ["load parent", "evaluate actions", "ranks + error keys", "staging", "hash inputs",
+NAMES = ["load parent", "evaluate actions", "ranks + error keys", "staging", "hash inputs (split: hash context)",
          "symmetry min", "seen-set probe + election", "-",
          # k_commit (slots 8-15)
          "commit: header wait (+ parents w/o winners)", "commit: record + election words + staged rows",
