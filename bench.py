@@ -52,7 +52,7 @@ WORKLOADS = {
 HBM_PEAK_GBS = 8000.0
 PHASES = ["expand_count", "expand_hash", "dedup", "materialize", "exchange", "other"]
 TIMED_PHASES = 1 << PHASES.index("expand_hash")  # HIP-event timing of the dominant kernel only
-TIMING_EVERY = 4
+TIMING_EVERY = 8
 
 
 def alg_bytes(phase, F, G, N, S, CCWB, slot_bytes=16, SWB=32, split=False, CTXB=112):

@@ -444,6 +444,7 @@ struct Shard {
     // per-round host bookkeeping (sharded path): first parent, parents, successors, global index
     // of the round's first parent in the level
     uint64_t p0 = 0, np = 0, G = 0, gblk = 0;
+    uint64_t Gself = 0;  // the round's successors the shard owns itself (G: those it sends)
 };
 
 // the host-staged transport installed by rmc_set_transport (process-wide; read by rmc_create)
@@ -1367,7 +1368,7 @@ struct rmc_ctx {
     // device, an RCCL rank posts one send and one receive per peer and payload, all in one group.
     // RMC_SELF_VIA_RCCL=1: a rank's part for itself goes through ncclSend / ncclRecv like any other
     // (the one-rank RCCL tests use it to run those calls on a one-GPU box); by default it is a
-    // device copy, and the successor items are placed in the receive buffer by k_route_place
+    // device copy (the successor items have no part for their own shard: k_local_elect decides those)
     const bool self_rccl = env_int("RMC_SELF_VIA_RCCL", 0, 0, 1) != 0;
     struct Payload {
         const std::vector<XPlan> *plans;
@@ -2392,8 +2393,13 @@ struct rmc_ctx {
                 HIPCHK(hipMemcpyAsync(s.hsum, s.ocnt, 64 * 4, hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
                 const uint32_t *hc = reinterpret_cast<const uint32_t *>(s.hsum);
+                // successors the shard owns itself stay out of the exchange (k_local_elect)
                 s.G = 0;
-                for (int d = 0; d < W; d++) { rows[li][d] = hc[d]; s.G += hc[d]; }
+                s.Gself = s.np ? hc[s.id] : 0;
+                for (int d = 0; d < W; d++) {
+                    rows[li][d] = d == s.id ? 0 : hc[d];
+                    s.G += rows[li][d];
+                }
                 guard(li, [&] {
                     inject(1, s.id, c, L);
                     if (s.G) grow_plain(s.xs, s.xs_cap, s.G);
@@ -2429,7 +2435,7 @@ struct rmc_ctx {
             }
             SDBG("0");
             // (2) successors to their owners: owner-grouped items, cursors preset to the groups
-            Payload items{&xp, std::vector<const void *>(NL), std::vector<void *>(NL), sizeof(XItem), !self_rccl};
+            Payload items{&xp, std::vector<const void *>(NL), std::vector<void *>(NL), sizeof(XItem)};
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
                 if (s.G) {
@@ -2438,11 +2444,9 @@ struct rmc_ctx {
                     uint32_t *hc = reinterpret_cast<uint32_t *>(s.hsum + 96);
                     for (int d = 0; d < W; d++) hc[d] = (uint32_t)xp[li].send_off[d];
                     HIPCHK(hipMemcpyAsync(s.ocnt, hc, W * 4, hipMemcpyHostToDevice, stream));
-                    // items for this shard itself go straight to its receive buffer
-                    const int64_t delta = (int64_t)xp[li].recv_off[s.id] - (int64_t)xp[li].send_off[s.id];
                     timed(PH_XCHG, [&] {
                         launch_route_place(s.fp, s.cnt, s.np, (uint32_t)MS, (uint32_t)W, s.ocnt, s.gblk, s.xs, s.perm,
-                                           self_rccl ? nullptr : s.xr, (uint32_t)s.id, delta, stream);
+                                           (uint32_t)s.id, stream);
                     });
                 }
                 items.send[li] = s.xs;
@@ -2455,17 +2459,27 @@ struct rmc_ctx {
             Payload verdicts{&xb, std::vector<const void *>(NL), std::vector<void *>(NL), 4};
             for (size_t li = 0; li < NL; li++) {
                 Shard &o = sh[li];
-                const uint64_t R = xp[li].recv_total;
+                const uint64_t R = xp[li].recv_total, Rl = o.Gself;  // received / its own
                 verdicts.send[li] = o.rflag;
                 verdicts.recv[li] = o.sflag;
-                if (!R) continue;
+                if (!R && !Rl) continue;
                 guard(li, [&] {
                     inject(3, o.id, c, L);
-                    grow_seen(o, o.T_count + R);
-                    const uint64_t cap = owner_table(o, R);
+                    grow_seen(o, o.T_count + R + Rl);
+                    const uint64_t cap = owner_table(o, R + Rl);
                     timed(PH_DEDUP, [&] {
-                        launch_owner_elect(o.xr, R, o.seen(), o.OT, o.OK, cap - 1, o.ot_round, o.rslot, stream);
-                        launch_owner_flags(o.xr, R, o.rslot, o.OK, o.ot_round, o.seen(), o.rflag, o.sum + 9, stream);
+                        const KParams Q = round_params(o, gbase);
+                        if (Rl)
+                            ks.local_elect(Q, o.np, o.seen(), o.OT, o.OK, cap - 1, o.ot_round, (uint32_t)W,
+                                           (uint32_t)o.id, o.gblk, stream);
+                        if (R) {
+                            launch_owner_elect(o.xr, R, o.seen(), o.OT, o.OK, cap - 1, o.ot_round, o.rslot, stream);
+                            launch_owner_flags(o.xr, R, o.rslot, o.OK, o.ot_round, o.seen(), o.rflag, o.sum + 9,
+                                               stream);
+                        }
+                        if (Rl)
+                            ks.local_flags(Q, o.np, o.seen(), o.OK, o.ot_round, (uint32_t)W, (uint32_t)o.id, o.gblk,
+                                           o.sum + 9, stream);
                     });
                 });
                 // a failed owner answers "no winner" everywhere (the round is abandoned at the next agreement)

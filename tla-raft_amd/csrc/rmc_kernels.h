@@ -174,6 +174,12 @@ struct KernelSet {
                                                             // chunk summary (and the device loop's next level)
     void (*commit_split)(const KParams &, uint64_t np, hipStream_t);  // ... a lane per successor slot of the parents
                                                             // with winners (plist; LS_WIN verdicts) + summary
+    // sharded round, the successors the shard owns itself: bids in the round's owner table, then
+    // (every bid in) verdicts in lslot, winners into the seen set and onto wacc
+    void (*local_elect)(const KParams &, uint64_t np, Seen, ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
+                        uint32_t round, uint32_t W, uint32_t self, uint64_t g0, hipStream_t);
+    void (*local_flags)(const KParams &, uint64_t np, Seen, const unsigned long long *OK, uint32_t round, uint32_t W,
+                        uint32_t self, uint64_t g0, unsigned long long *inserted, hipStream_t);
     void (*fp_states)(const KParams &, uint64_t n, hipStream_t);  // fp of front[0..n) -> fp
     void (*inv_states)(const KParams &, uint64_t n, int32_t *out, hipStream_t); // per state: 1/0/-1 for inv_mask bits
     // host codec of the packed core (rmc_spec.h Codec)
@@ -207,8 +213,7 @@ struct XItem { unsigned long long x, y, key; };
 void launch_route_count(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
                         uint32_t *ocnt, hipStream_t s);
 void launch_route_place(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
-                        uint32_t *cursor, uint64_t g0, XItem *items, uint32_t *perm, XItem *self_items, uint32_t self,
-                        int64_t self_delta, hipStream_t s);
+                        uint32_t *cursor, uint64_t g0, XItem *items, uint32_t *perm, uint32_t self, hipStream_t s);
 void launch_owner_elect(const XItem *it, uint64_t R, Seen seen, ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
                         uint32_t round, uint32_t *rslot, hipStream_t s);
 void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const unsigned long long *OK, uint32_t round,

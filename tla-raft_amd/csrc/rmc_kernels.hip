@@ -1576,6 +1576,7 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
                 }
             }
             __syncthreads();
+            PHASE(4);
             if ((uint32_t)lane < nb) {  // (c2) signatures, tie ranks and coset size per successor
                 const uint32_t l = (uint32_t)lane, sv = sS[b0 + l];
                 uint64_t rs = 0;
@@ -1646,7 +1647,7 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
             PHASE(6);
             if ((uint32_t)lane < nb) emit(b0 + (uint32_t)lane, sBest[lane]);
             __syncthreads();
-            PHASE(5);
+            PHASE(7);
         }
         asm volatile("" ::"v"(nnstart));  // the offset two parents ahead is in by now: keep its load up top
         if (MODE == M_FUSED) continue;
@@ -2011,19 +2012,27 @@ template <int MAXS, int RECW_MAX>
 __device__ void finish_level(const KParams &P) {
     // one wave, everything it reads in flight at once: lanes 0..3 take the error slots, lane 4
     // the flags, lane 0 the summary and the control block
+    // (the summary words and the control block, which this launch does not write, go out with the
+    // exchanges: one round trip)
     const int lane = threadIdx.x;
+    unsigned long long *sm = P.sum;
+    unsigned long long G = 0, Wn = 0, Ww = 0;
+    LevelCtl c{};
+    if (lane == 0) {
+        G = sm[0];
+        Wn = sm[1];
+        Ww = sm[SUM_WORDS];
+        if (P.ctl) c = *P.ctl;
+    }
     unsigned long long e = 0;
     if (lane < ERR_NSLOTS)
         e = __hip_atomic_exchange(&P.err[lane], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else if (lane == ERR_NSLOTS)
         e = __hip_atomic_exchange(&P.flags[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool bad = __ballot(lane < ERR_NSLOTS ? e != ~0ull : (lane == ERR_NSLOTS && e != 0)) != 0;
-    unsigned long long *sm = P.sum;
     if (lane <= ERR_NSLOTS) sm[2 + lane] = e;
     if (lane != 0) return;
-    const unsigned long long G = sm[0], Wn = sm[1], Ww = sm[SUM_WORDS];
     if (!P.ctl) return;
-    LevelCtl c = *P.ctl;
     if (bad) {  // the host reports the error from this level's buffers
         P.ctl->stop = CTL_ERROR;
         if (P.hloop) {
@@ -2082,7 +2091,13 @@ __device__ __forceinline__ bool last_commit_block(uint32_t *tick, uint32_t nb) {
     if (blockIdx.x >= nb) return false;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t last = 0;
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && nb <= CTICK_SUB) {  // few blocks: straight to the top counter
+        uint32_t *top = tick + CTICK_SUB * CTICK_STRIDE;
+        if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1) {
+            __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = 1;
+        }
+    } else if (threadIdx.x == 0) {
         const uint32_t g = nb, b = blockIdx.x, sub = b % CTICK_SUB;
         const uint32_t nsub = g < CTICK_SUB ? g : CTICK_SUB;
         const uint32_t expect = (g - sub + CTICK_SUB - 1) / CTICK_SUB;  // blocks with b % CTICK_SUB == sub
@@ -2446,6 +2461,106 @@ __global__ __launch_bounds__(64) void k_commit_finish(KParams P) {
     finish_level<MX, RECW_MAX>(P);
 }
 
+// ---- sharded round: the owner's election (W > 1, and the one-rank rehearsal) -------------------
+// owner(fp) = high bits of fp.y mod W -- independent of the seen-set and election index bits
+__device__ __forceinline__ uint32_t fp_owner(const ulonglong2 f, uint32_t W) {
+    return (uint32_t)((f.y >> 40) % W);
+}
+
+// A fingerprint already in the seen set loses; otherwise it takes (or finds) its slot in the
+// round's election table and bids its key.  The table is cleared only every 65533 rounds
+// (owner_table): `round` counts the rounds since, and both words of a slot carry its 16-bit tag
+// round + 1 in their low bits, so a slot of an earlier round reads as free, and a key word is the
+// round's key below ((0xFFFF - tag) << 48) -- smaller than any earlier round's -- so every bid just
+// takes the minimum (OT: fingerprint, OK: smallest tagged key; the same protocol as the fused
+// election).  key = (parent's global index in the level << 10) | rank: TLC's order of the level.
+__device__ __forceinline__ unsigned long long owner_key(uint32_t tag, uint64_t key) {
+    return ((unsigned long long)(0xFFFFu - tag) << 48) | key;  // key = global parent index << 10 | rank < 2^48
+}
+__device__ __forceinline__ uint32_t owner_bid(ulonglong2 *OT, unsigned long long *OK, uint64_t mask, uint32_t tag32,
+                                              const ulonglong2 f, uint64_t key) {
+    const unsigned long long tag = tag32;
+    const unsigned long long xk = (f.x & ~0xFFFFull) | tag, yk = (f.y & ~0xFFFFull) | tag;
+    // one exit at the bottom (no break): a claimer stores its y inside the loop, in the same
+    // iteration as its CAS, before any lane of its wave waits for that y (a divergent break
+    // lets the compiler defer the claimer's store until every lane has left the loop)
+    uint64_t g = l_index(f, mask);
+    unsigned long long v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool done = false;
+    while (!done) {
+        bool next = false;
+        if ((v & 0xFFFFull) != tag) {  // free, or an earlier round's: claim it
+            const unsigned long long prev = atomicCAS(&OT[g].x, v, xk);
+            if (prev == v) {
+                __hip_atomic_store(&OT[g].y, yk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                done = true;
+            } else {
+                v = prev;
+            }
+        }
+        if (!done && (v & 0xFFFFull) == tag) {
+            if (v == xk) {
+                const unsigned long long y = __hip_atomic_load(&OT[g].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (y == yk) done = true;
+                else if ((y & 0xFFFFull) == tag) next = true;
+                else v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // y not visible yet
+            } else {
+                next = true;
+            }
+        }
+        if (next) {
+            g = (g + 1) & mask;
+            v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    atomicMin(&OK[g], owner_key(tag32, key));
+    return (uint32_t)g;
+}
+
+// Owner's own successors (fingerprint owner == self), a lane each: they bid in the round's table
+// straight from the expansion's slots -- no item through the exchange -- and the slot (or LS_SEEN)
+// waits in lslot for k_local_flags.  Successors other shards own are marked LS_ELECT and left to
+// the exchange (their verdicts arrive by k_scatter_win).
+template <int MX>
+__global__ __launch_bounds__(256) void k_local_elect(KParams P, Seen seen, ulonglong2 *OT, unsigned long long *OK,
+                                                     uint64_t mask, uint32_t round, uint32_t W, uint32_t self,
+                                                     uint64_t g0) {
+    each_successor<MX>(P, [&](uint64_t pl, uint32_t r) {
+        const uint64_t q = pl * (uint64_t)MX + r;
+        const ulonglong2 f = P.fp[q];
+        P.lslot[q] = fp_owner(f, W) != self ? LS_ELECT
+                     : seen_contains(seen, f) ? LS_SEEN
+                                              : owner_bid(OT, OK, mask, round + 1u, f, ((g0 + pl) << 10) | r);
+    });
+}
+
+// ... once every bid of the round is in (the received ones too): the verdict in lslot (LS_WIN /
+// LS_SEEN), each winner into the seen set and counted on its parent as k_scatter_win counts a
+// received verdict (wacc = winners | extra words << 12), *inserted counting them.
+template <int MX, int SW4>
+__global__ __launch_bounds__(256) void k_local_flags(KParams P, Seen seen, const unsigned long long *OK, uint32_t round,
+                                                     uint32_t W, uint32_t self, uint64_t g0,
+                                                     unsigned long long *inserted) {
+    const uint32_t tag = round + 1u;
+    uint32_t mine = 0;
+    each_successor<MX>(P, [&](uint64_t pl, uint32_t r) {
+        const uint64_t q = pl * (uint64_t)MX + r;
+        const uint32_t g = P.lslot[q];
+        if (g == LS_ELECT || g == LS_SEEN) return;  // another shard's, or seen: nothing to decide
+        const bool w = OK[g] == owner_key(tag, ((g0 + pl) << 10) | r);
+        P.lslot[q] = w ? LS_WIN : LS_SEEN;
+        if (w) {
+            seen_insert(seen, P.fp[q]);
+            const uint32_t nadd = P.score[q * (uint64_t)SW4 + 1].z >> 16;
+            const uint32_t e = (nadd + (P.pnm[pl] & 1u) + 1u) >> 1;
+            atomicAdd(&P.wacc[pl], 1u + (e << 12));
+            mine++;
+        }
+    });
+    for (int d = 32; d >= 1; d >>= 1) mine += __shfl_xor(mine, d, 64);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(inserted, (unsigned long long)mine);
+}
+
 static inline unsigned grid_for(uint64_t n) {
     const uint64_t cap = 256ull * RMC_GRID_PER_CU;  // one-wave blocks per CU (default 32) on 256 CUs
     return (unsigned)(n < cap ? (n ? n : 1) : cap);
@@ -2489,6 +2604,19 @@ struct Launch {
                            dim3(256), 0, s, P);
         hipLaunchKernelGGL((k_commit_finish<MX, Spec<N, V, MR>::RECW_MAX>), dim3(1), dim3(64), 0, s, P);
     }
+    static void local_elect(const KParams &P, uint64_t np, Seen seen, ulonglong2 *OT, unsigned long long *OK,
+                            uint64_t mask, uint32_t round, uint32_t W, uint32_t self, uint64_t g0, hipStream_t s) {
+        const uint64_t blocks = (np + 255) / 256;  // a wave per 64 parents (each_successor)
+        hipLaunchKernelGGL((k_local_elect<MX>), dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u),
+                           dim3(256), 0, s, P, seen, OT, OK, mask, round, W, self, g0);
+    }
+    static void local_flags(const KParams &P, uint64_t np, Seen seen, const unsigned long long *OK, uint32_t round,
+                            uint32_t W, uint32_t self, uint64_t g0, unsigned long long *inserted, hipStream_t s) {
+        const uint64_t blocks = (np + 255) / 256;
+        hipLaunchKernelGGL((k_local_flags<MX, Spec<N, V, MR>::SW4>),
+                           dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u), dim3(256), 0, s, P,
+                           seen, OK, round, W, self, g0, inserted);
+    }
     static void fps(const KParams &P, uint64_t n, hipStream_t s) {
         hipLaunchKernelGGL((k_fp_states<N, V, MR>), dim3(grid_for(n)), dim3(64), 0, s, P, n);
     }
@@ -2513,6 +2641,8 @@ static void fill(KernelSet *ks) {
     ks->wincount = &Launch<N, V, MR>::wincount;
     ks->commit = &Launch<N, V, MR, BFV>::commit;
     ks->commit_split = &Launch<N, V, MR, BFV>::commit_split;
+    ks->local_elect = &Launch<N, V, MR, BFV>::local_elect;
+    ks->local_flags = &Launch<N, V, MR, BFV>::local_flags;
     ks->fp_states = &Launch<N, V, MR>::fps;
     ks->inv_states = &Launch<N, V, MR>::invs;
     ks->encode = &Launch<N, V, MR>::enc;
@@ -2599,11 +2729,6 @@ void launch_rebase(const uint64_t *in, uint64_t n, uint64_t sub, uint64_t *out, 
 }
 
 // ---- sharded round (W > 1) -------------------------------------------------------------------
-// owner(fp) = high bits of fp.y mod W -- independent of the seen-set and election index bits
-__device__ __forceinline__ uint32_t fp_owner(const ulonglong2 f, uint32_t W) {
-    return (uint32_t)((f.y >> 40) % W);
-}
-
 // Source: successors of the round's parents (sparse slots q = pl * maxsucc + r, r < cnt[pl]) per
 // owner, into ocnt[W] (zeroed by the caller).
 __global__ __launch_bounds__(256) void k_route_count(const ulonglong2 *__restrict__ fp, const uint32_t *__restrict__ cnt,
@@ -2619,23 +2744,26 @@ __global__ __launch_bounds__(256) void k_route_count(const ulonglong2 *__restric
     if (threadIdx.x < W && h[threadIdx.x]) atomicAdd(&ocnt[threadIdx.x], h[threadIdx.x]);
 }
 
-// Source: every successor to its owner's segment of the send buffer (cursor[o] = the segment's
-// next free item, preset to its start): {fingerprint, global key = (parent's global index in the
-// level << 10) | rank among its successors (< 1024, checked at create)} -- the key orders the level's successors as TLC
-// generates them -- and perm[item] = its slot q, for the owner's verdict to come back to.
-// Items owned by the source itself (owner == self) go straight to their place in its receive
-// buffer (self_items[pos + self_delta]): no copy of them through the exchange.
+// Source: every successor another shard owns to that owner's segment of the send buffer
+// (cursor[o] = the segment's next free item, preset to its start): {fingerprint, global key =
+// (parent's global index in the level << 10) | rank among its successors (< 1024, checked at
+// create)} -- the key orders the level's successors as TLC generates them -- and perm[item] = its
+// slot q, for the owner's verdict to come back to.  Successors the source owns itself stay where
+// they are: k_local_elect / k_local_flags decide them.
 __global__ __launch_bounds__(256) void k_route_place(const ulonglong2 *__restrict__ fp, const uint32_t *__restrict__ cnt,
                                                      uint64_t np, uint32_t maxsucc, uint32_t W, uint32_t *__restrict__ cursor,
                                                      uint64_t g0, XItem *__restrict__ items, uint32_t *__restrict__ perm,
-                                                     XItem *__restrict__ self_items, uint32_t self, int64_t self_delta) {
+                                                     uint32_t self) {
     __shared__ uint32_t h[64], base[64];
     for (uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x; t0 < np; t0 += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t pl = t0 + threadIdx.x;
         if (threadIdx.x < 64) h[threadIdx.x] = 0;
         __syncthreads();
         const uint32_t t = pl < np ? cnt[pl] : 0u;
-        for (uint32_t r = 0; r < t; r++) atomicAdd(&h[fp_owner(fp[pl * maxsucc + r], W)], 1u);
+        for (uint32_t r = 0; r < t; r++) {
+            const uint32_t o = fp_owner(fp[pl * maxsucc + r], W);
+            if (o != self) atomicAdd(&h[o], 1u);
+        }
         __syncthreads();
         if (threadIdx.x < W) {
             const uint32_t c = h[threadIdx.x];
@@ -2647,70 +2775,24 @@ __global__ __launch_bounds__(256) void k_route_place(const ulonglong2 *__restric
             const uint64_t q = pl * maxsucc + r;
             const ulonglong2 f = fp[q];
             const uint32_t o = fp_owner(f, W);
+            if (o == self) continue;
             const uint32_t pos = base[o] + atomicAdd(&h[o], 1u);
-            const XItem it{f.x, f.y, ((g0 + pl) << 10) | r};
-            if (o == self && self_items) self_items[(int64_t)pos + self_delta] = it;
-            else items[pos] = it;
+            items[pos] = XItem{f.x, f.y, ((g0 + pl) << 10) | r};
             perm[pos] = (uint32_t)q;
         }
         __syncthreads();
     }
 }
 
-// Owner: the received successors of the round.  A fingerprint already in the seen set loses;
-// otherwise it takes (or finds) its slot in the round's election table and bids its key.  The table
-// is cleared only every 65533 rounds (owner_table): `round` counts the rounds since, and both words
-// of a slot carry its 16-bit tag round + 1 in their low bits, so a slot of an earlier round reads as
-// free, and a key word is the round's key below ((0xFFFF - tag) << 48) -- smaller than any earlier
-// round's -- so every bid just takes the minimum (OT: fingerprint, OK: smallest tagged key; the same
-// protocol as the fused election).
-__device__ __forceinline__ unsigned long long owner_key(uint32_t tag, uint64_t key) {
-    return ((unsigned long long)(0xFFFFu - tag) << 48) | key;  // key = global parent index << 10 | rank < 2^48
-}
-
+// Owner: the received successors of the round -- bids (owner_bid) by k_owner_elect, and by the
+// owner's own successors in k_local_elect.
 __global__ __launch_bounds__(256) void k_owner_elect(const XItem *__restrict__ it, uint64_t R, Seen seen,
                                                      ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
                                                      uint32_t round, uint32_t *__restrict__ rslot) {
-    const unsigned long long tag = round + 1u;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
         const XItem e = it[i];
         const ulonglong2 f = make_ulonglong2(e.x, e.y);
-        if (seen_contains(seen, f)) { rslot[i] = LS_SEEN; continue; }
-        const unsigned long long xk = (f.x & ~0xFFFFull) | tag, yk = (f.y & ~0xFFFFull) | tag;
-        // one exit at the bottom (no break): a claimer stores its y inside the loop, in the same
-        // iteration as its CAS, before any lane of its wave waits for that y (a divergent break
-        // lets the compiler defer the claimer's store until every lane has left the loop)
-        uint64_t g = l_index(f, mask);
-        unsigned long long v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bool done = false;
-        while (!done) {
-            bool next = false;
-            if ((v & 0xFFFFull) != tag) {  // free, or an earlier round's: claim it
-                const unsigned long long prev = atomicCAS(&OT[g].x, v, xk);
-                if (prev == v) {
-                    __hip_atomic_store(&OT[g].y, yk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    done = true;
-                } else {
-                    v = prev;
-                }
-            }
-            if (!done && (v & 0xFFFFull) == tag) {
-                if (v == xk) {
-                    const unsigned long long y = __hip_atomic_load(&OT[g].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (y == yk) done = true;
-                    else if ((y & 0xFFFFull) == tag) next = true;
-                    else v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // y not visible yet
-                } else {
-                    next = true;
-                }
-            }
-            if (next) {
-                g = (g + 1) & mask;
-                v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        atomicMin(&OK[g], owner_key((uint32_t)tag, e.key));
-        rslot[i] = (uint32_t)g;
+        rslot[i] = seen_contains(seen, f) ? LS_SEEN : owner_bid(OT, OK, mask, round + 1u, f, e.key);
     }
 }
 
@@ -2783,11 +2865,10 @@ void launch_route_count(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, 
     if (np) hipLaunchKernelGGL(k_route_count, dim3(grid256(np)), dim3(256), 0, s, fp, cnt, np, maxsucc, W, ocnt);
 }
 void launch_route_place(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
-                        uint32_t *cursor, uint64_t g0, XItem *items, uint32_t *perm, XItem *self_items, uint32_t self,
-                        int64_t self_delta, hipStream_t s) {
+                        uint32_t *cursor, uint64_t g0, XItem *items, uint32_t *perm, uint32_t self, hipStream_t s) {
     if (np)
         hipLaunchKernelGGL(k_route_place, dim3(grid256(np)), dim3(256), 0, s, fp, cnt, np, maxsucc, W, cursor, g0, items,
-                           perm, self_items, self, self_delta);
+                           perm, self);
 }
 void launch_owner_elect(const XItem *it, uint64_t R, Seen seen, ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
                         uint32_t round, uint32_t *rslot, hipStream_t s) {

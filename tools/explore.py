@@ -28,6 +28,7 @@ ap.add_argument("--seen-mem-gb", type=float, default=0)
 ap.add_argument("--frontier-mem-gb", type=float, default=0)
 ap.add_argument("--rccl1", action="store_true", help="the sharded protocol on a one-rank RCCL communicator")
 ap.add_argument("--shard-min", type=int, default=0)
+ap.add_argument("--us", action="store_true", help="phase kernel times in microseconds")
 a = ap.parse_args()
 extra = dict(world_size=1, rank=0, comm_unique_id=raftmc.comm_unique_id()) if a.rccl1 else {}
 cfg = raftmc.ModelConfig(n_servers=a.n, n_vals=a.V, max_election=a.E, max_restart=a.R,
@@ -50,7 +51,7 @@ while ls.status == "ok" and time.time() - t1 < a.budget and not (a.levels and ls
         print(f"STOPPED at level {ls.level + 1}: {e}", flush=True)
         break
     el = time.time() - t1
-    ms = " ".join(f"{x:.1f}" for x in ls.kernel_ms)
+    ms = " ".join(f"{x * 1e3:.0f}" if a.us else f"{x:.1f}" for x in ls.kernel_ms)
     print(f"L{ls.level:3d} F={ls.expanded:>11d} G={ls.generated:>12d} N={ls.new_states:>11d} "
           f"tot={ls.total_distinct:>12d} {ls.seconds * 1e3:9.1f}ms [{ms}] el={el:.1f}s "
           f"{ls.total_distinct / el:.3e} ds/s rec={ls.new_bytes / max(1, ls.new_states):.1f}B", flush=True)

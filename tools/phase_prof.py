@@ -6,9 +6,9 @@ RMC_LIBRARY=.../librmc.so.  Runs one configuration for --levels BFS levels (or t
 prints each phase's share of the waves' time in k_expand:
   0 load parent record (+ message hash rows)   1 evaluate actions (one candidate per lane)
   2 TLC-order ranks, error keys               3 staging of the successor rows (fused level)
-  4 parent/successor hash inputs (rows, signatures); a split chunk's hash context
-  5 symmetry minimum (+ seen-set probe / election on the n = 3 path)
-  6 seen-set probe + election (n >= 4 signature path)
+  4 parent content matrix, successor row inputs, acting-row contents; a split chunk's hash context
+  5 signatures, coset ranks and sizes    6 hash tasks (coset minimum)
+  7 seen-set probe + election (fused levels)
 
 usage: RMC_LIBRARY=tla-raft_amd/build_prof/librmc.so python tools/phase_prof.py N V E R [--levels L]"""
 import argparse
@@ -21,8 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tla-raft_amd"))
 import raftmc  # noqa: E402
 
-NAMES = ["load parent", "evaluate actions", "ranks + error keys", "staging", "hash inputs (split: hash context)",
-         "symmetry min", "seen-set probe + election", "-",
+NAMES = ["load parent", "evaluate actions", "ranks + error keys", "staging", "hash inputs, acting-row contents (split: hash context)",
+         "signatures, coset ranks", "hash tasks (coset minimum)", "seen-set probe + election (fused)",
          # k_commit (slots 8-15)
          "commit: header wait (+ parents w/o winners)", "commit: record + election words + staged rows",
          "commit: winner test", "-", "commit: rebuild, encode, seen insert, trace, invariants",
