@@ -1690,7 +1690,7 @@ struct rmc_ctx {
                 n += hi - lo;
                 words += hoff[hi] - hoff[lo];
             }
-            const uint64_t cap = std::max<uint64_t>(words + words / 2, 1ull << 14);
+            uint64_t cap = std::max<uint64_t>(words + words / 2, 1ull << 14);
             uint32_t *nr = dmalloc<uint32_t>(cap);
             uint64_t *noff = dmalloc<uint64_t>(std::max<uint64_t>(n + n / 2, 1 << 16));
             uint64_t at = 0, wat = 0;
@@ -1735,6 +1735,15 @@ struct rmc_ctx {
                 t.epoch = std::max(t.epoch, s0.epoch);
                 dfree(t.R);
                 dfree(t.cur_off);
+            } else if (was_fixed && sh.size() == 1) {
+                // a rank's ring already at its budget stays: its part of the level goes back to the
+                // ring's start (freeing and allocating ~100 GB again took ~3 s on MI355X)
+                old_off_ = s0.cur_off;
+                if (words) HIPCHK(hipMemcpyAsync(s0.R, nr, words * 4, hipMemcpyDeviceToDevice, stream));
+                HIPCHK(hipStreamSynchronize(stream));
+                dfree(nr);
+                nr = s0.R;
+                cap = src_cap;
             } else {
                 old_rings.push_back(s0.R);
                 old_off_ = s0.cur_off;
@@ -1757,7 +1766,7 @@ struct rmc_ctx {
         dfree(old_off_);
         old_off_ = nullptr;
         if (was_fixed)
-            for (Shard &t : sh) fix_ring(t, sh.size());
+            for (Shard &t : sh) fix_ring(t, sh.size());  // (a kept ring: already at its budget)
         replicated = false;
     }
     uint64_t *old_off_ = nullptr;
@@ -2374,16 +2383,19 @@ struct rmc_ctx {
                 HIPCHK(hipMemsetAsync(s.ocnt, 0, 64 * 4, stream));
                 HIPCHK(hipMemsetAsync(s.sum + 9, 0, 8, stream));
                 if (!s.np || fail[li]) continue;
+                const bool split = split_min && s.np >= split_min;
                 timed(PH_HASH, [&] {
-                    const KParams Q = round_params(s, gbase);
-                    if (split_min && s.np >= split_min) {  // fingerprints a lane per successor (route: no probe)
+                    KParams Q = round_params(s, gbase);
+                    if (split) {  // fingerprints a lane per successor (route: no probe), counted per owner
+                        Q.ocnt = s.ocnt;
+                        Q.nown = (uint32_t)W;
                         ks.split(Q, stream);
                         ks.hash_probe(Q, s.np, stream);
                     } else {
                         ks.fused(Q, stream);
                     }
                 });
-                launch_route_count(s.fp, s.cnt, s.np, (uint32_t)MS, (uint32_t)W, s.ocnt, stream);
+                if (!split) launch_route_count(s.fp, s.cnt, s.np, (uint32_t)MS, (uint32_t)W, s.ocnt, stream);
             }
             // gathered row per shard: its successors per owner, its receive capacity, its failure
             const int K1 = W + 2;

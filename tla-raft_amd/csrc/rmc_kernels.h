@@ -114,6 +114,8 @@ struct KParams {
     // xside[i] = {parent global id lo, hi, slot key, record words} instead of par / pslot
     int route;
     uint4 *xside;
+    uint32_t *ocnt;            // sharded split round: k_hash_probe counts the successors per owner here
+    uint32_t nown;             // ... of that many owners (W)
     // split chunk (host-driven chunks of many parents): the expansion (M_SPLIT) stages the successors
     // and writes each parent's hash context (hctx, ctx_words per parent), and k_hash_probe gives every
     // successor a lane of its own for its fingerprint, the seen-set probe and the election (bit 0);

@@ -1191,6 +1191,10 @@ __device__ __forceinline__ void seen_insert(const Seen &S, ulonglong2 f) {
 __device__ __forceinline__ uint64_t l_index(const ulonglong2 f, uint64_t mask) {
     return (f.x ^ (f.x >> 31) ^ (f.y >> 7)) & mask;
 }
+// sharded run: owner(fp) = high bits of fp.y mod W -- independent of the seen-set and election index bits
+__device__ __forceinline__ uint32_t fp_owner(const ulonglong2 f, uint32_t W) {
+    return (uint32_t)((f.y >> 40) % W);
+}
 
 // ---- in-launch election (fused single-GPU level) -------------------------------------------
 // The first successor in TLC order (smallest slot q) per new fingerprint wins.  Election slot g
@@ -1710,10 +1714,12 @@ __global__ __launch_bounds__(256) void k_hash_probe(KParams P) {
     using Lo = Layout<N, V>;
     constexpr int CTXW = ctx_words<N, V>(), CC4 = (S::CCW + 3) / 4;
     __shared__ uint64_t sK[2][N * N];
+    __shared__ uint32_t sOwn[64];  // sharded round: the block's successors per owner (P.ocnt)
     if (threadIdx.x < 2 * N * N) {
         const int f = threadIdx.x / (N * N), a = (threadIdx.x / N) % N, b = threadIdx.x % N;
         sK[f][a * N + b] = P.t.seeds[f * SEEDS_PER_F + a * MAXN + b];
     }
+    if (threadIdx.x < 64) sOwn[threadIdx.x] = 0u;
     __syncthreads();
     each_successor<MX>(P, [&](uint64_t pl, uint32_t r) {
         const uint64_t q = pl * (uint64_t)MX + r;
@@ -1779,7 +1785,10 @@ __global__ __launch_bounds__(256) void k_hash_probe(KParams P) {
         }
         const ulonglong2 f = make_ulonglong2(best.x | 1ull, best.y);
         P.fp[q] = f;
-        if (P.route) return;
+        if (P.route) {  // the owners probe and elect; the round's counts per owner (k_route_count's)
+            if (P.ocnt) atomicAdd(&sOwn[fp_owner(f, P.nown)], 1u);
+            return;
+        }
         const uint32_t nm = (pc[Lo::W_MISC] >> 16) & 0xFFu;
         const uint32_t e = (nadd + (nm & 1u) + 1u) >> 1;  // record words a winner adds (elect_key)
         const uint64_t g = l_index(f, P.Lmask);
@@ -1787,6 +1796,10 @@ __global__ __launch_bounds__(256) void k_hash_probe(KParams P) {
         P.lslot[q] = seen_contains(P.seen, f) ? LS_SEEN
                                               : elect_slot<MX>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g, v0);
     });
+    if (P.route && P.ocnt) {
+        __syncthreads();
+        if (threadIdx.x < P.nown && sOwn[threadIdx.x]) atomicAdd(&P.ocnt[threadIdx.x], sOwn[threadIdx.x]);
+    }
 }
 
 // Split chunk, once the election is over: every winner's fingerprint into the seen set, a lane per
@@ -2462,10 +2475,6 @@ __global__ __launch_bounds__(64) void k_commit_finish(KParams P) {
 }
 
 // ---- sharded round: the owner's election (W > 1, and the one-rank rehearsal) -------------------
-// owner(fp) = high bits of fp.y mod W -- independent of the seen-set and election index bits
-__device__ __forceinline__ uint32_t fp_owner(const ulonglong2 f, uint32_t W) {
-    return (uint32_t)((f.y >> 40) % W);
-}
 
 // A fingerprint already in the seen set loses; otherwise it takes (or finds) its slot in the
 // round's election table and bids its key.  The table is cleared only every 65533 rounds
