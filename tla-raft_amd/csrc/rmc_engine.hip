@@ -432,6 +432,11 @@ struct Shard {
     unsigned long long *OK = nullptr;
     uint64_t ot_cap = 0;
     uint32_t ot_round = 0;  // rounds on the owner table since it was last cleared (its tag, k_owner_elect)
+    // split rounds: the fused election table (LXY / L, unused once the run is sharded) is the owner
+    // table, so k_hash_probe bids the shard's own successors as it fingerprints them; rounds on it
+    // since its last clear (0: not yet cleared for this use), and whether this round's own bids went in
+    uint32_t lx_round = 0;
+    bool lx_bid = false;
     uint32_t *ob = nullptr, *ib = nullptr;
     uint64_t ob_cap = 0, ib_cap = 0;
     uint4 *oside = nullptr, *iside = nullptr;
@@ -1247,6 +1252,18 @@ struct rmc_ctx {
     // also across rmc_reset, so a stale slot never reads as current and its key is never smaller.
     // rounds between clears of the owner table (RMC_OT_CLEAR_ROUNDS: tests take it down to a few)
     const uint32_t ot_clear_rounds = (uint32_t)env_int("RMC_OT_CLEAR_ROUNDS", 0xFFFD, 1, 0xFFFD);
+    // the round's tag on LXY / L as the owner table (cleared on first use and every ot_clear_rounds)
+    uint32_t lx_table(Shard &s) {
+        if (s.lx_round == 0 || s.lx_round >= ot_clear_rounds) {
+            HIPCHK(hipMemsetAsync(s.LXY, 0, s.lcap * 16, stream));
+            HIPCHK(hipMemsetAsync(s.L, 0xFF, s.lcap * 8, stream));
+            s.lx_round = 1;
+        } else {
+            ++s.lx_round;
+        }
+        return s.lx_round;
+    }
+
     uint64_t owner_table(Shard &o, uint64_t R) {
         const uint64_t need = next_pow2(std::max<uint64_t>(2 * R, 1024));
         bool clear = false;
@@ -2373,6 +2390,7 @@ struct rmc_ctx {
             agree(worst);
         };
         std::vector<uint64_t> hoff_buf;  // piece boundaries read back in one copy per round
+        std::vector<uint64_t> consumed_(NL, 0);  // per shard: ring words of the current level no longer needed
         for (uint64_t c = 0; c < rounds; c++) {
             // (1) expand the round's block: fingerprints, staged rows; successors per owner
             for (size_t li = 0; li < NL; li++) {
@@ -2384,11 +2402,21 @@ struct rmc_ctx {
                 HIPCHK(hipMemsetAsync(s.sum + 9, 0, 8, stream));
                 if (!s.np || fail[li]) continue;
                 const bool split = split_min && s.np >= split_min;
+                // (the fused election table holds a round's successors at load <= 1/2: ensure_chunk)
+                s.lx_bid = split && s.L && s.lcap >= 2 * s.np * MS;
                 timed(PH_HASH, [&] {
                     KParams Q = round_params(s, gbase);
                     if (split) {  // fingerprints a lane per successor (route: no probe), counted per owner
                         Q.ocnt = s.ocnt;
                         Q.nown = (uint32_t)W;
+                        if (s.lx_bid) {  // ... and the shard's own successors' bids
+                            Q.ot_round = lx_table(s);
+                            Q.OT = s.LXY;
+                            Q.OK = s.L;
+                            Q.ot_mask = s.lcap - 1;
+                            Q.self = (uint32_t)s.id;
+                            Q.gblk = s.gblk;
+                        }
                         ks.split(Q, stream);
                         ks.hash_probe(Q, s.np, stream);
                     } else {
@@ -2478,19 +2506,30 @@ struct rmc_ctx {
                 guard(li, [&] {
                     inject(3, o.id, c, L);
                     grow_seen(o, o.T_count + R + Rl);
-                    const uint64_t cap = owner_table(o, R + Rl);
+                    // the own successors' bids are in LXY / L already (k_hash_probe) if the received
+                    // ones fit beside them at load <= 1/2; otherwise every bid goes to the owner table
+                    const bool lx = o.lx_bid && 2 * (R + Rl) <= o.lcap;
+                    ulonglong2 *OT = o.LXY;
+                    unsigned long long *OK = o.L;
+                    uint64_t mask = o.lcap - 1;
+                    uint32_t rnd = o.lx_round;
+                    if (!lx) {
+                        mask = owner_table(o, R + Rl) - 1;
+                        OT = o.OT;
+                        OK = o.OK;
+                        rnd = o.ot_round;
+                    }
                     timed(PH_DEDUP, [&] {
                         const KParams Q = round_params(o, gbase);
-                        if (Rl)
-                            ks.local_elect(Q, o.np, o.seen(), o.OT, o.OK, cap - 1, o.ot_round, (uint32_t)W,
-                                           (uint32_t)o.id, o.gblk, stream);
+                        if (Rl && !lx)
+                            ks.local_elect(Q, o.np, o.seen(), OT, OK, mask, rnd, (uint32_t)W, (uint32_t)o.id, o.gblk,
+                                           stream);
                         if (R) {
-                            launch_owner_elect(o.xr, R, o.seen(), o.OT, o.OK, cap - 1, o.ot_round, o.rslot, stream);
-                            launch_owner_flags(o.xr, R, o.rslot, o.OK, o.ot_round, o.seen(), o.rflag, o.sum + 9,
-                                               stream);
+                            launch_owner_elect(o.xr, R, o.seen(), OT, OK, mask, rnd, o.rslot, stream);
+                            launch_owner_flags(o.xr, R, o.rslot, OK, rnd, o.seen(), o.rflag, o.sum + 9, stream);
                         }
                         if (Rl)
-                            ks.local_flags(Q, o.np, o.seen(), o.OK, o.ot_round, (uint32_t)W, (uint32_t)o.id, o.gblk,
+                            ks.local_flags(Q, o.np, o.seen(), OK, rnd, (uint32_t)W, (uint32_t)o.id, o.gblk,
                                            o.sum + 9, stream);
                     });
                 });
@@ -2607,7 +2646,24 @@ struct rmc_ctx {
                 for (size_t li = 0; li < NL; li++)
                     for (const Piece &pe : pcs[li])
                         HIPCHK(hipMemcpyAsync(h_red + k++, sh[li].ooff + pe.i0, 8, hipMemcpyDeviceToHost, stream));
+                // ... and, for a ring at its budget, where the current level's unexpanded records
+                // start (what the append below may reuse)
+                const size_t kc = k;
+                for (size_t li = 0; li < NL; li++) {
+                    const Shard &o = sh[li];
+                    const uint64_t done = std::min(o.cur_n, (c + 1) * B);
+                    if (o.ring_fixed && done < o.cur_n) {
+                        if (kc + NL > (size_t)RED_CAP) throw Fail(RMC_E_ARG, "too many winner pieces in a round");
+                        HIPCHK(hipMemcpyAsync(h_red + kc + li, o.cur_off + done, 8, hipMemcpyDeviceToHost, stream));
+                        nb++;
+                    }
+                }
                 if (nb) HIPCHK(hipStreamSynchronize(stream));
+                for (size_t li = 0; li < NL; li++) {
+                    const Shard &o = sh[li];
+                    const uint64_t done = std::min(o.cur_n, (c + 1) * B);
+                    consumed_[li] = !o.ring_fixed ? 0 : done < o.cur_n ? h_red[kc + li] : o.cur_words;
+                }
                 k = 0;
                 for (size_t li = 0; li < NL; li++) {
                     const uint64_t w = A[sh[li].id + 1] - A[sh[li].id];
@@ -2712,11 +2768,7 @@ struct rmc_ctx {
                 Shard &o = sh[li];
                 const uint64_t n = xs_[li].recv_total, words = xw_[li].recv_total;
                 if (!n) continue;
-                uint64_t consumed = 0;
-                if (o.ring_fixed) {
-                    const uint64_t done = std::min(o.cur_n, (c + 1) * B);
-                    consumed = done < o.cur_n ? d2h(o.cur_off + done) : o.cur_words;
-                }
+                const uint64_t consumed = consumed_[li];
                 guard(li, [&] {
                     inject(7, o.id, c, L);
                     ensure_ring(o, words, consumed);
@@ -2757,9 +2809,11 @@ struct rmc_ctx {
                 level_new += tab[TAB * t + 1];
                 level_words += tab[TAB * t + 2];
             }
-            HIPCHK(hipStreamSynchronize(stream));
-            collect_times(st);
+            // (no wait here: the next round's first read-back orders everything before it, and its
+            // phase times are collected after that)
         }
+        HIPCHK(hipStreamSynchronize(stream));
+        collect_times(st);
         total_generated += level_gen;
         total_distinct += level_new;
         st->generated = level_gen;
@@ -3228,6 +3282,7 @@ struct rmc_ctx {
             s.tflushed = s.trace_end = 0;
             s.hpar.n = s.hslot.n = 0;
             s.level_start.clear();
+            s.lx_round = 0;  // the fused levels of the next run use LXY / L again
         }
         // (the clears are stream-ordered before the next run's first kernel: no wait here)
         trace.clear();

@@ -116,6 +116,12 @@ struct KParams {
     uint4 *xside;
     uint32_t *ocnt;            // sharded split round: k_hash_probe counts the successors per owner here
     uint32_t nown;             // ... of that many owners (W)
+    // ... and, with OT set, the shard's own successors bid in its owner table (k_local_elect's work):
+    // lslot = LS_ELECT (another shard's), LS_SEEN, or the table slot; key (gblk + pl) << 10 | rank
+    ulonglong2 *OT;
+    unsigned long long *OK;
+    uint64_t ot_mask, gblk;
+    uint32_t ot_round, self;
     // split chunk (host-driven chunks of many parents): the expansion (M_SPLIT) stages the successors
     // and writes each parent's hash context (hctx, ctx_words per parent), and k_hash_probe gives every
     // successor a lane of its own for its fingerprint, the seen-set probe and the election (bit 0);

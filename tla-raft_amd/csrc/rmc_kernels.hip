@@ -1701,6 +1701,57 @@ __device__ __forceinline__ void each_successor(const KParams &P, F &&f) {
     }
 }
 
+// ---- sharded round: the owner's election table (k_hash_probe, k_local_elect, k_owner_elect) ----
+// A fingerprint already in the seen set loses; otherwise it takes (or finds) its slot in the
+// round's election table and bids its key.  The table is cleared only every 65533 rounds
+// (owner_table): `round` counts the rounds since, and both words of a slot carry its 16-bit tag
+// round + 1 in their low bits, so a slot of an earlier round reads as free, and a key word is the
+// round's key below ((0xFFFF - tag) << 48) -- smaller than any earlier round's -- so every bid just
+// takes the minimum (OT: fingerprint, OK: smallest tagged key; the same protocol as the fused
+// election).  key = (parent's global index in the level << 10) | rank: TLC's order of the level.
+__device__ __forceinline__ unsigned long long owner_key(uint32_t tag, uint64_t key) {
+    return ((unsigned long long)(0xFFFFu - tag) << 48) | key;  // key = global parent index << 10 | rank < 2^48
+}
+__device__ __forceinline__ uint32_t owner_bid(ulonglong2 *OT, unsigned long long *OK, uint64_t mask, uint32_t tag32,
+                                              const ulonglong2 f, uint64_t key) {
+    const unsigned long long tag = tag32;
+    const unsigned long long xk = (f.x & ~0xFFFFull) | tag, yk = (f.y & ~0xFFFFull) | tag;
+    // one exit at the bottom (no break): a claimer stores its y inside the loop, in the same
+    // iteration as its CAS, before any lane of its wave waits for that y (a divergent break
+    // lets the compiler defer the claimer's store until every lane has left the loop)
+    uint64_t g = l_index(f, mask);
+    unsigned long long v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool done = false;
+    while (!done) {
+        bool next = false;
+        if ((v & 0xFFFFull) != tag) {  // free, or an earlier round's: claim it
+            const unsigned long long prev = atomicCAS(&OT[g].x, v, xk);
+            if (prev == v) {
+                __hip_atomic_store(&OT[g].y, yk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                done = true;
+            } else {
+                v = prev;
+            }
+        }
+        if (!done && (v & 0xFFFFull) == tag) {
+            if (v == xk) {
+                const unsigned long long y = __hip_atomic_load(&OT[g].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (y == yk) done = true;
+                else if ((y & 0xFFFFull) == tag) next = true;
+                else v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // y not visible yet
+            } else {
+                next = true;
+            }
+        }
+        if (next) {
+            g = (g + 1) & mask;
+            v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    atomicMin(&OK[g], owner_key(tag32, key));
+    return (uint32_t)g;
+}
+
 // Split chunk: every successor's fingerprint, seen-set probe and election, a lane per successor.
 // The expansion (M_SPLIT) left each parent's hash context (its packed core and its message-hash
 // sums per server pair, ctx_words) and each successor's staged row; the successor's content
@@ -1786,7 +1837,15 @@ __global__ __launch_bounds__(256) void k_hash_probe(KParams P) {
         const ulonglong2 f = make_ulonglong2(best.x | 1ull, best.y);
         P.fp[q] = f;
         if (P.route) {  // the owners probe and elect; the round's counts per owner (k_route_count's)
-            if (P.ocnt) atomicAdd(&sOwn[fp_owner(f, P.nown)], 1u);
+            const uint32_t o = fp_owner(f, P.nown);
+            if (P.ocnt) atomicAdd(&sOwn[o], 1u);
+            // the shard's own successors bid in its owner table right here (k_local_elect's work;
+            // the others are marked for the exchange)
+            if (P.OT)
+                P.lslot[q] = o != P.self ? LS_ELECT
+                             : seen_contains(P.seen, f)
+                                 ? LS_SEEN
+                                 : owner_bid(P.OT, P.OK, P.ot_mask, P.ot_round + 1u, f, ((P.gblk + pl) << 10) | r);
             return;
         }
         const uint32_t nm = (pc[Lo::W_MISC] >> 16) & 0xFFu;
@@ -2475,56 +2534,6 @@ __global__ __launch_bounds__(64) void k_commit_finish(KParams P) {
 }
 
 // ---- sharded round: the owner's election (W > 1, and the one-rank rehearsal) -------------------
-
-// A fingerprint already in the seen set loses; otherwise it takes (or finds) its slot in the
-// round's election table and bids its key.  The table is cleared only every 65533 rounds
-// (owner_table): `round` counts the rounds since, and both words of a slot carry its 16-bit tag
-// round + 1 in their low bits, so a slot of an earlier round reads as free, and a key word is the
-// round's key below ((0xFFFF - tag) << 48) -- smaller than any earlier round's -- so every bid just
-// takes the minimum (OT: fingerprint, OK: smallest tagged key; the same protocol as the fused
-// election).  key = (parent's global index in the level << 10) | rank: TLC's order of the level.
-__device__ __forceinline__ unsigned long long owner_key(uint32_t tag, uint64_t key) {
-    return ((unsigned long long)(0xFFFFu - tag) << 48) | key;  // key = global parent index << 10 | rank < 2^48
-}
-__device__ __forceinline__ uint32_t owner_bid(ulonglong2 *OT, unsigned long long *OK, uint64_t mask, uint32_t tag32,
-                                              const ulonglong2 f, uint64_t key) {
-    const unsigned long long tag = tag32;
-    const unsigned long long xk = (f.x & ~0xFFFFull) | tag, yk = (f.y & ~0xFFFFull) | tag;
-    // one exit at the bottom (no break): a claimer stores its y inside the loop, in the same
-    // iteration as its CAS, before any lane of its wave waits for that y (a divergent break
-    // lets the compiler defer the claimer's store until every lane has left the loop)
-    uint64_t g = l_index(f, mask);
-    unsigned long long v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    bool done = false;
-    while (!done) {
-        bool next = false;
-        if ((v & 0xFFFFull) != tag) {  // free, or an earlier round's: claim it
-            const unsigned long long prev = atomicCAS(&OT[g].x, v, xk);
-            if (prev == v) {
-                __hip_atomic_store(&OT[g].y, yk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                done = true;
-            } else {
-                v = prev;
-            }
-        }
-        if (!done && (v & 0xFFFFull) == tag) {
-            if (v == xk) {
-                const unsigned long long y = __hip_atomic_load(&OT[g].y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (y == yk) done = true;
-                else if ((y & 0xFFFFull) == tag) next = true;
-                else v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // y not visible yet
-            } else {
-                next = true;
-            }
-        }
-        if (next) {
-            g = (g + 1) & mask;
-            v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    atomicMin(&OK[g], owner_key(tag32, key));
-    return (uint32_t)g;
-}
 
 // Owner's own successors (fingerprint owner == self), a lane each: they bid in the round's table
 // straight from the expansion's slots -- no item through the exchange -- and the slot (or LS_SEEN)
