@@ -501,11 +501,12 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_scale:
         mc.close()  # the at-scale run gets the whole device (this checker's chunk buffers are ~12 GB)
-        line["at_scale"] = at_scale(local, probes_per_s=pk_hbm)
+        line["at_scale"] = dict(path="single-gpu", n_gpus=1, **at_scale(local, probes_per_s=pk_hbm))
         if not args.no_cpu_baseline:
             line["cpu_baseline_at_scale"] = cpu_baseline_at_scale(local)
     if rank == 0 and sharded is not None:
-        line["at_scale_sharded"] = sharded
+        # N > 1: the same workload (Raft.cfg exhausted) under the same key, over all N GPUs
+        line["at_scale"] = dict(path=f"sharded over {world} GPUs (RCCL)", **sharded)
     if rank == 0 and sharded_c4 is not None:
         line["at_scale_sharded_configs3"] = sharded_c4
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -36,7 +36,9 @@ from bench import HBM_PEAK_GBS, VALU_PEAK, alg_bytes, ctx_bytes  # noqa: E402
 LEVEL = re.compile(r"^L\s*(\d+) F=\s*(\d+) G=\s*(\d+) N=\s*(\d+) tot=\s*\d+\s+[\d.]+ms \[([^\]]*)\].*rec=([\d.]+)B")
 # name -> (kernel name fragment, explore phase column of its HIP-event time, alg_bytes phase)
 KERNELS = {"expand": ("k_expand", 1, "expand_hash"), "probe": ("k_hash_probe", 5, "probe"),
-           "insert": ("k_insert_winners", 5, "insert"), "commit": ("k_commit", 3, "materialize")}
+           "insert": ("k_insert_winners", 5, "insert"),
+           # split chunks commit with k_commit_split (+ its one-wave k_commit_finish, not counted)
+           "commit": ("k_commit_split", 3, "materialize")}
 
 
 def levels_of(log):
@@ -90,7 +92,7 @@ def main():
         per = []
         for L in lv_f:
             nch = max(1, -(-L["F"] // chunk))
-            if key in ("probe", "insert"):
+            if key in ("probe", "insert", "commit"):
                 nch = sum(1 for c in range(nch) if min(chunk, L["F"] - c * chunk) >= a.split_min)
             per.append(nch)
         if not (len(fetch) == len(write) == len(sq) == sum(per)):
