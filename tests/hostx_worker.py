@@ -28,7 +28,10 @@ def main():
         os.environ["RMC_FAULT_INJECT"] = spec["inject"]
     out = {"rank": r}
     try:
-        mc = raftmc.ModelChecker(raftmc.ModelConfig(rank=r, world_size=W, device=0, **spec["cfg"]))
+        cfg = dict(spec["cfg"])
+        if os.environ.get("RMC_TEST_DEVICE_LEVELS"):  # (debugging: levels per host round trip)
+            cfg["device_levels"] = int(os.environ["RMC_TEST_DEVICE_LEVELS"])
+        mc = raftmc.ModelChecker(raftmc.ModelConfig(rank=r, world_size=W, device=0, **cfg))
         os.environ.pop("RMC_FAULT_INJECT", None)
         try:
             res = mc.run()

@@ -281,14 +281,20 @@ def test_split_probe_chunks_match_golden_levels(name, monkeypatch):
     mc.close()
 
 
-@pytest.mark.parametrize("mode", ["virtual2", "rccl1"])
+@pytest.mark.parametrize("mode", ["virtual2", "rccl1", "virtual3_rebid"])
 @pytest.mark.parametrize("name", sorted(LEVELS))
 def test_sharded_commit_list_matches_golden_levels(name, mode, monkeypatch):
-    """Sharded rounds whose commit visits only the parents with winners (k_nzlist; RMC_SPLIT_MIN=1
-    turns it on for every round): levels, counters at an error and traces as the golden run."""
+    """Split sharded rounds (RMC_SPLIT_MIN=1 makes every round one): the fingerprint pass bids each
+    shard's own successors in its election table, the commit visits only the parents with winners
+    (k_nzlist) -- levels, counters at an error and traces as the golden run.  virtual3_rebid: the
+    bids are always redone in the owner table (RMC_OWNER_LXY=2, the fallback for received items
+    that do not fit beside them)."""
     monkeypatch.setenv("RMC_SPLIT_MIN", "1")
     g = LEVELS[name]
-    if mode == "virtual2":
+    if mode == "virtual3_rebid":
+        monkeypatch.setenv("RMC_OWNER_LXY", "2")
+        kw = dict(virtual_shards=3, chunk_successors=3000, shard_min_states=1)
+    elif mode == "virtual2":
         kw = dict(virtual_shards=2, chunk_successors=3000, shard_min_states=1)
     else:
         kw = dict(world_size=1, rank=0, comm_unique_id=raftmc.comm_unique_id(), chunk_successors=3000,

@@ -43,8 +43,11 @@ def run_ranks(tmp_path, W, cfg, inject=None, inject_rank=None, trace=False, time
         out = str(tmp_path / f"rank{r}.json")
         spec = dict(rank=r, world=W, port=port, cfg=cfg, out=out, trace=trace,
                     inject=inject if (inject_rank is None or inject_rank == r) else None)
+        # RMC_COLL_CHECK: the ranks compare every collective's sequence number, call site and size
+        # first, so a rank off the common path fails with both sites named instead of hanging
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "hostx_worker.py"), json.dumps(spec)],
-                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                                      env=dict(os.environ, RMC_COLL_CHECK="1")))
         outs.append(out)
     logs = []
     try:
@@ -56,7 +59,10 @@ def run_ranks(tmp_path, W, cfg, inject=None, inject_rank=None, trace=False, time
         raise AssertionError("a rank did not finish (left in a collective?)")
     for p, log in zip(procs, logs):
         assert p.returncode == 0, log[-3000:]
-    return [json.load(open(o)) for o in outs]
+    rs = [json.load(open(o)) for o in outs]
+    for r, log in zip(rs, logs):
+        r["_log"] = log[-2000:]
+    return rs
 
 
 def golden_cfg(g, **kw):
@@ -87,6 +93,15 @@ def test_ranks_identical_to_single(name, W, shard_min, tmp_path):
     g = LEVELS[name]
     rs = run_ranks(tmp_path, W, golden_cfg(g, chunk_successors=3000, shard_min_states=shard_min),
                    trace=name in TRACES)
+    errs = [r.get("error") for r in rs]
+    assert not any(errs), "\n".join(f"rank {i}: {e}\n{r['_log']}" for i, (e, r) in enumerate(zip(errs, rs)))
+    got = [[lv[3] for lv in r["levels"] if lv[3]] for r in rs]
+    if g["verdict"] == "ok":  # the first level that differs, on every rank (before the totals)
+        for i, lv in enumerate(got):
+            bad = next((k for k, (a, b) in enumerate(zip(lv, g["levels"])) if a != b), None)
+            assert bad is None and len(lv) == len(g["levels"]), \
+                f"rank {i}: level {bad}: {lv[bad - 1:bad + 2] if bad else lv[-3:]} vs golden " \
+                f"{g['levels'][bad - 1:bad + 2] if bad else g['levels'][-3:]}; all ranks: {got}"
     for r in rs:
         check(g, r)
         assert r["levels"] == rs[0]["levels"]

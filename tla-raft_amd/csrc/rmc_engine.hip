@@ -1033,6 +1033,8 @@ struct rmc_ctx {
         dfree(d_flags1); dfree(d_red);
         if (h_red) (void)hipHostFree(h_red);
         h_red = nullptr;
+        hx_send.release();
+        hx_recv.release();
         for (hipEvent_t e : evpool) (void)hipEventDestroy(e);
         evpool.clear();
         for (hipEvent_t e : gev) (void)hipEventDestroy(e);
@@ -1252,6 +1254,10 @@ struct rmc_ctx {
     // also across rmc_reset, so a stale slot never reads as current and its key is never smaller.
     // rounds between clears of the owner table (RMC_OT_CLEAR_ROUNDS: tests take it down to a few)
     const uint32_t ot_clear_rounds = (uint32_t)env_int("RMC_OT_CLEAR_ROUNDS", 0xFFFD, 1, 0xFFFD);
+    // split sharded rounds: 1 = the own successors bid in LXY / L inside k_hash_probe (when the table
+    // fits them), 0 = never (k_local_elect into the owner table), 2 = bid there but always redo the
+    // bids in the owner table (a test of that fallback)
+    const int owner_lxy = env_int("RMC_OWNER_LXY", 1, 0, 2);
     // the round's tag on LXY / L as the owner table (cleared on first use and every ot_clear_rounds)
     uint32_t lx_table(Shard &s) {
         if (s.lx_round == 0 || s.lx_round >= ot_clear_rounds) {
@@ -1337,8 +1343,27 @@ struct rmc_ctx {
     // ---- collectives over shards --------------------------------------------------------
     // Every host value handed to these is this process's contribution (virtual mode: the
     // sum/max over all local shards already IS the global value).
-    void allreduce(uint64_t *v, int n, bool is_max) {
+    // RMC_COLL_CHECK=1 (host-staged transport): before every collective the ranks compare its
+    // sequence number, call site and size (one extra all-gather each) and stop with the first
+    // difference -- a rank taking another path through the protocol shows up there, not as a hang
+    const bool coll_check = env_int("RMC_COLL_CHECK", 0, 0, 1) != 0;
+    uint64_t coll_seq = 0;
+    void coll_guard(int line, uint64_t n) {
+        if (!hostx || !coll_check) return;
+        uint64_t row[3] = {coll_seq++, (uint64_t)line, n};
+        std::vector<uint64_t> all((size_t)W * 3);
+        if (tx.allgather_u64(tx.user, row, 3, all.data()) != 0) throw Fail(RMC_E_COMM, "transport allgather failed");
+        for (int r = 0; r < W; r++)
+            if (all[3 * r] != row[0] || all[3 * r + 1] != row[1] || all[3 * r + 2] != row[2])
+                throw Fail(RMC_E_COMM, "collective mismatch: rank " + std::to_string(rank) + " #" +
+                                           std::to_string(row[0]) + " at line " + std::to_string(row[1]) + " n " +
+                                           std::to_string(row[2]) + ", rank " + std::to_string(r) + " #" +
+                                           std::to_string(all[3 * r]) + " at line " + std::to_string(all[3 * r + 1]) +
+                                           " n " + std::to_string(all[3 * r + 2]));
+    }
+    void allreduce(uint64_t *v, int n, bool is_max, int line = __builtin_LINE()) {
         if (hostx) {
+            coll_guard(line, (uint64_t)n);
             if (tx.allreduce_u64(tx.user, v, n, is_max ? 1 : 0) != 0) throw Fail(RMC_E_COMM, "transport allreduce failed");
             return;
         }
@@ -1356,9 +1381,10 @@ struct rmc_ctx {
 
     // Every shard's row of K values on every rank: rows[li] = sh[li]'s row in, the W x K matrix
     // (row t = shard t) out.  One ncclAllGather through RCCL; virtual shards are all local.
-    std::vector<uint64_t> gather_rows(const std::vector<std::vector<uint64_t>> &rows, int K) {
+    std::vector<uint64_t> gather_rows(const std::vector<std::vector<uint64_t>> &rows, int K, int line = __builtin_LINE()) {
         std::vector<uint64_t> M((size_t)W * K, 0);
         if (hostx) {
+            coll_guard(line, (uint64_t)K);
             if (tx.allgather_u64(tx.user, rows[0].data(), K, M.data()) != 0) throw Fail(RMC_E_COMM, "transport allgather failed");
             return M;
         }
@@ -1397,9 +1423,32 @@ struct rmc_ctx {
     // The host-staged transport: a rank's part for itself is a device copy (or nothing), every peer's
     // part of every payload goes to host memory in one packed buffer, the transport's
     // all-to-all-v moves the bytes, and the received parts go back to the device.
-    std::vector<char> hx_send, hx_recv;
-    void exchange_host(const std::vector<Payload> &P) {
+    // pinned staging for the host-staged exchange (an asynchronous copy to or from pageable memory
+    // is staged by the runtime itself; pinned buffers keep every leg inside the stream)
+    struct PinnedBuf {
+        char *p = nullptr;
+        size_t cap = 0;
+        char *get(size_t n) {
+            if (n > cap) {
+                if (p) (void)hipHostFree(p);
+                p = nullptr;
+                cap = 0;
+                const size_t nc = std::max<size_t>(n + n / 2, 1 << 16);
+                HIPCHK(hipHostMalloc((void **)&p, nc, hipHostMallocDefault));
+                cap = nc;
+            }
+            return p;
+        }
+        void release() {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+        }
+    };
+    PinnedBuf hx_send, hx_recv;
+    void exchange_host(const std::vector<Payload> &P, int line) {
         for (const Payload &p : P) {
+            coll_guard(line, p.elem);
             const XPlan &x = (*p.plans)[0];
             const uint64_t own = x.send_cnt[rank];
             if (own && !p.self_in_place)
@@ -1413,27 +1462,26 @@ struct rmc_ctx {
                 so[q] = ts; sb[q] = x.send_cnt[q] * p.elem; ts += sb[q];
                 ro[q] = tr; rb[q] = x.recv_cnt[q] * p.elem; tr += rb[q];
             }
-            hx_send.resize(std::max<size_t>(ts, 1));
-            hx_recv.resize(std::max<size_t>(tr, 1));
+            char *hs = hx_send.get(std::max<size_t>(ts, 1)), *hr = hx_recv.get(std::max<size_t>(tr, 1));
             for (int q = 0; q < W; q++)
                 if (sb[q])
-                    HIPCHK(hipMemcpyAsync(hx_send.data() + so[q], (const char *)p.send[0] + x.send_off[q] * p.elem, sb[q],
+                    HIPCHK(hipMemcpyAsync(hs + so[q], (const char *)p.send[0] + x.send_off[q] * p.elem, sb[q],
                                           hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
-            if (tx.alltoallv(tx.user, hx_send.data(), so.data(), sb.data(), hx_recv.data(), ro.data(), rb.data()) != 0)
+            if (tx.alltoallv(tx.user, hs, so.data(), sb.data(), hr, ro.data(), rb.data()) != 0)
                 throw Fail(RMC_E_COMM, "transport alltoallv failed");
             for (int q = 0; q < W; q++)
                 if (rb[q])
-                    HIPCHK(hipMemcpyAsync((char *)p.recv[0] + x.recv_off[q] * p.elem, hx_recv.data() + ro[q], rb[q],
+                    HIPCHK(hipMemcpyAsync((char *)p.recv[0] + x.recv_off[q] * p.elem, hr + ro[q], rb[q],
                                           hipMemcpyHostToDevice, stream));
             HIPCHK(hipStreamSynchronize(stream));
         }
     }
 
     // A shard's part for itself never goes through RCCL: a device copy (or nothing, self_in_place).
-    void exchange(const std::vector<Payload> &P) {
+    void exchange(const std::vector<Payload> &P, int line = __builtin_LINE()) {
         if (hostx) {
-            exchange_host(P);
+            exchange_host(P, line);
             return;
         }
         if (!rccl) {
@@ -2403,7 +2451,7 @@ struct rmc_ctx {
                 if (!s.np || fail[li]) continue;
                 const bool split = split_min && s.np >= split_min;
                 // (the fused election table holds a round's successors at load <= 1/2: ensure_chunk)
-                s.lx_bid = split && s.L && s.lcap >= 2 * s.np * MS;
+                s.lx_bid = owner_lxy && split && s.L && s.lcap >= 2 * s.np * MS;
                 timed(PH_HASH, [&] {
                     KParams Q = round_params(s, gbase);
                     if (split) {  // fingerprints a lane per successor (route: no probe), counted per owner
@@ -2508,7 +2556,7 @@ struct rmc_ctx {
                     grow_seen(o, o.T_count + R + Rl);
                     // the own successors' bids are in LXY / L already (k_hash_probe) if the received
                     // ones fit beside them at load <= 1/2; otherwise every bid goes to the owner table
-                    const bool lx = o.lx_bid && 2 * (R + Rl) <= o.lcap;
+                    const bool lx = o.lx_bid && 2 * (R + Rl) <= o.lcap && owner_lxy != 2;
                     ulonglong2 *OT = o.LXY;
                     unsigned long long *OK = o.L;
                     uint64_t mask = o.lcap - 1;
