@@ -2115,7 +2115,7 @@ struct rmc_ctx {
                 if ((spin & 255u) == 255u && std::chrono::steady_clock::now() >= tq) {
                     tq = std::chrono::steady_clock::now() + std::chrono::microseconds(dl_query_us);
                     const hipError_t q = hipStreamQuery(stream);
-                    if (q == hipSuccess) {  // drained: the mirror is final
+                    if (q == hipSuccess) {  // drained (the mirror may still lag: the caller reads the device's block)
                         if (__atomic_load_n(&s.hloop->stop, __ATOMIC_ACQUIRE) != (uint32_t)CTL_RUN) return false;
                         return __atomic_load_n(&s.hloop->done, __ATOMIC_ACQUIRE) >= need;
                     }
@@ -2132,15 +2132,26 @@ struct rmc_ctx {
         for (int i = enq * GL; i < K; i++) mark[i] = evrecs.size();
         HIPCHK(hipStreamSynchronize(stream));
         HIPCHK(hipGetLastError());
-        *s.hctl = s.hloop->ctl;
-        const LevelCtl c = *s.hctl;
+        // The control block and the level records as the device holds them.  The pinned mirror is
+        // for the progress polls only: its last system-scope writes can still be in flight when the
+        // stream reports drained, and a poll that read a lagging `done` stops enqueueing while the
+        // loop still runs -- the mirror's control block is then an earlier batch's (two rank
+        // processes on one MI355X: a spurious error or a count off by one about one run in ten).
+        // (both in one wait: the records of every level the batch may have run; pinned targets)
+        HIPCHK(hipMemcpyAsync(s.hctl, s.ctl, sizeof(LevelCtl), hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(s.hlrec, s.lrec, sizeof(LevelRec) * K, hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+        LevelCtl c = *s.hctl;
         const int D = (int)c.done_levels;
-        if (D > 0 && D <= K) std::memcpy(s.hlrec, s.hloop->rec, sizeof(LevelRec) * D);
+        if (D > K) throw Fail(RMC_E_STATE, "device level loop ran past its batch");
+        if (c.stop == CTL_RUN) {  // enqueueing stopped first: the levels done stand, the next batch goes on
+            c.stop = CTL_HOST;
+            *s.hctl = c;
+        }
         if (c.stop == CTL_ERROR) {  // the erroring level's summary (error keys, winners) for the host path
             HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
         }
-        if (D > K || c.stop == CTL_RUN) throw Fail(RMC_E_STATE, "device level loop did not stop");
         const int nst = D + (c.stop == CTL_ERROR ? 1 : 0);
         for (int i = 0; i < nst; i++) std::memset(&out[i], 0, sizeof out[i]);
         // phase times of the levels that ran (later levels' kernels returned at once)
