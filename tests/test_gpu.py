@@ -383,7 +383,7 @@ def test_results_independent_of_chunking_and_seen_growth():
         mc.close()
 
 
-@pytest.mark.parametrize("device_levels", [1, 2, 3])
+@pytest.mark.parametrize("device_levels", [1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("name", sorted(LEVELS))
 def test_device_level_loop_matches_golden(name, device_levels):
     """Host-driven levels (1) and device-driven batches of 2 / 3 levels (odd and even
