@@ -968,9 +968,9 @@ struct rmc_ctx {
         s.plist = dmalloc<uint32_t>(chunk_parents + 1);
         s.tickets = dmalloc<uint32_t>(4);
         HIPCHK(hipMemsetAsync(s.tickets, 0, 16, stream));
-        s.ctl = dmalloc<LevelCtl>(1);
+        s.ctl = dmalloc<LevelCtl>(2);  // level i reads ctl[i & 1], its commit writes the other
         s.lrec = dmalloc<LevelRec>(LREC_CAP);
-        HIPCHK(hipHostMalloc((void **)&s.hctl, sizeof(LevelCtl), hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void **)&s.hctl, 2 * sizeof(LevelCtl), hipHostMallocDefault));
         HIPCHK(hipHostMalloc((void **)&s.hloop, sizeof(HostLoop), hipHostMallocMapped | hipHostMallocCoherent));
         HIPCHK(hipHostGetDevicePointer((void **)&s.dloop, s.hloop, 0));
         HIPCHK(hipHostMalloc((void **)&s.hlrec, sizeof(LevelRec) * LREC_CAP, hipHostMallocDefault));
@@ -2073,6 +2073,7 @@ struct rmc_ctx {
         __atomic_store_n(&s.hloop->done, 0u, __ATOMIC_RELAXED);
         __atomic_store_n(&s.hloop->stop, (uint32_t)CTL_RUN, __ATOMIC_RELEASE);
         launch_set_ctl(s.ctl, h, stream);
+        launch_set_ctl(s.ctl + 1, h, stream);
         uint64_t *offs[2] = {s.cur_off, s.nxt_off};
         std::vector<size_t> mark(K);
         // Levels go in groups of GL.  The loop's progress is mirrored into pinned host memory
@@ -2092,7 +2093,8 @@ struct rmc_ctx {
                 KParams Q = chunk_params(s);
                 Q.foff = offs[i & 1];
                 Q.noff = offs[(i + 1) & 1];
-                Q.ctl = s.ctl;
+                Q.ctl = s.ctl + (i & 1);
+                Q.ctl_next = s.ctl + ((i + 1) & 1);
                 Q.lrec = s.lrec;
                 Q.hloop = s.dloop;
                 Q.p_begin = 0;
@@ -2138,10 +2140,12 @@ struct rmc_ctx {
         // loop still runs -- the mirror's control block is then an earlier batch's (two rank
         // processes on one MI355X: a spurious error or a count off by one about one run in ten).
         // (both in one wait: the records of every level the batch may have run; pinned targets)
-        HIPCHK(hipMemcpyAsync(s.hctl, s.ctl, sizeof(LevelCtl), hipMemcpyDeviceToHost, stream));
+        HIPCHK(hipMemcpyAsync(s.hctl, s.ctl, 2 * sizeof(LevelCtl), hipMemcpyDeviceToHost, stream));
         HIPCHK(hipMemcpyAsync(s.hlrec, s.lrec, sizeof(LevelRec) * K, hipMemcpyDeviceToHost, stream));
         HIPCHK(hipStreamSynchronize(stream));
-        LevelCtl c = *s.hctl;
+        // the pair's newer block: more levels done, or (an error stops without advancing) the stopped one
+        const LevelCtl &c0 = s.hctl[0], &c1 = s.hctl[1];
+        LevelCtl c = (c1.done_levels > c0.done_levels || (c1.done_levels == c0.done_levels && c1.stop != CTL_RUN)) ? c1 : c0;
         const int D = (int)c.done_levels;
         if (D > K) throw Fail(RMC_E_STATE, "device level loop ran past its batch");
         if (c.stop == CTL_RUN) {  // enqueueing stopped first: the levels done stand, the next batch goes on

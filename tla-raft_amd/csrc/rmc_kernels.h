@@ -160,6 +160,7 @@ struct KParams {
     uint32_t *ctick;           // commit pass: arrival counters (last_commit_block; 0 between launches)
     unsigned long long *sum;   // chunk summary {generated, winners, error keys[ERR_NSLOTS], flags, words}
     LevelCtl *ctl;             // device-driven level loop (nullptr: the host drives the chunk)
+    LevelCtl *ctl_next;        // device loop: the block the next level reads (finish_level writes it)
     LevelRec *lrec;            // statistics of each level the device loop commits
     HostLoop *hloop;           // device loop: host-mapped mirror of the loop's progress (k_expand, finish_level)
     uint32_t done_levels;      // device loop: levels of the batch committed before this one (level_args)

@@ -2106,7 +2106,9 @@ __device__ void finish_level(const KParams &P) {
     if (lane != 0) return;
     if (!P.ctl) return;
     if (bad) {  // the host reports the error from this level's buffers
-        P.ctl->stop = CTL_ERROR;
+        c.stop = CTL_ERROR;  // the erroring level's block, not advanced, into both (see below)
+        *P.ctl_next = c;
+        *P.ctl = c;
         if (P.hloop) {
             c.stop = CTL_ERROR;
             P.hloop->ctl = c;
@@ -2141,7 +2143,11 @@ __device__ void finish_level(const KParams &P) {
              Gub > c.off_cap || Ww + Gub * RECW_MAX > c.rcap || c.gid_cur + Wn + Gub - c.trace_base > c.trace_cap ||
              2 * (c.T_count + Gub) > c.T_cap)
         c.stop = CTL_HOST;  // the next level is not known to fit the buffers: the host grows them
-    *P.ctl = c;
+    // into the other block of the pair: a late block of this launch (one with no parent, which
+    // leaves without arriving) still reads this level's block, never the next level's
+    // A stopped loop's block goes into both: the no-op launches after it read either.
+    *P.ctl_next = c;
+    if (c.stop != CTL_RUN) *P.ctl = c;
     // The loop's stop goes to the host here, with the control block (read after the drain); the
     // running loop's progress is reported by the next level's expansion as it starts (k_expand):
     // a write to host memory at the end of this kernel would hold the next launch ~5.6 us.
