@@ -307,6 +307,34 @@ def test_sharded_commit_list_matches_golden_levels(name, mode, monkeypatch):
     mc.close()
 
 
+@pytest.mark.parametrize("mode", ["virtual2", "rccl1"])
+@pytest.mark.parametrize("name", ["n3_v1_e2_r3", "seeded_n3_v2_e2_r3", "n4_v1_e1_r3"])
+def test_sharded_run_then_reset_reruns_golden(name, mode, monkeypatch):
+    """A sharded run whose split rounds used the fused election table (LXY / L) as their owner table,
+    then rmc_reset, then a second run whose first levels are replicated (the fused election again):
+    both runs give the golden levels, counters and traces (the owner keys a sharded round leaves in L
+    are smaller than any fused election word; reset must clear them)."""
+    if name not in LEVELS:
+        pytest.skip("no such golden configuration")
+    monkeypatch.setenv("RMC_SPLIT_MIN", "1")
+    g = LEVELS[name]
+    if mode == "virtual2":
+        kw = dict(virtual_shards=2, chunk_successors=3000, shard_min_states=40)
+    else:
+        kw = dict(world_size=1, rank=0, comm_unique_id=raftmc.comm_unique_id(), chunk_successors=3000,
+                  shard_min_states=40)
+    mc, res = run_cfg(g, **kw)
+    check_levels(g, res)
+    for _ in range(2):
+        mc.reset()
+        res = mc.run()
+        check_levels(g, res)
+        if name in TRACES:
+            assert [(list(k) if k else None, st) for k, st in mc.trace()] == \
+                   [(e["key"], e["state"]) for e in TRACES[name]["steps"]]
+    mc.close()
+
+
 @pytest.mark.parametrize("name", sorted(LEVELS_BIG))
 def test_bfs_matches_golden_levels_at_scale(name):
     """bench.py's at-scale workload (10^7 states) against the C oracle's full BFS, level by level."""

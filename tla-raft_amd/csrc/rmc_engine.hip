@@ -492,6 +492,7 @@ struct rmc_ctx {
 
     std::vector<Shard> sh;
     uint64_t chunk_parents = 0, Gcap = 0, Lcap_max = 0;
+    uint64_t want_chunk_parents_adopt = 0;  // resume: a checkpoint's smaller chunk size, taken over
     // W > 1: levels below shard_min states are expanded whole on every shard with the fused
     // single-GPU level (replicated: no exchange); the run shards from the first level that reaches it
     uint64_t shard_min = 0;
@@ -828,6 +829,9 @@ struct rmc_ctx {
 #endif
         }
 
+        d_red = dmalloc<unsigned long long>(2 * RED_CAP);  // collective scratch (the chunk-size agreement below)
+        HIPCHK(hipHostMalloc((void **)&h_red, RED_CAP * 8, hipHostMallocDefault));
+
         U.build(N, V, cfg.max_election);
         d_info = dmalloc<uint32_t>(U.info.size());
         d_nat2id = dmalloc<uint16_t>(U.nat2id.size());
@@ -880,7 +884,18 @@ struct rmc_ctx {
             // beside the budgets: the live levels' record offsets (8 B a state; the two widest levels
             // of configs[3] hold about a third of its seen set's states) and some slack
             const uint64_t budgets = cfg.seen_mem_bytes + cfg.frontier_mem_bytes + cfg.seen_mem_bytes / 2 + (4ull << 30);
-            while (Gcap > (1ull << 24) && budgets + Gcap * per_slot > (uint64_t)fr) Gcap >>= 1;
+            uint64_t halvings = 0;
+            while (Gcap > (1ull << 24) && budgets + Gcap * per_slot > (uint64_t)fr) {
+                Gcap >>= 1;
+                ++halvings;
+            }
+            // B = chunk_parents sets the block-cyclic level layout every rank must share (step_sharded,
+            // route_pieces), and free memory differs between ranks (another process on the device,
+            // rank 0's extra allocations): every rank takes the most-halved chunk
+            if (rccl || hostx) {
+                allreduce(&halvings, 1, true);
+                Gcap = (cfg.chunk_successors ? cfg.chunk_successors : (1ull << 28)) >> halvings;
+            }
         }
         Gcap = std::max<uint64_t>(Gcap, (uint64_t)ks.maxsucc * 64);
         if (Gcap >= (1ull << 30)) throw Fail(RMC_E_ARG, "chunk_successors must be < 2^30");
@@ -900,8 +915,6 @@ struct rmc_ctx {
         d_inv = dmalloc<int32_t>(7);
         d_err1 = dmalloc<unsigned long long>(ERR_NSLOTS);
         d_flags1 = dmalloc<uint32_t>(4);
-        d_red = dmalloc<unsigned long long>(2 * RED_CAP);
-        HIPCHK(hipHostMalloc((void **)&h_red, RED_CAP * 8, hipHostMallocDefault));
         HIPCHK(hipStreamSynchronize(stream));
     }
 
@@ -2387,11 +2400,6 @@ struct rmc_ctx {
     // per-shard round row: generated, winners, words, inserted, error kind + 1, error key, -failure code
     static constexpr int TAB = 7;
 
-#ifdef RMC_SHARD_DEBUG
-#define SDBG(x) do { HIPCHK(hipStreamSynchronize(stream)); std::fprintf(stderr, "sharded L%d c%llu phase %s\n", L, (unsigned long long)c, x); } while (0)
-#else
-#define SDBG(x) do {} while (0)
-#endif
     int step_sharded(rmc_level_stats *st) {
         auto t0 = std::chrono::steady_clock::now();
         const int L = (int)sh[0].level_start.size();
@@ -2463,6 +2471,9 @@ struct rmc_ctx {
                 s.gblk = (c * (uint64_t)W + (uint64_t)s.id) * B;
                 HIPCHK(hipMemsetAsync(s.ocnt, 0, 64 * 4, stream));
                 HIPCHK(hipMemsetAsync(s.sum + 9, 0, 8, stream));
+                // (before any skip: a shard with no parents this round receives items, and they must
+                // not bid in LXY / L under an earlier round's tag)
+                s.lx_bid = false;
                 if (!s.np || fail[li]) continue;
                 const bool split = split_min && s.np >= split_min;
                 // (the fused election table holds a round's successors at load <= 1/2: ensure_chunk)
@@ -2536,7 +2547,6 @@ struct rmc_ctx {
                 xp[li] = make_plan(M.data(), W, K1, sh[li].id);
                 xb[li] = reverse_plan(xp[li]);
             }
-            SDBG("0");
             // (2) successors to their owners: owner-grouped items, cursors preset to the groups
             Payload items{&xp, std::vector<const void *>(NL), std::vector<void *>(NL), sizeof(XItem)};
             for (size_t li = 0; li < NL; li++) {
@@ -2555,9 +2565,7 @@ struct rmc_ctx {
                 items.send[li] = s.xs;
                 items.recv[li] = s.xr;
             }
-            SDBG("1");
             timed(PH_XCHG, [&] { exchange({items}); });
-            SDBG("2");
             // (3) owners: seen-set probe, smallest key per new fingerprint, verdicts, seen-set insert
             Payload verdicts{&xb, std::vector<const void *>(NL), std::vector<void *>(NL), 4};
             for (size_t li = 0; li < NL; li++) {
@@ -2599,9 +2607,7 @@ struct rmc_ctx {
                 // a failed owner answers "no winner" everywhere (the round is abandoned at the next agreement)
                 if (fail[li]) HIPCHK(hipMemsetAsync(o.rflag, 0, R * 4, stream));
             }
-            SDBG("3");
             timed(PH_XCHG, [&] { exchange({verdicts}); });
-            SDBG("4");
             // (4) sources: verdicts on the slots, winners per parent and their words
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
@@ -2614,7 +2620,6 @@ struct rmc_ctx {
                     if (Q.plist) launch_nzlist(Q, s.np, stream);
                 });
             }
-            SDBG("5");
             std::vector<uint64_t> tab((size_t)TAB * W, 0);
             std::vector<uint64_t> ins(NL, 0), wnum(NL, 0), wwords(NL, 0);
             for (size_t li = 0; li < NL; li++) {
@@ -2629,7 +2634,6 @@ struct rmc_ctx {
                 }
             }
             collect_times(st);
-            SDBG("6");
             // (5) commit: every shard's winners, in TLC order, into its outbox (+ invariants)
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
@@ -2669,7 +2673,6 @@ struct rmc_ctx {
                 }
             }
             collect_times(st);
-            SDBG("7");
             for (size_t li = 0; li < NL; li++) tab[TAB * sh[li].id + 6] = (uint64_t)(-fail[li]);
             allreduce(tab.data(), TAB * W, false);  // rows: each shard's own, zero elsewhere
             {
@@ -2689,7 +2692,6 @@ struct rmc_ctx {
                 seconds += st->seconds;
                 return status;
             }
-            SDBG("8");
             // (7) winners to the shards owning their global next-level indices (rmc_plan.h route_pieces)
             std::vector<uint64_t> A(W + 1, level_new);
             for (int t = 0; t < W; t++) A[t + 1] = A[t] + tab[TAB * t + 1];
@@ -2783,7 +2785,6 @@ struct rmc_ctx {
                 rows2[li][2 * W + 1] = force ? 0 : s.ib_cap;
                 rows2[li][2 * W + 2] = (uint64_t)(-fail[li]);
             }
-            SDBG("9");
             std::vector<uint64_t> M2 = gather_rows(rows2, K2);
             agree(col_max(M2, K2, 2 * W + 2));
             {
@@ -2825,7 +2826,6 @@ struct rmc_ctx {
                 words_.recv[li] = s.ib;
             }
             timed(PH_XCHG, [&] { exchange({sides, words_}); });
-            SDBG("10");
             // (8) owners append what they received, in source order, to the next level
             for (size_t li = 0; li < NL; li++) {
                 Shard &o = sh[li];
@@ -2863,7 +2863,6 @@ struct rmc_ctx {
                 o.nxt_n += n;
                 o.nxt_words += words;
             }
-            SDBG("11");
             // an append failure rides on the next round's gathered matrix; after the level's last
             // round it is agreed here
             if (c + 1 == rounds) agree_now();
@@ -3197,13 +3196,20 @@ struct rmc_ctx {
             h.spec_variant != want.spec_variant || h.no_symmetry != want.no_symmetry || h.msg_cap != want.msg_cap)
             fail(" is not a checkpoint of this configuration");
         if (h.scheme != want.scheme) fail(" was written with another fingerprint scheme");
+        // a smaller stored chunk size is adopted (the buffers hold it): the chunk follows free memory at
+        // create when budgets are explicit, so a resume on a device with less headroom must not fail
+        if (multi && h.chunk_parents && h.chunk_parents < want.chunk_parents)
+            want_chunk_parents_adopt = h.chunk_parents;
+        else
+            want_chunk_parents_adopt = 0;
         if (h.W != want.W || h.first_shard != want.first_shard || h.nshards != want.nshards ||
-            h.chunk_parents != want.chunk_parents || h.shard_min != want.shard_min)
+            (h.chunk_parents != want.chunk_parents && !want_chunk_parents_adopt) || h.shard_min != want.shard_min)
             fail(" was written with another shard layout (world size, rank, virtual shards, chunk size or shard_min)");
         // the header's own consistency, before anything is allocated from it
         if (h.check != header_check(h) || h.n_glevel > 100000 || (h.replicated && h.n_glevel) ||
             (multi && !h.replicated && (h.n_glevel == 0 || h.L_shard <= 0)))
             fail(" has an inconsistent header");
+        if (want_chunk_parents_adopt) chunk_parents = want_chunk_parents_adopt;  // (<= the buffers' size)
         std::vector<uint64_t> gl(h.n_glevel);
         ok = std::fread(gl.data(), 8, gl.size(), f) == gl.size();
         for (size_t i = 1; ok && i < gl.size(); i++) ok = gl[i] > gl[i - 1];
@@ -3345,6 +3351,14 @@ struct rmc_ctx {
             s.tflushed = s.trace_end = 0;
             s.hpar.n = s.hslot.n = 0;
             s.level_start.clear();
+            if (s.lx_round) {
+                // LXY / L served as a sharded run's owner table: its owner keys (top 16 bits <= 0xFFFD)
+                // are smaller than any fused election word (elect_key: 0xFFFF...), so the next run's
+                // fused levels would keep them and drop states -- back to the fused table's empty state
+                HIPCHK(hipMemsetAsync(s.LXY, 0, s.lcap * 16, stream));
+                HIPCHK(hipMemsetAsync(s.L, 0xFF, s.lcap * 8, stream));
+                s.lxy_epoch0 = s.epoch;
+            }
             s.lx_round = 0;  // the fused levels of the next run use LXY / L again
         }
         // (the clears are stream-ordered before the next run's first kernel: no wait here)

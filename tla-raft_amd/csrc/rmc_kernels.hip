@@ -2681,15 +2681,11 @@ bool get_kernels(int N, int V, int msg_cap, bool become_follower, KernelSet *ks)
         else fill<n, v, mr, false>(ks);                           \
         return true;                                              \
     }
-#ifdef RMC_QUICK  // kernel experiments: Raft.cfg's instance only (compile time)
-    RMC_CASE(3, 2, 1)
-#else
     RMC_CASE(2, 1, 1) RMC_CASE(2, 2, 1)
     RMC_CASE(3, 1, 1) RMC_CASE(3, 2, 1) RMC_CASE(3, 3, 1)
     RMC_CASE(3, 1, 2) RMC_CASE(3, 2, 2)
     RMC_CASE(4, 1, 2) RMC_CASE(4, 2, 2)
     RMC_CASE(5, 1, 2) RMC_CASE(5, 2, 2)
-#endif
 #undef RMC_CASE
     return false;
 }
