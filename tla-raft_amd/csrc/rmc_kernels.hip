@@ -24,6 +24,8 @@
 //   FUSED        single-GPU level: expand + fingerprint + seen-set probe + election + staging
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "rmc_kernels.h"
 
 // waves per SIMD the n >= 4 / two-round expansion kernel is compiled for (register budget)
@@ -101,13 +103,44 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane, uint32_
     return x - v;
 }
 
+// ---- race probe (a test build: -DRMC_RACE_PROBE, tools/build_variant.sh race) -----------------------
+// Every place where blocks of one launch hand state to each other gets a forced worst-case schedule:
+//   * the device loop's commit: the first block without a parent of its level waits until the
+//     launch's last arriver has written the next level's control block, then reads its own -- the
+//     late-block race of round 4, made to happen on every level;
+//   * the last-arriver counters (k_wincount's tickets, k_commit's ticks): block 0 arrives last;
+//   * the elections (elect_slot, owner_bid): a claimer holds its y word back, so candidates of the
+//     same fingerprint find x claimed and y not yet visible.
+// rmc_debug_race(1) switches the device loop back to one control block per level (read and written
+// in place, the logic before the pair): with the late block forced, that must give wrong results.
+#ifdef RMC_RACE_PROBE
+__device__ int g_race_single = 0;
+extern "C" int rmc_debug_race(int single) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_race_single), &single, sizeof single) == hipSuccess ? 0 : -1;
+}
+// the block a level reads and the one its commit writes (single: the pair's first block for both)
+__device__ __forceinline__ LevelCtl *ctl_cur(const KParams &P) {
+    return g_race_single ? (P.ctl < P.ctl_next ? P.ctl : P.ctl_next) : P.ctl;
+}
+__device__ __forceinline__ LevelCtl *ctl_nxt(const KParams &P) { return g_race_single ? ctl_cur(P) : P.ctl_next; }
+// bounded wait: s_sleep 127 (~8 K clocks) up to `n` times while pred()
+template <class F>
+__device__ __forceinline__ void race_wait(int n, F &&pred) {
+    for (int i = 0; i < n && pred(); i++) __builtin_amdgcn_s_sleep(127);
+}
+__device__ __forceinline__ void race_delay(int n) { race_wait(n, [] { return true; }); }
+#else
+__device__ __forceinline__ LevelCtl *ctl_cur(const KParams &P) { return P.ctl; }
+__device__ __forceinline__ LevelCtl *ctl_nxt(const KParams &P) { return P.ctl_next; }
+#endif
+
 // ---- device-driven level loop -------------------------------------------------------------
 // With P.ctl set, a level's kernels take the parent range, id bases, ring positions, election
 // epoch and table size from the control block the previous level's commit wrote (a kernel
 // boundary makes it visible); once the loop has stopped every block returns at once.
 __device__ __forceinline__ bool level_args(KParams &P) {
     if (!P.ctl) return true;
-    const LevelCtl *c = P.ctl;
+    const LevelCtl *c = ctl_cur(P);
     if (c->stop != CTL_RUN) return false;
     P.done_levels = c->done_levels;
     P.p_begin = 0;
@@ -1229,6 +1262,9 @@ __device__ __forceinline__ uint32_t elect_slot(ulonglong2 *LXY, unsigned long lo
         if ((v & 0xFFFFull) != tag) {
             const unsigned long long prev = atomicCAS(px, v, xk);
             if (prev == v) {
+#ifdef RMC_RACE_PROBE
+                if ((q & 7u) == 0u) race_delay(2);  // x claimed, y not yet visible
+#endif
                 __hip_atomic_store(py, yk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
             }
@@ -1672,6 +1708,580 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
     PHASE_FLUSH;
 }
 
+// ---- split chunk expansion, a lane per (parent, item) -------------------------------------------
+// k_expand<..., M_SPLIT> gives every parent a 64-lane wave: the wave decodes the parent's core on all
+// 64 lanes, builds a bitmap of its message ids, then lane k evaluates message k's receive action and
+// lanes 0 .. N * SLOTS_PER_SERVER - 1 the non-message slots -- about 26 + 24 busy lanes of 128 at
+// Raft.cfg's depth, every message type's branch run one after another, and the TLC-order ranks by
+// a loop over the enabled lanes.  Here a 256-thread block takes 64 consecutive parents at a time:
+//   (a) their records -- consecutive in the frontier ring -- are copied into LDS in one coalesced
+//       pass; a lane per parent decodes its core once into LDS and lists its *items*: one per
+//       message (UpdateTerm tla:175, ResponseVote tla:132, FollowerAccept/RejectEntry tla:275/302,
+//       HandleAppendResp tla:374 -- at most one is enabled per message; with the tla:420 variant also
+//       BecomeFollower) and one per non-message slot the server's role can enable (a follower only
+//       BecomeCandidate tla:107, a candidate also BecomeLeader tla:157, a leader ClientReq tla:233 per
+//       value, LeaderAppendEntry tla:242 per peer, LeaderCanCommit tla:398 and Restart tla:409);
+//   (b) a lane per message adds its hashes into the parent's per-pair sums (the hash context
+//       k_hash_probe reads) and counts the votes BecomeLeader needs (tla:160-164), LDS atomics;
+//   (c) the items of whole parents, up to 256 at a time, a lane each: the action on the acting
+//       server's row only (every action of tla:107-414 changes only votedFor / currentTerm / role /
+//       commitIndex / logs / matchIndex / nextIndex of its server s, pendingResponse, the aux
+//       counters and msgs), `m \notin msgs` by a binary search of the parent's sorted ids in LDS;
+//   (d) each enabled successor's rank in TLC order (slot keys increase in TLC order, Next tla:416-430)
+//       from the parent's list of enabled keys, and its staged row at slot pl * MX + rank -- the
+//       layout k_hash_probe, k_insert_winners and the commits read, unchanged.
+#ifndef RMC_ITEMS_PB
+#define RMC_ITEMS_PB 64
+#endif
+constexpr int XB_PARENTS = RMC_ITEMS_PB;  // parents per batch (<= 64: a lane of wave 0 each)
+constexpr int XB_THREADS = 256;  // threads per block = items per evaluation round at most
+
+// votedFor, currentTerm, role, commitIndex, Len(logs) of server s and s itself: staging word 0
+__device__ __forceinline__ uint32_t row_w0(uint32_t vf, uint32_t ct, uint32_t role, uint32_t ci, uint32_t ll,
+                                           uint32_t s) {
+    return vf | (ct << 4) | (role << 8) | (ci << 12) | (ll << 16) | (s << 20);
+}
+
+// g \in msgs of a parent whose sorted ids are ids[0 .. nm) (LDS): branch-free lower bound
+template <int MCAP>
+__device__ __forceinline__ bool ids_contain(const uint16_t *ids, uint32_t nm, uint32_t g) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t st = (uint32_t)MCAP; st; st >>= 1)
+        if (pos + st <= nm && (uint32_t)ids[pos + st - 1] < g) pos += st;
+    return pos < nm && (uint32_t)ids[pos] == g;
+}
+
+// one successor candidate of an item: the acting server's staged row (stage_succ's layout)
+template <int NADD>
+struct RowSucc {
+    uint32_t w0, lw, mirow, nirow, pend, misc;
+    uint32_t key;  // KEY_NONE: disabled
+    uint32_t nadd;
+    uint32_t add[NADD];
+};
+
+template <int NADD>
+__device__ __forceinline__ void row_stage(const RowSucc<NADD> &o, uint32_t nm, int sw4, uint4 *dst) {
+    uint32_t a[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < NADD; k++) a[k] = o.add[k];
+    const uint32_t misc = (o.misc & ~0xFF0000u) | ((nm + o.nadd) << 16);
+    dst[0] = make_uint4(o.w0, o.lw, o.mirow, o.nirow);
+    dst[1] = make_uint4(o.pend, misc, o.key | (o.nadd << 16), a[0] | (a[1] << 16));
+    if (sw4 > 2) dst[2] = make_uint4(a[2] | (a[3] << 16), 0u, 0u, 0u);
+}
+
+// The message item k (info word m) of a parent whose nibble core is pc (LDS) -> at most one successor
+// o (and with BFV the BecomeFollower one, ob).  The same guards and updates as eval_msg, on the row of
+// s = m.dst; pid is the id of the one message the action may send (looked up before any branch).
+template <int N, int V, int MR, bool BFV>
+__device__ __forceinline__ void item_msg(const KParams &P, const uint32_t *pc, const uint16_t *ids, uint32_t nm,
+                                         uint32_t k, uint32_t m, uint32_t pid, bool pres, RowSucc<Spec<N, V, MR>::NADD> &o,
+                                         RowSucc<Spec<N, V, MR>::NADD> &ob, uint32_t &akey) {
+    // pres: pid \in msgs (the parent's), found by the message pass
+    using Lo = Layout<N, V>;
+    using S = Spec<N, V, MR>;
+    const uint32_t s = mi_dst(m), typ = mi_type(m), mt = mi_term(m), src = mi_src(m);
+    uint32_t vf = nib(pc[Lo::W_VF], s), ct = nib(pc[Lo::W_CT], s), role = nib(pc[Lo::W_ROLE], s);
+    uint32_t ci = nib(pc[Lo::W_CI], s), ll = nib(pc[Lo::W_LL], s);
+    const uint32_t lw = pc[Lo::W_LOG + s], mirow = pc[Lo::W_MI + s], nirow = pc[Lo::W_NI + s];
+    const uint32_t pend = pc[Lo::W_PEND], misc = pc[Lo::W_MISC];
+    o.key = KEY_NONE;
+    o.nadd = 0;
+#pragma unroll
+    for (int a = 0; a < S::NADD; a++) o.add[a] = 0;
+    o.lw = lw; o.mirow = mirow; o.nirow = nirow; o.pend = pend; o.misc = misc;
+    o.w0 = row_w0(vf, ct, role, ci, ll, s);
+    if (BFV) {
+        // FollowerUpdateTerm / CandidateToFollower / LeaderToFollower (tla:190-229); msgs unchanged
+        ob = o;
+        const bool up = mt > ct, step = mt == ct && typ == AREQ && role == CAN;
+        if (up || step) {
+            const uint32_t bct = up ? mt : ct, brole = role != FOL ? (uint32_t)FOL : role;
+            const uint32_t bvf = (role != FOL && up) ? VF_NONE : vf;
+            ob.w0 = row_w0(bvf, bct, brole, ci, ll, s);
+            ob.key = slot_key(s, BF, k);
+        }
+    }
+    if (mt > ct) {  // UpdateTerm, first disjunct (tla:178-182)
+        o.w0 = row_w0(VF_NONE, mt, FOL, ci, ll, s);
+        o.key = slot_key(s, UT, k);
+        return;
+    }
+    if (mt != ct) return;
+    if (typ == AREQ && role != FOL) {  // UpdateTerm, second disjunct (tla:183-188)
+        if (role == LEA) { akey = slot_key(s, UT, 0); return; }  // Assert(role[s] # Leader) tla:185
+        o.w0 = row_w0(vf, ct, FOL, ci, ll, s);
+        o.key = slot_key(s, UT, k);
+        return;
+    }
+    if (typ == VREQ && role == FOL) {  // ResponseVote tla:132-155
+        if (!(vf == VF_NONE || vf == src)) return;
+        const uint32_t llt = lw_term(lw, ll), mlli = mi_x1(m), mllt = mi_x2(m);
+        if (!(mllt > llt || (mllt == llt && mlli >= ll))) return;
+        if (pres) return;
+        o.w0 = row_w0(src, ct, role, ci, ll, s);
+        o.add[0] = pid; o.nadd = 1;
+        o.key = slot_key(s, RV, k);
+        return;
+    }
+    if (typ == AREQ && role == FOL) {  // FollowerAcceptEntry / FollowerRejectEntry tla:275-321
+        const uint32_t pli = mi_x1(m), plt = mi_x2(m), lc = mi_x3(m), ent = mi_ent(m);
+        const bool match = pli <= ll && plt == lw_term(lw, pli);  // LogMatch tla:271-273
+        if (match) {
+            const uint32_t nl = pli + ent;
+            const bool append_new = nl > ll;
+            const uint32_t eb = mi_et(m) | (mi_ev(m) << 4);
+            const bool truncated = nl <= ll && ent && lw_byte(lw, nl) != eb;
+            const uint32_t mn = (lc < nl || (P.quirks & 2u)) ? lc : nl;  // (RaftCommitPastLog: no Min)
+            const uint32_t nci = ci > mn ? ci : mn;
+            uint32_t nll = ll;
+            if (truncated || append_new) {
+                // newLog == SubSeq(logs[s], 1, prevLogIndex) \o entries   (tla:291)
+                const uint32_t keep = pli >= 2 ? (pli - 1) * 8 : 0;  // bytes of indices 2..pli
+                uint32_t nlw = keep >= 32 ? lw : (lw & ((1u << keep) - 1u));
+                if (ent) nlw |= eb << (8 * (nl - 2));
+                o.lw = nlw;
+                nll = nl;
+            }
+            o.w0 = row_w0(vf, ct, role, nci, nll, s);
+            if (!pres) { o.add[0] = pid; o.nadd = 1; }
+            o.key = slot_key(s, FAE, k);
+        } else {
+            if (pres) return;
+            o.add[0] = pid; o.nadd = 1;
+            o.key = slot_key(s, FRE, k);
+        }
+        return;
+    }
+    if (typ == ARESP && role == LEA) {  // HandleAppendResp tla:374-396
+        const uint32_t pb = s * N + src;
+        if (!((pend >> pb) & 1u)) return;
+        const uint32_t pli = mi_x1(m);
+        const uint32_t mi = nib(mirow, src), ni = nib(nirow, src);
+        uint32_t nmi = mirow, nni = nirow;
+        if (mi_x2(m)) {
+            if (!(mi < pli)) return;
+            nmi = setnib(mirow, src, pli);
+            nni = setnib(nirow, src, pli + 1);
+        } else {
+            if (!(pli + 1 == ni)) return;
+            if (!(pli > mi)) return;
+            nni = setnib(nirow, src, pli);
+        }
+        o.mirow = nmi;
+        o.nirow = nni;
+        o.pend = pend & ~(1u << pb);
+        o.key = slot_key(s, HAR, k);
+    }
+}
+
+// the id of the one message a message item's action may send (ResponseVote's VoteResp, FollowerAccept /
+// RejectEntry's AppendResp), or NAT_NONE -- msg_nat on the item's row
+template <int N, int V>
+__device__ __forceinline__ uint32_t item_msg_nat(const KParams &P, const uint32_t *pc, uint32_t m) {
+    using Lo = Layout<N, V>;
+    const uint32_t s = mi_dst(m), typ = mi_type(m), mt = mi_term(m), src = mi_src(m);
+    if (mt != nib(pc[Lo::W_CT], s) || nib(pc[Lo::W_ROLE], s) != FOL) return NAT_NONE;
+    if (typ == VREQ) return nat_vresp(P.d, s, src, mt);
+    if (typ != AREQ) return NAT_NONE;
+    const uint32_t ll = nib(pc[Lo::W_LL], s), lw = pc[Lo::W_LOG + s];
+    const uint32_t pli = mi_x1(m), plt = mi_x2(m), ent = mi_ent(m);
+    const bool match = pli <= ll && plt == lw_term(lw, pli);  // LogMatch tla:271-273
+    return match ? nat_aresp(P.d, s, src, mt, pli + ent, 1) : nat_aresp(P.d, s, src, mt, pli, 0);
+}
+
+// The non-message slot t of server s (eval_slot's slots: 0 BecomeCandidate, 1 BecomeLeader, 2 .. 1 + V
+// ClientReq, then LeaderAppendEntry per peer, LeaderCanCommit, Restart) -> at most one successor.
+template <int N, int V, int MR>
+__device__ __forceinline__ void item_slot(const KParams &P, const uint32_t *pc, const uint16_t *ids, uint32_t nm,
+                                          uint32_t vp, uint32_t s, uint32_t t, RowSucc<Spec<N, V, MR>::NADD> &o) {
+    using Lo = Layout<N, V>;
+    using S = Spec<N, V, MR>;
+    const uint32_t vf = nib(pc[Lo::W_VF], s), ct = nib(pc[Lo::W_CT], s), role = nib(pc[Lo::W_ROLE], s);
+    const uint32_t ci = nib(pc[Lo::W_CI], s), ll = nib(pc[Lo::W_LL], s);
+    const uint32_t lw = pc[Lo::W_LOG + s], mirow = pc[Lo::W_MI + s], nirow = pc[Lo::W_NI + s];
+    const uint32_t pend = pc[Lo::W_PEND], misc = pc[Lo::W_MISC];
+    o.key = KEY_NONE;
+    o.nadd = 0;
+#pragma unroll
+    for (int a = 0; a < S::NADD; a++) o.add[a] = 0;
+    o.lw = lw; o.mirow = mirow; o.nirow = nirow; o.pend = pend; o.misc = misc;
+    o.w0 = row_w0(vf, ct, role, ci, ll, s);
+    if (t == 0) {  // BecomeCandidate tla:107-130
+        const uint32_t ec = misc & 15u;
+        if (!((int)ec < P.E) || !(role == FOL || role == CAN)) return;
+        const uint32_t term = ct + 1, llt = lw_term(lw, ll);
+        uint32_t sid[N - 1];  // the VoteReqs to the N - 1 peers, looked up together
+#pragma unroll
+        for (int i = 0; i < N - 1; i++) {
+            const uint32_t p = (uint32_t)i < s ? (uint32_t)i : (uint32_t)i + 1u;
+            sid[i] = (uint32_t)P.t.nat2id[nat_vreq(P.d, s, p, term, ll, llt)];
+        }
+        uint32_t na = 0;
+#pragma unroll
+        for (int i = 0; i < N - 1; i++) {
+            if (!ids_contain<S::MCAP>(ids, nm, sid[i])) {
+#pragma unroll
+                for (int a = 0; a < S::NADD; a++) o.add[a] = ((uint32_t)a == na) ? sid[i] : o.add[a];
+                na++;
+            }
+        }
+        o.nadd = na;
+        o.w0 = row_w0(s, term, CAN, ci, ll, s);
+        o.misc = (misc & ~15u) | (ec + 1);
+        o.key = slot_key(s, BC, 0);
+        return;
+    }
+    if (t == 1) {  // BecomeLeader tla:157-173
+        if (role != CAN) return;
+        if (!(vp + 1 >= ((P.quirks & 1u) ? 1u : (uint32_t)(N / 2 + 1)))) return;  // (RaftSplitBrain: quorum 1)
+        uint32_t mr = 0, nr = 0;
+#pragma unroll
+        for (int u = 0; u < N; u++) {
+            mr = setnib(mr, u, (uint32_t)u != s ? 1u : ll);
+            nr = setnib(nr, u, ll + 1);
+        }
+        o.mirow = mr;
+        o.nirow = nr;
+        o.pend = pend & ~(((1u << N) - 1u) << (s * N));
+        o.w0 = row_w0(vf, ct, LEA, ci, ll, s);
+        o.key = slot_key(s, BL, 0);
+        return;
+    }
+    if (role != LEA) return;
+    if (t < 2 + (uint32_t)V) {  // ClientReq tla:233-240, witness v
+        const uint32_t v = t - 2;
+        if ((misc >> (8 + v)) & 1u) return;  // valSent[v] # None
+        o.misc = misc | (1u << (8 + v));
+        o.lw = lw | ((ct | (v << 4)) << (8 * (ll + 1 - 2)));
+        o.mirow = setnib(mirow, s, ll + 1);
+        o.w0 = row_w0(vf, ct, role, ci, ll + 1, s);
+        o.key = slot_key(s, CR, v);
+        return;
+    }
+    if (t < 2 + (uint32_t)V + (N - 1)) {  // LeaderAppendEntry tla:242-269, witness dst
+        const uint32_t q = t - 2 - V;
+        const uint32_t dst = q < s ? q : q + 1;
+        const uint32_t ni = nib(nirow, dst);
+        if (!(ni <= ll + 1)) return;
+        const uint32_t pb = s * N + dst;
+        if ((pend >> pb) & 1u) return;
+        const uint32_t pli = ni - 1, plt = lw_term(lw, pli);
+        const uint32_t ent = ni <= ll ? 1u : 0u;
+        const uint32_t eb = ent ? lw_byte(lw, ni) : 0u;
+        const uint32_t id = P.t.nat2id[nat_areq(P.d, s, dst, ct, pli, plt, ent, eb & 15u, eb >> 4, ci)];
+        if (ids_contain<S::MCAP>(ids, nm, id)) return;  // m \notin msgs
+        o.pend = pend | (1u << pb);
+        o.add[0] = id;
+        o.nadd = 1;
+        o.key = slot_key(s, LAE, dst);
+        return;
+    }
+    if (t == 2 + (uint32_t)V + (N - 1)) {  // LeaderCanCommit tla:398-407
+        const uint32_t thr = P.seeded ? (uint32_t)N : (uint32_t)(N / 2 + 1);
+        const uint32_t med = median_row<N>(mirow, thr);
+        if (!(med > ci)) return;
+        o.w0 = row_w0(vf, ct, role, med, ll, s);
+        o.key = slot_key(s, LCC, 0);
+        return;
+    }
+    {  // Restart tla:409-414
+        const uint32_t rc = (misc >> 4) & 15u;
+        if (!((int)rc < P.R)) return;
+        o.w0 = row_w0(vf, ct, FOL, ci, ll, s);
+        o.misc = (misc & ~0xF0u) | ((rc + 1) << 4);
+        o.key = slot_key(s, RS, 0);
+    }
+}
+
+// the non-message slots a server's role can enable: first slot and count, 4 bits each, per server
+template <int N, int V>
+__device__ __forceinline__ uint32_t slot_range(uint32_t role, uint32_t ec, uint32_t rc, int E, int R) {
+    constexpr uint32_t SPS = 4 + V + (N - 1);
+    if (role == LEA) return 2u | ((SPS - 2u - ((int)rc < R ? 0u : 1u)) << 4);  // ClientReq .. LeaderCanCommit (+ Restart)
+    const uint32_t bc = (int)ec < E ? 1u : 0u;                              // BecomeCandidate while elections remain
+    if (role == CAN) return (bc ? 0u : 1u) | ((bc + 1u) << 4);               // (+ BecomeLeader)
+    return bc << 4;
+}
+
+#ifndef RMC_ITEMS_WAVES  // waves per SIMD the item-parallel expansion's registers are cut for (0: the compiler's)
+#define RMC_ITEMS_WAVES 0
+#endif
+// Item classes: the action an item can take, from its message and its server's term and role alone
+// (the first guards of eval_msg / eval_slot) -- a round's items are evaluated class by class, so the
+// lanes of a wave take one action's branch, and messages no action can receive (an older term than
+// their destination's, a VoteResp) are never items at all.
+enum ItemClass : uint32_t {
+    IC_UT = 0,  // m.term > currentTerm[s]: UpdateTerm's first disjunct (+ BecomeFollower)        tla:178-182
+    IC_UT2,     // = term, AppendReq, s not a follower: UpdateTerm's second (Assert tla:185) (+ BF)  tla:183-188
+    IC_RV,      // = term, VoteReq, s a follower: ResponseVote                                      tla:132-155
+    IC_AE,      // = term, AppendReq, s a follower: FollowerAcceptEntry / FollowerRejectEntry       tla:275-321
+    IC_HAR,     // = term, AppendResp, s a leader: HandleAppendResp                                 tla:374-396
+    IC_BC, IC_BL, IC_CR, IC_LAE, IC_LCC, IC_RS,  // the non-message slots (eval_slot)
+    IC_N,
+    IC_DEAD = 0xFF
+};
+__device__ __forceinline__ uint32_t msg_class(uint32_t m, uint32_t ct, uint32_t role) {
+    const uint32_t mt = mi_term(m), typ = mi_type(m);
+    if (mt > ct) return IC_UT;
+    if (mt < ct) return IC_DEAD;
+    if (typ == AREQ) return role != FOL ? IC_UT2 : IC_AE;
+    if (typ == VREQ) return role == FOL ? IC_RV : IC_DEAD;
+    if (typ == ARESP) return role == LEA ? IC_HAR : IC_DEAD;
+    return IC_DEAD;  // VoteResp: only counted (BecomeLeader)
+}
+template <int N, int V>
+__device__ __forceinline__ uint32_t slot_class(uint32_t t) {
+    return t == 0 ? IC_BC : t == 1 ? IC_BL : t < 2 + (uint32_t)V ? IC_CR : t < 2 + (uint32_t)V + (N - 1) ? IC_LAE
+         : t == 2 + (uint32_t)V + (N - 1) ? IC_LCC : IC_RS;
+}
+
+template <int N, int V, int MR, bool BFV>
+__global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KParams P) {
+    using S = Spec<N, V, MR>;
+    using Lo = Layout<N, V>;
+    constexpr int PB = XB_PARENTS, NT = XB_THREADS;
+    constexpr int CCW = S::CCW, RECW = S::RECW_MAX, NW = Lo::NW, NWP = (NW + 3) / 4 * 4;
+    constexpr int MX = S::MAXS + (BFV ? S::MCAP : 0);
+    constexpr int NCI = BFV ? 2 : 1;  // candidates of a message item
+    constexpr int NPR = N * (N - 1);
+    constexpr int CTXW = ctx_words<N, V>(), CC = ((CCW + 3) / 4) * 4;
+    static_assert(S::MCAP + N * S::SLOTS_PER_SERVER <= NT, "a parent's items fit one evaluation round");
+    static_assert(S::MCAP <= 128 && PB <= 64, "item codes: parent << 8 | slot bit << 7 | message index or s << 4 | t");
+    __shared__ uint32_t sRec[PB * RECW];           // the batch's records, as in the ring
+    __shared__ uint32_t sCore[PB * NWP];           // their nibble cores
+    // per message of the batch: parent | class << 8 | (the id its action may send \in msgs) << 12 | that id << 16
+    __shared__ uint32_t sMI[PB * S::MCAP];
+    __shared__ uint32_t sVp[PB * N];               // per parent and server: VoteResps to it in its term (tla:160-164)
+    __shared__ uint32_t sOff[PB];                  // record's first word in sRec
+    __shared__ uint32_t sItm[PB + 1], sMsc[PB + 1];  // items / messages: exclusive scans over the batch
+    __shared__ uint32_t sLive[PB];                 // per parent: messages some action may receive
+    __shared__ unsigned long long sSlot[PB];       // slot_range per server, 8 bits each
+    __shared__ uint32_t sCnt[PB], sAk[PB];         // enabled successors, smallest Assert key
+    __shared__ uint32_t sCc[IC_N];                 // the round's items per class
+    // the batch's hash sums (until the hash context is written), then the rounds' item lists and keys
+    constexpr int UM = 2 * PB * NPR * 8, UQ = IC_N * NT * 2 + NT * NCI * 2;
+    __shared__ __attribute__((aligned(16))) unsigned char sU[UM > UQ ? UM : UQ];
+    unsigned long long *sM0 = reinterpret_cast<unsigned long long *>(sU), *sM1 = sM0 + PB * NPR;
+    uint16_t *sQ = reinterpret_cast<uint16_t *>(sU);   // [IC_N][NT] item codes by class
+    uint16_t *sKey = sQ + IC_N * NT;                    // [NT * NCI] the round's enabled keys, per parent at its items' offset
+    __shared__ uint32_t sSpan;
+    const int tid = threadIdx.x;
+    const uint64_t np = P.p_end - P.p_begin;
+    PHASE_DECL
+    for (uint64_t b0 = (uint64_t)blockIdx.x * PB; b0 < np; b0 += (uint64_t)gridDim.x * PB) {
+        const uint32_t nb = (uint32_t)(np - b0 < (uint64_t)PB ? np - b0 : (uint64_t)PB);
+        // (a) the batch's records: consecutive in the ring (every level is laid out in parent order)
+        if (tid < 64) {  // wave 0: a lane per parent
+            const uint64_t o = (uint32_t)tid < nb ? P.foff[P.p_begin + b0 + tid] : 0ull;
+            const uint64_t first = rdlane64(o, 0);
+            const uint64_t last = rdlane64(o, (int)nb - 1);
+            if ((uint32_t)tid < nb) sOff[tid] = (uint32_t)(o - first);
+            if (tid == 0) {
+                uint64_t span = last - first + RECW;
+                if (span > (uint64_t)PB * RECW) {  // not consecutive: never the case (see the commits)
+                    atomicOr(&P.flags[0], 2u);
+                    span = (uint64_t)PB * RECW;
+                }
+                sSpan = (uint32_t)span;
+            }
+        }
+        __syncthreads();
+        {
+            const uint64_t f0 = P.foff[P.p_begin + b0];
+            const uint64_t start = ring_wrap(P.fbase + f0, P.rcap);
+            const uint32_t span = sSpan;
+            for (uint32_t w = (uint32_t)tid; w < span; w += NT) sRec[w] = ring_word(P.front, start, w, P.rcap);
+        }
+        __syncthreads();
+        PHASE(0);
+        // a lane per parent: core, slots, counters; the message scan in wave 0
+        if (tid < 64) {
+            uint32_t nmj = 0;
+            if ((uint32_t)tid < nb) {
+                const uint32_t *rec = sRec + sOff[tid];
+                uint32_t pk[CCW], c[NW];
+#pragma unroll
+                for (int k = 0; k < CCW; k++) pk[k] = rec[k];
+                decode_core<N, V>(pk, c);
+#pragma unroll
+                for (int w = 0; w < NW; w++) sCore[tid * NWP + w] = c[w];
+                nmj = (c[Lo::W_MISC] >> 16) & 0xFFu;
+                const uint32_t ec = c[Lo::W_MISC] & 15u, rc = (c[Lo::W_MISC] >> 4) & 15u;
+                unsigned long long sl = 0;
+#pragma unroll
+                for (int s = 0; s < N; s++)
+                    sl |= (unsigned long long)slot_range<N, V>(nib(c[Lo::W_ROLE], s), ec, rc, P.E, P.R) << (8 * s);
+                sSlot[tid] = sl;
+#pragma unroll
+                for (int s = 0; s < N; s++) sVp[tid * N + s] = 0u;
+#pragma unroll
+                for (int k = 0; k < NPR; k++) { sM0[tid * NPR + k] = 0ull; sM1[tid * NPR + k] = 0ull; }
+                sCnt[tid] = 0u;
+                sAk[tid] = KEY_NONE;
+                sLive[tid] = 0u;
+            }
+            uint32_t tm;
+            const uint32_t xm = wave_excl_scan(nmj, tid, &tm);
+            if ((uint32_t)tid < nb) sMsc[tid] = xm;
+            if (tid == 0) sMsc[nb] = tm;
+        }
+        __syncthreads();
+        PHASE(1);
+        // (b) a lane per message: hash sums per server pair, votes per server, its class
+        const uint32_t tmsg = sMsc[nb];
+        for (uint32_t m = (uint32_t)tid; m < tmsg; m += NT) {
+            uint32_t j = 0;  // the last parent j with sMsc[j] <= m
+#pragma unroll
+            for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < nb && sMsc[j + st] <= m) ? j + st : j;
+            const uint32_t k = m - sMsc[j];
+            const uint32_t id = reinterpret_cast<const uint16_t *>(sRec + sOff[j] + CCW)[k];
+            const uint32_t inf = P.t.info[id];
+            const ulonglong2 g = P.t.gmsg[id];
+            const uint32_t src = mi_src(inf), dst = mi_dst(inf);
+            const int pi = pair_index(N, (int)src, (int)dst);
+            atomicAdd(&sM0[j * NPR + pi], (unsigned long long)g.x);
+            atomicAdd(&sM1[j * NPR + pi], (unsigned long long)g.y);
+            const uint32_t *pc = sCore + j * NWP;
+            const uint32_t ct = nib(pc[Lo::W_CT], dst);
+            if (mi_type(inf) == VRESP && mi_term(inf) == ct) atomicAdd(&sVp[j * N + dst], 1u);
+            const uint32_t c = msg_class(inf, ct, nib(pc[Lo::W_ROLE], dst));
+            // ResponseVote's VoteResp / Follower{Accept,Reject}Entry's AppendResp: its id and whether the
+            // parent holds it (m \notin msgs, tla:144,296,318), here where the parent's ids are at hand
+            uint32_t e = j | ((c == IC_DEAD ? 15u : c) << 8);
+            if (c == IC_RV || c == IC_AE) {
+                const uint32_t pid = P.t.nat2id[item_msg_nat<N, V>(P, pc, inf)];
+                const uint16_t *ids = reinterpret_cast<const uint16_t *>(sRec + sOff[j] + CCW);
+                e |= (ids_contain<S::MCAP>(ids, sMsc[j + 1] - sMsc[j], pid) ? 1u << 12 : 0u) | (pid << 16);
+            }
+            sMI[m] = e;
+            if (c != IC_DEAD) atomicAdd(&sLive[j], 1u);
+        }
+        __syncthreads();
+        PHASE(2);
+        // the batch's hash contexts (k_hash_probe): packed core padded to 16 B, then per server pair its
+        // sums {M_0 lo, hi, M_1 lo, hi}; the batch's parents are consecutive, so one coalesced range
+        for (uint32_t w = (uint32_t)tid; w < nb * (uint32_t)CTXW; w += NT) {
+            const uint32_t j = w / CTXW, k = w % CTXW;
+            uint32_t v = 0u;
+            if (k < (uint32_t)CC) {
+                v = k < (uint32_t)CCW ? sRec[sOff[j] + k] : 0u;
+            } else {
+                const uint32_t pi = (k - CC) >> 2, part = k & 3u;
+                const unsigned long long mm = (part >> 1) ? sM1[j * NPR + pi] : sM0[j * NPR + pi];
+                v = (part & 1u) ? (uint32_t)(mm >> 32) : (uint32_t)mm;
+            }
+            P.hctx[(b0 + j) * (uint64_t)CTXW + k] = v;
+        }
+        // items per parent: its live messages and its slots; their scan (wave 0)
+        if (tid < 64) {
+            uint32_t ni = 0;
+            if ((uint32_t)tid < nb) {
+                const unsigned long long sl = sSlot[tid];
+                ni = sLive[tid];
+#pragma unroll
+                for (int u = 0; u < N; u++) ni += (uint32_t)(sl >> (8 * u + 4)) & 15u;
+            }
+            uint32_t ti;
+            const uint32_t xi = wave_excl_scan(ni, tid, &ti);
+            if ((uint32_t)tid < nb) sItm[tid] = xi;
+            if (tid == 0) sItm[nb] = ti;
+        }
+        if (tid < IC_N) sCc[tid] = 0u;
+        __syncthreads();  // (also: the hash sums are read; sQ / sKey may reuse their words)
+        PHASE(3);
+        // (c) + (d): rounds of whole parents, up to NT items each
+        for (uint32_t a = 0; a < nb;) {
+            const uint32_t ibase = sItm[a];
+            uint32_t b = a;  // the last parent b with sItm[b] <= ibase + NT: parents a .. b - 1 fit
+#pragma unroll
+            for (uint32_t st = PB; st; st >>= 1) b = (b + st <= nb && sItm[b + st] <= ibase + NT) ? b + st : b;
+            const uint32_t nI = sItm[b] - ibase;
+            // the round's items into their class lists: live messages, then each parent's slots
+            for (uint32_t m = sMsc[a] + (uint32_t)tid; m < sMsc[b]; m += NT) {
+                const uint32_t e = sMI[m], c = (e >> 8) & 15u;
+                if (c == 15u) continue;
+                const uint32_t j = e & 0xFFu;
+                sQ[c * NT + atomicAdd(&sCc[c], 1u)] = (uint16_t)((j << 8) | (m - sMsc[j]));
+            }
+            for (uint32_t q = (uint32_t)tid; q < (b - a) * (uint32_t)N; q += NT) {  // a lane per (parent, server)
+                const uint32_t j = a + q / N, u = q % N;
+                const uint32_t rg = (uint32_t)(sSlot[j] >> (8 * u)) & 0xFFu;
+                for (uint32_t r = 0; r < (rg >> 4); r++) {
+                    const uint32_t t = (rg & 15u) + r, c = slot_class<N, V>(t);
+                    sQ[c * NT + atomicAdd(&sCc[c], 1u)] = (uint16_t)((j << 8) | 0x80u | (u << 4) | t);
+                }
+            }
+            __syncthreads();
+            RowSucc<S::NADD> o, ob;
+            o.key = KEY_NONE;
+            ob.key = KEY_NONE;
+            uint32_t j = 0, nmj = 0;
+            if ((uint32_t)tid < nI) {
+                // this lane's item: class lists concatenated in class order
+                uint32_t pre = 0, code = 0;
+#pragma unroll
+                for (uint32_t c = 0; c < IC_N; c++) {
+                    const uint32_t n = sCc[c], t = (uint32_t)tid - pre;
+                    if (t < n) code = sQ[c * NT + t];
+                    pre += n;
+                }
+                j = code >> 8;
+                const uint32_t *pc = sCore + j * NWP;
+                const uint16_t *ids = reinterpret_cast<const uint16_t *>(sRec + sOff[j] + CCW);
+                nmj = (pc[Lo::W_MISC] >> 16) & 0xFFu;
+                uint32_t akey = KEY_NONE;
+                if (!(code & 0x80u)) {
+                    const uint32_t k = code & 0x7Fu;
+                    const uint32_t inf = P.t.info[ids[k]], e = sMI[sMsc[j] + k];
+                    item_msg<N, V, MR, BFV>(P, pc, ids, nmj, k, inf, e >> 16, (e >> 12) & 1u, o, ob, akey);
+                } else {
+                    const uint32_t s = (code >> 4) & 7u, t = code & 15u;
+                    item_slot<N, V, MR>(P, pc, ids, nmj, sVp[j * N + s], s, t, o);
+                }
+                if (akey != KEY_NONE) atomicMin(&sAk[j], akey);
+                const uint32_t kb = (sItm[j] - ibase) * NCI;  // the parent's key list
+                if (o.key != KEY_NONE) sKey[kb + atomicAdd(&sCnt[j], 1u)] = (uint16_t)o.key;
+                if (BFV && ob.key != KEY_NONE) sKey[kb + atomicAdd(&sCnt[j], 1u)] = (uint16_t)ob.key;
+                if ((o.key != KEY_NONE && nmj + o.nadd > (uint32_t)S::MCAP)) atomicOr(&P.flags[0], 1u);
+            }
+            __syncthreads();
+            PHASE(4);
+            if ((uint32_t)tid < nI) {
+                const uint32_t kb = (sItm[j] - ibase) * NCI, cn = sCnt[j];
+                const uint64_t pl = b0 + j;
+#pragma unroll
+                for (int c = 0; c < NCI; c++) {
+                    const RowSucc<S::NADD> &x = c ? ob : o;
+                    if (x.key == KEY_NONE) continue;
+                    uint32_t rank = 0;
+                    for (uint32_t e = 0; e < cn; e++) rank += (uint32_t)sKey[kb + e] < x.key ? 1u : 0u;
+                    row_stage<S::NADD>(x, nmj, S::SW4, P.score + (pl * (uint64_t)MX + rank) * (uint64_t)S::SW4);
+                }
+            }
+            PHASE(5);
+            // per parent: successor count, |msgs|, Assert and deadlock keys (level-local index p)
+            if ((uint32_t)tid < b - a) {
+                const uint32_t jj = a + (uint32_t)tid;
+                const uint64_t pl = b0 + jj, p = P.p_begin + pl;
+                const uint32_t total = sCnt[jj], ak = sAk[jj];
+                P.cnt[pl] = total;
+                P.pnm[pl] = (sCore[jj * NWP + Lo::W_MISC] >> 16) & 0xFFu;
+                if (ak != KEY_NONE) atomicMin(&P.err[ERR_ASSERT], (((unsigned long long)p << 16) | ak) << 8);
+                else if (total == 0 && P.check_deadlock)
+                    atomicMin(&P.err[ERR_DEADLOCK], ((unsigned long long)p << 16) << 8);
+            }
+            if (tid < IC_N) sCc[tid] = 0u;  // (every lane has read its item: the sync above)
+            __syncthreads();
+            PHASE(6);
+            a = b;
+        }
+    }
+    PHASE_FLUSH;
+}
+
 // Every successor slot of a split chunk, a lane each: a wave takes 64 consecutive parents, their
 // successor counts are scanned across the wave and successor i of the group goes to lane i % 64 of
 // round i / 64 (its parent found by a binary search over the scan); f(parent pl, rank r).
@@ -1727,6 +2337,9 @@ __device__ __forceinline__ uint32_t owner_bid(ulonglong2 *OT, unsigned long long
         if ((v & 0xFFFFull) != tag) {  // free, or an earlier round's: claim it
             const unsigned long long prev = atomicCAS(&OT[g].x, v, xk);
             if (prev == v) {
+#ifdef RMC_RACE_PROBE
+                if ((key & 7u) == 0u) race_delay(2);  // x claimed, y not yet visible
+#endif
                 __hip_atomic_store(&OT[g].y, yk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 done = true;
             } else {
@@ -1996,6 +2609,9 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
     // agent-scope atomic add; the last adder reads the payload with sc1 loads)
     const uint32_t nb = ntiles < gridDim.x ? (ntiles ? ntiles : 1u) : gridDim.x;
     if (blockIdx.x >= nb) return;
+#ifdef RMC_RACE_PROBE
+    if (blockIdx.x == 0 && nb > 1) race_delay(8);  // block 0 arrives last
+#endif
     if (threadIdx.x == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t a = __hip_atomic_fetch_add(&P.tickets[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2094,7 +2710,7 @@ __device__ void finish_level(const KParams &P) {
         G = sm[0];
         Wn = sm[1];
         Ww = sm[SUM_WORDS];
-        if (P.ctl) c = *P.ctl;
+        if (P.ctl) c = *ctl_cur(P);
     }
     unsigned long long e = 0;
     if (lane < ERR_NSLOTS)
@@ -2107,8 +2723,8 @@ __device__ void finish_level(const KParams &P) {
     if (!P.ctl) return;
     if (bad) {  // the host reports the error from this level's buffers
         c.stop = CTL_ERROR;  // the erroring level's block, not advanced, into both (see below)
-        *P.ctl_next = c;
-        *P.ctl = c;
+        *ctl_nxt(P) = c;
+        *ctl_cur(P) = c;
         if (P.hloop) {
             c.stop = CTL_ERROR;
             P.hloop->ctl = c;
@@ -2146,8 +2762,13 @@ __device__ void finish_level(const KParams &P) {
     // into the other block of the pair: a late block of this launch (one with no parent, which
     // leaves without arriving) still reads this level's block, never the next level's
     // A stopped loop's block goes into both: the no-op launches after it read either.
-    *P.ctl_next = c;
-    if (c.stop != CTL_RUN) *P.ctl = c;
+    *ctl_nxt(P) = c;
+    if (c.stop != CTL_RUN) *ctl_cur(P) = c;
+#ifdef RMC_RACE_PROBE
+    // (the probe's late block polls `level`: the block's words visible device-wide first)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(&ctl_nxt(P)->level, c.level, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     // The loop's stop goes to the host here, with the control block (read after the drain); the
     // running loop's progress is reported by the next level's expansion as it starts (k_expand):
     // a write to host memory at the end of this kernel would hold the next launch ~5.6 us.
@@ -2167,6 +2788,9 @@ __device__ void finish_level(const KParams &P) {
 constexpr uint32_t CTICK_SUB = 32, CTICK_STRIDE = 32;
 __device__ __forceinline__ bool last_commit_block(uint32_t *tick, uint32_t nb) {
     if (blockIdx.x >= nb) return false;
+#ifdef RMC_RACE_PROBE
+    if (blockIdx.x == 0 && nb > 1) race_delay(8);  // block 0 arrives last
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t last = 0;
     if (threadIdx.x == 0 && nb <= CTICK_SUB) {  // few blocks: straight to the top counter
@@ -2200,6 +2824,18 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
     constexpr int MX = S::MAXS + (BFV ? S::MCAP : 0);  // successor slots per parent (k_expand)
+#ifdef RMC_RACE_PROBE
+    if (P.ctl) {  // the first block without a parent of this level reads its block after the level advanced
+        const LevelCtl *c = ctl_cur(P);
+        const uint32_t lv = c->level;
+        if (c->stop == CTL_RUN && (uint64_t)blockIdx.x == c->cur_n) {
+            race_wait(4000, [&] {
+                return __hip_atomic_load(&ctl_nxt(P)->level, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == lv;
+            });
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+    }
+#endif
     if (!level_args(P)) return;
     const int lane = threadIdx.x;
     const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -2585,6 +3221,15 @@ __global__ __launch_bounds__(256) void k_local_flags(KParams P, Seen seen, const
     if ((threadIdx.x & 63) == 0 && mine) atomicAdd(inserted, (unsigned long long)mine);
 }
 
+// split chunks: the item-parallel expansion (k_expand_items; RMC_SPLIT_ITEMS=0: the wave-per-parent one)
+static bool split_items() {
+    static const bool on = [] {
+        const char *v = std::getenv("RMC_SPLIT_ITEMS");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 static inline unsigned grid_for(uint64_t n) {
     const uint64_t cap = 256ull * RMC_GRID_PER_CU;  // one-wave blocks per CU (default 32) on 256 CUs
     return (unsigned)(n < cap ? (n ? n : 1) : cap);
@@ -2602,6 +3247,12 @@ struct Launch {
                            bm_bytes(P), s, P);
     }
     static void split(const KParams &P, hipStream_t s) {
+        if (split_items()) {
+            const uint64_t nbat = (P.p_end - P.p_begin + XB_PARENTS - 1) / XB_PARENTS;
+            hipLaunchKernelGGL((k_expand_items<N, V, MR, BFV>), dim3((unsigned)(nbat < 2048 ? (nbat ? nbat : 1) : 2048)),
+                               dim3(XB_THREADS), 0, s, P);
+            return;
+        }
         hipLaunchKernelGGL((k_expand<N, V, MR, M_SPLIT, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64),
                            bm_bytes(P), s, P);
     }

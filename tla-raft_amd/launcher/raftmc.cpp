@@ -336,6 +336,53 @@ int run_ranks(int N, bool onerank, const rmc_config &base, const std::function<i
     return code0;
 }
 
+// The process that prints TLC's output is not the one whose exit frees the run's memory: run_detached
+// forks one worker before anything touches a GPU; the worker prints everything, then closes its
+// stdout / stderr (tee's pipe, myrun.sh:3) and reports its exit code up a pipe before it exits.  The
+// kernel's teardown of the worker (~110 GB of host trace and the device memory after a Raft.cfg
+// exhaustion: ~4 s) then runs after this process has returned TLC's exit code,
+// so the shell returns as the "Finished" line prints.
+int g_report_fd = -1;
+
+void report_and_exit(int code) {
+    std::fflush(stdout);
+    std::fflush(stderr);
+    if (g_report_fd >= 0) {
+        ::close(1);  // (exit tears memory down before it closes files: tee would wait for the teardown)
+        ::close(2);
+        unsigned char c = (unsigned char)code;
+        io_all(g_report_fd, &c, 1, true);
+        ::close(g_report_fd);
+    }
+    std::_Exit(code);
+}
+
+int run_detached(const rmc_config &cfg, const std::function<int(const rmc_config &)> &body) {
+    std::fflush(stdout);
+    std::fflush(stderr);
+    int pp[2];
+    if (::pipe(pp) != 0) return body(cfg);
+    const pid_t k = ::fork();
+    if (k < 0) {
+        ::close(pp[0]);
+        ::close(pp[1]);
+        return body(cfg);  // no worker: run here
+    }
+    if (k == 0) {
+        ::close(pp[0]);
+        g_report_fd = pp[1];
+        report_and_exit(body(cfg));
+    }
+    ::close(pp[1]);
+    unsigned char c = 0;
+    const bool got = io_all(pp[0], &c, 1, false);
+    ::close(pp[0]);
+    if (got) return c;  // the worker's teardown goes on without us
+    int st = 0;  // the worker ended without reporting (a crash): its status
+    if (::waitpid(k, &st, 0) < 0) return 75;
+    return WIFEXITED(st) ? WEXITSTATUS(st) : 75;
+}
+
 }  // namespace
 
 // RMC_LAUNCHER_TIMES=1: seconds since process start at each phase, on stderr (stdout stays TLC's)
@@ -580,12 +627,14 @@ int main(int argc, char **argv) {
     std::fflush(stdout);
     std::fflush(stderr);
     const char *fe = std::getenv("RMC_FAST_EXIT");
-    if (!(fe && std::string(fe) == "0")) std::_Exit(exit_code);
+    if (!(fe && std::string(fe) == "0")) report_and_exit(exit_code);
     phase_time("destroy");
     rmc_destroy(ctx);
     phase_time("destroyed");
     return exit_code;
     };
     if (gpus > 1 || onerank) return run_ranks(gpus, onerank, cfg, check);
-    return check(cfg);
+    const char *det = std::getenv("RMC_DETACH");  // RMC_DETACH=0: one process, exit after the teardown
+    if (det && std::string(det) == "0") return check(cfg);
+    return run_detached(cfg, check);
 }

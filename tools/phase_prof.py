@@ -35,7 +35,13 @@ ap.add_argument("E", type=int)
 ap.add_argument("R", type=int)
 ap.add_argument("--levels", type=int, default=1000)
 ap.add_argument("--device-levels", type=int, default=0)
+ap.add_argument("--items", action="store_true", help="split chunks expand with k_expand_items: its phases in slots 0-6")
 a = ap.parse_args()
+if a.items:
+    NAMES[:8] = ["items: record offsets + copy into LDS", "items: decode cores, message scan",
+                 "items: message pass (hash sums, votes, classes)", "items: hash context write, item scan",
+                 "items: class lists + evaluate (action, key list)", "items: ranks + staging",
+                 "items: per-parent counts, error keys, round sync", "-"]
 cfg = raftmc.ModelConfig(n_servers=a.n, n_vals=a.V, max_election=a.E, max_restart=a.R, device_levels=a.device_levels)
 mc = raftmc.ModelChecker(cfg)
 lib = raftmc.load_library()
