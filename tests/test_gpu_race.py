@@ -78,8 +78,11 @@ def test_forced_schedules_keep_golden_results(tmp_path):
 
 def test_single_control_block_fails_under_the_forced_late_block(tmp_path):
     """The logic before the pair (one control block per level, read and advanced in place) with the
-    late commit block forced: configs[1] (3 servers, 1 value, MaxElection 2) must not reproduce its
-    golden levels -- the probe does reach the schedule that broke round 4's device loop."""
+    late commit block forced: configs[1] (3 servers, 1 value, MaxElection 2) must fail -- the late block
+    takes the next level's parent count, arrives at the next level's counters and leaves them off by
+    one (the probe build checks that every counter has re-armed itself when a level finishes; a
+    violation found at that level could otherwise go to the wrong level's summary, round 4's symptom)."""
     g = LEVELS["n3_v1_e2_r3"]
     res = run_worker(1, [{"name": "n3_v1_e2_r3", "cfg": cfg_of(g)}], tmp_path)
     assert not matches(g, res[0], "n3_v1_e2_r3"), "the forced late block went unnoticed"
+    assert "arrival counters" in res[0].get("error", ""), res[0]

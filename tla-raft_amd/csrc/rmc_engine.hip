@@ -403,6 +403,7 @@ struct Shard {
     std::vector<uint64_t> level_start;  // local gid of the first state of each level
     // chunk buffers (source side)
     uint32_t *cnt = nullptr, *lslot = nullptr, *wpos = nullptr;
+    uint32_t *hcnt = nullptr;   // split chunks: successors per parent to fingerprint (KParams::hcnt)
     ulonglong2 *fp = nullptr;
     unsigned long long *L = nullptr;
     ulonglong2 *LXY = nullptr;  // fused path: fingerprint of each election slot (tagged)
@@ -967,6 +968,7 @@ struct rmc_ctx {
         s.wcnt = dmalloc<uint32_t>(chunk_parents + 1);
         s.wacc = dmalloc<uint32_t>(chunk_parents + 1);
         s.pnm = dmalloc<uint32_t>(chunk_parents + 1);
+        s.hcnt = dmalloc<uint32_t>(chunk_parents + 1);
         s.wposw = dmalloc<uint32_t>(chunk_parents + 1);
         s.ctick = dmalloc<uint32_t>(33 * 32);
         HIPCHK(hipMemsetAsync(s.ctick, 0, 33 * 32 * 4, stream));
@@ -1020,7 +1022,7 @@ struct rmc_ctx {
         dfree(s.OT); dfree(s.OK); dfree(s.ob); dfree(s.ib); dfree(s.oside); dfree(s.iside); dfree(s.ooff);
         dfree(s.isz); dfree(s.ioff);
         dfree(s.err); dfree(s.sum); dfree(s.flags);
-        dfree(s.score); dfree(s.wcnt); dfree(s.wacc); dfree(s.pnm); dfree(s.wposw); dfree(s.ctick);
+        dfree(s.score); dfree(s.wcnt); dfree(s.wacc); dfree(s.pnm); dfree(s.hcnt); dfree(s.wposw); dfree(s.ctick);
         dfree(s.bw); dfree(s.bg); dfree(s.boff); dfree(s.bww); dfree(s.boffw); dfree(s.tickets);
         dfree(s.bn); dfree(s.boffn); dfree(s.plist); dfree(s.hctx);
         dfree(s.ctl); dfree(s.lrec);
@@ -1853,6 +1855,14 @@ struct rmc_ctx {
 
     // First error in TLC order among the error slots: smaller (parent, slot) first; on a
     // tie the Assert wins (its sub-action's batch is discarded).
+    // the chunk summary's flag word (KParams::flags[0]): what stopped the level
+    std::string flag_msg(unsigned long long f) const {
+        if (f & 1u) return "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages";
+        if (f & 2u) return "internal: a split chunk's parent records are not consecutive in the frontier ring";
+        if (f & 4u) return "race probe: the commit's arrival counters were not all re-armed when the level finished";
+        return "internal: unknown flag " + std::to_string(f);
+    }
+
     static int first_error(const unsigned long long *e, unsigned long long *best) {
         int kind = -1;
         *best = ~0ull;
@@ -1927,6 +1937,8 @@ struct rmc_ctx {
                 Q.epoch = s.epoch;
                 Q.split = split ? (split_insert ? split_flags : 1) : 0;
                 Q.plist = split && nzlist ? s.plist : nullptr;
+                // (a split chunk's self-loops are staged after the successors to fingerprint)
+                Q.hcnt = split && split_insert && split_flags == 7 && nzlist ? s.hcnt : nullptr;
                 return Q;
             };
             // expand + fingerprint + seen-set probe + staging, one evaluation per parent (a split
@@ -1963,7 +1975,7 @@ struct rmc_ctx {
             HIPCHK(hipGetLastError());
             collect_times(st);
             const uint64_t G = s.hsum[0], Wn = s.hsum[1], Ww = s.hsum[SUM_WORDS];
-            if (s.hsum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
+            if (s.hsum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, flag_msg(s.hsum[2 + ERR_NSLOTS]));
             flush_trace(s, gid_nxt + s.nxt_n + Wn);
             level_gen += G;
             s.T_count += Wn;
@@ -2230,7 +2242,7 @@ struct rmc_ctx {
             // the level the loop stopped in is intact: report its error as the host path does
             rmc_level_stats *st = &out[D];
             st->seconds = el / nst;
-            if (s.hsum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages");
+            if (s.hsum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, flag_msg(s.hsum[2 + ERR_NSLOTS]));
             const int L = (int)s.level_start.size();
             st->level = L;
             st->expanded = s.cur_n;
@@ -2658,7 +2670,7 @@ struct rmc_ctx {
                 HIPCHK(hipGetLastError());
                 if (s.hsum[2 + ERR_NSLOTS] && !fail[li]) {
                     fail[li] = RMC_E_CAPACITY;
-                    fail_msg = "a state exceeds msg_cap = " + std::to_string(ks.MCAP) + " messages";
+                    fail_msg = flag_msg(s.hsum[2 + ERR_NSLOTS]);
                 }
                 uint64_t *row = &tab[TAB * s.id];
                 row[1] = wnum[li];

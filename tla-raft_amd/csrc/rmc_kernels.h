@@ -88,6 +88,11 @@ struct KParams {
     uint64_t p_begin, p_end;   // parents of this chunk (level-local indices)
     // per parent (chunk-local: index p - p_begin)
     uint32_t *cnt;             // successor counts
+    // split chunk (single GPU): successors per parent that need a fingerprint -- the expansion stages a
+    // parent's self-loops (a successor equal to it: FollowerAcceptEntry of an entry it holds, already in
+    // the seen set with the parent) after them, and every later pass of the chunk visits hcnt[pl] slots
+    // only; nullptr: cnt (every successor)
+    uint32_t *hcnt;
     const uint32_t *off;       // exclusive scan of cnt (chunk-local successor index)
     // per successor (chunk-local index j)
     ulonglong2 *fp;

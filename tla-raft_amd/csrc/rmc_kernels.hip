@@ -1495,6 +1495,7 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
         }
         if (MODE != M_SINGLE && lane == 0) {
             P.cnt[pl] = total;
+            if (MODE == M_SPLIT && P.hcnt) P.hcnt[pl] = total;  // (no self-loops set apart here)
             P.pnm[pl] = W.nm;
             if (total == 0 && !am && P.check_deadlock) atomicMin(&P.err[ERR_DEADLOCK], ((unsigned long long)p << 16) << 8);
         }
@@ -1759,6 +1760,7 @@ struct RowSucc {
     uint32_t key;  // KEY_NONE: disabled
     uint32_t nadd;
     uint32_t add[NADD];
+    bool self;     // the successor is the parent itself (FollowerAcceptEntry changing nothing)
 };
 
 template <int NADD>
@@ -1777,9 +1779,8 @@ __device__ __forceinline__ void row_stage(const RowSucc<NADD> &o, uint32_t nm, i
 // s = m.dst; pid is the id of the one message the action may send (looked up before any branch).
 template <int N, int V, int MR, bool BFV>
 __device__ __forceinline__ void item_msg(const KParams &P, const uint32_t *pc, const uint16_t *ids, uint32_t nm,
-                                         uint32_t k, uint32_t m, uint32_t pid, bool pres, RowSucc<Spec<N, V, MR>::NADD> &o,
+                                         uint32_t k, uint32_t m, uint32_t pid, RowSucc<Spec<N, V, MR>::NADD> &o,
                                          RowSucc<Spec<N, V, MR>::NADD> &ob, uint32_t &akey) {
-    // pres: pid \in msgs (the parent's), found by the message pass
     using Lo = Layout<N, V>;
     using S = Spec<N, V, MR>;
     const uint32_t s = mi_dst(m), typ = mi_type(m), mt = mi_term(m), src = mi_src(m);
@@ -1789,6 +1790,7 @@ __device__ __forceinline__ void item_msg(const KParams &P, const uint32_t *pc, c
     const uint32_t pend = pc[Lo::W_PEND], misc = pc[Lo::W_MISC];
     o.key = KEY_NONE;
     o.nadd = 0;
+    o.self = false;
 #pragma unroll
     for (int a = 0; a < S::NADD; a++) o.add[a] = 0;
     o.lw = lw; o.mirow = mirow; o.nirow = nirow; o.pend = pend; o.misc = misc;
@@ -1820,7 +1822,7 @@ __device__ __forceinline__ void item_msg(const KParams &P, const uint32_t *pc, c
         if (!(vf == VF_NONE || vf == src)) return;
         const uint32_t llt = lw_term(lw, ll), mlli = mi_x1(m), mllt = mi_x2(m);
         if (!(mllt > llt || (mllt == llt && mlli >= ll))) return;
-        if (pres) return;
+        if (ids_contain<S::MCAP>(ids, nm, pid)) return;
         o.w0 = row_w0(src, ct, role, ci, ll, s);
         o.add[0] = pid; o.nadd = 1;
         o.key = slot_key(s, RV, k);
@@ -1846,10 +1848,13 @@ __device__ __forceinline__ void item_msg(const KParams &P, const uint32_t *pc, c
                 nll = nl;
             }
             o.w0 = row_w0(vf, ct, role, nci, nll, s);
-            if (!pres) { o.add[0] = pid; o.nadd = 1; }
+            const bool has = ids_contain<S::MCAP>(ids, nm, pid);
+            if (!has) { o.add[0] = pid; o.nadd = 1; }
+            // (no new entry, no truncation, no commit, the response already sent: the parent itself)
+            o.self = has && !(truncated || append_new) && nci == ci;
             o.key = slot_key(s, FAE, k);
         } else {
-            if (pres) return;
+            if (ids_contain<S::MCAP>(ids, nm, pid)) return;
             o.add[0] = pid; o.nadd = 1;
             o.key = slot_key(s, FRE, k);
         }
@@ -1905,6 +1910,7 @@ __device__ __forceinline__ void item_slot(const KParams &P, const uint32_t *pc, 
     const uint32_t pend = pc[Lo::W_PEND], misc = pc[Lo::W_MISC];
     o.key = KEY_NONE;
     o.nadd = 0;
+    o.self = false;
 #pragma unroll
     for (int a = 0; a < S::NADD; a++) o.add[a] = 0;
     o.lw = lw; o.mirow = mirow; o.nirow = nirow; o.pend = pend; o.misc = misc;
@@ -2052,14 +2058,14 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
     static_assert(S::MCAP <= 128 && PB <= 64, "item codes: parent << 8 | slot bit << 7 | message index or s << 4 | t");
     __shared__ uint32_t sRec[PB * RECW];           // the batch's records, as in the ring
     __shared__ uint32_t sCore[PB * NWP];           // their nibble cores
-    // per message of the batch: parent | class << 8 | (the id its action may send \in msgs) << 12 | that id << 16
-    __shared__ uint32_t sMI[PB * S::MCAP];
+    __shared__ uint8_t sMI[PB * S::MCAP];          // per message of the batch: its class (15: none)
     __shared__ uint32_t sVp[PB * N];               // per parent and server: VoteResps to it in its term (tla:160-164)
     __shared__ uint32_t sOff[PB];                  // record's first word in sRec
     __shared__ uint32_t sItm[PB + 1], sMsc[PB + 1];  // items / messages: exclusive scans over the batch
     __shared__ uint32_t sLive[PB];                 // per parent: messages some action may receive
     __shared__ unsigned long long sSlot[PB];       // slot_range per server, 8 bits each
-    __shared__ uint32_t sCnt[PB], sAk[PB];         // enabled successors, smallest Assert key
+    __shared__ uint32_t sCnt[PB], sAk[PB];         // enabled successors (self-loops apart), smallest Assert key
+    __shared__ uint32_t sSelf[PB];                 // self-loops (P.hcnt: staged nowhere, never fingerprinted)
     __shared__ uint32_t sCc[IC_N];                 // the round's items per class
     // the batch's hash sums (until the hash context is written), then the rounds' item lists and keys
     constexpr int UM = 2 * PB * NPR * 8, UQ = IC_N * NT * 2 + NT * NCI * 2;
@@ -2120,6 +2126,7 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
 #pragma unroll
                 for (int k = 0; k < NPR; k++) { sM0[tid * NPR + k] = 0ull; sM1[tid * NPR + k] = 0ull; }
                 sCnt[tid] = 0u;
+                sSelf[tid] = 0u;
                 sAk[tid] = KEY_NONE;
                 sLive[tid] = 0u;
             }
@@ -2148,15 +2155,7 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
             const uint32_t ct = nib(pc[Lo::W_CT], dst);
             if (mi_type(inf) == VRESP && mi_term(inf) == ct) atomicAdd(&sVp[j * N + dst], 1u);
             const uint32_t c = msg_class(inf, ct, nib(pc[Lo::W_ROLE], dst));
-            // ResponseVote's VoteResp / Follower{Accept,Reject}Entry's AppendResp: its id and whether the
-            // parent holds it (m \notin msgs, tla:144,296,318), here where the parent's ids are at hand
-            uint32_t e = j | ((c == IC_DEAD ? 15u : c) << 8);
-            if (c == IC_RV || c == IC_AE) {
-                const uint32_t pid = P.t.nat2id[item_msg_nat<N, V>(P, pc, inf)];
-                const uint16_t *ids = reinterpret_cast<const uint16_t *>(sRec + sOff[j] + CCW);
-                e |= (ids_contain<S::MCAP>(ids, sMsc[j + 1] - sMsc[j], pid) ? 1u << 12 : 0u) | (pid << 16);
-            }
-            sMI[m] = e;
+            sMI[m] = (uint8_t)(c == IC_DEAD ? 15u : c);
             if (c != IC_DEAD) atomicAdd(&sLive[j], 1u);
         }
         __syncthreads();
@@ -2201,9 +2200,11 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
             const uint32_t nI = sItm[b] - ibase;
             // the round's items into their class lists: live messages, then each parent's slots
             for (uint32_t m = sMsc[a] + (uint32_t)tid; m < sMsc[b]; m += NT) {
-                const uint32_t e = sMI[m], c = (e >> 8) & 15u;
+                const uint32_t c = sMI[m];
                 if (c == 15u) continue;
-                const uint32_t j = e & 0xFFu;
+                uint32_t j = a;  // the last parent j with sMsc[j] <= m
+#pragma unroll
+                for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < b && sMsc[j + st] <= m) ? j + st : j;
                 sQ[c * NT + atomicAdd(&sCc[c], 1u)] = (uint16_t)((j << 8) | (m - sMsc[j]));
             }
             for (uint32_t q = (uint32_t)tid; q < (b - a) * (uint32_t)N; q += NT) {  // a lane per (parent, server)
@@ -2235,15 +2236,18 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
                 uint32_t akey = KEY_NONE;
                 if (!(code & 0x80u)) {
                     const uint32_t k = code & 0x7Fu;
-                    const uint32_t inf = P.t.info[ids[k]], e = sMI[sMsc[j] + k];
-                    item_msg<N, V, MR, BFV>(P, pc, ids, nmj, k, inf, e >> 16, (e >> 12) & 1u, o, ob, akey);
+                    const uint32_t inf = P.t.info[ids[k]];
+                    const uint32_t nat = item_msg_nat<N, V>(P, pc, inf);
+                    const uint32_t pid = nat != NAT_NONE ? (uint32_t)P.t.nat2id[nat] : 0u;
+                    item_msg<N, V, MR, BFV>(P, pc, ids, nmj, k, inf, pid, o, ob, akey);
                 } else {
                     const uint32_t s = (code >> 4) & 7u, t = code & 15u;
                     item_slot<N, V, MR>(P, pc, ids, nmj, sVp[j * N + s], s, t, o);
                 }
                 if (akey != KEY_NONE) atomicMin(&sAk[j], akey);
                 const uint32_t kb = (sItm[j] - ibase) * NCI;  // the parent's key list
-                if (o.key != KEY_NONE) sKey[kb + atomicAdd(&sCnt[j], 1u)] = (uint16_t)o.key;
+                if (o.key != KEY_NONE && o.self && P.hcnt) atomicAdd(&sSelf[j], 1u);
+                else if (o.key != KEY_NONE) sKey[kb + atomicAdd(&sCnt[j], 1u)] = (uint16_t)o.key;
                 if (BFV && ob.key != KEY_NONE) sKey[kb + atomicAdd(&sCnt[j], 1u)] = (uint16_t)ob.key;
                 if ((o.key != KEY_NONE && nmj + o.nadd > (uint32_t)S::MCAP)) atomicOr(&P.flags[0], 1u);
             }
@@ -2255,7 +2259,7 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
 #pragma unroll
                 for (int c = 0; c < NCI; c++) {
                     const RowSucc<S::NADD> &x = c ? ob : o;
-                    if (x.key == KEY_NONE) continue;
+                    if (x.key == KEY_NONE || (x.self && P.hcnt)) continue;
                     uint32_t rank = 0;
                     for (uint32_t e = 0; e < cn; e++) rank += (uint32_t)sKey[kb + e] < x.key ? 1u : 0u;
                     row_stage<S::NADD>(x, nmj, S::SW4, P.score + (pl * (uint64_t)MX + rank) * (uint64_t)S::SW4);
@@ -2266,8 +2270,9 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
             if ((uint32_t)tid < b - a) {
                 const uint32_t jj = a + (uint32_t)tid;
                 const uint64_t pl = b0 + jj, p = P.p_begin + pl;
-                const uint32_t total = sCnt[jj], ak = sAk[jj];
+                const uint32_t total = sCnt[jj] + sSelf[jj], ak = sAk[jj];
                 P.cnt[pl] = total;
+                if (P.hcnt) P.hcnt[pl] = sCnt[jj];
                 P.pnm[pl] = (sCore[jj * NWP + Lo::W_MISC] >> 16) & 0xFFu;
                 if (ak != KEY_NONE) atomicMin(&P.err[ERR_ASSERT], (((unsigned long long)p << 16) | ak) << 8);
                 else if (total == 0 && P.check_deadlock)
@@ -2293,7 +2298,7 @@ __device__ __forceinline__ void each_successor(const KParams &P, F &&f) {
     for (uint64_t g0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; g0 < np;
          g0 += nwaves * 64) {
         const uint64_t pl = g0 + (uint64_t)lane;
-        const uint32_t t = pl < np ? P.cnt[pl] : 0u;
+        const uint32_t t = pl < np ? (P.hcnt ? P.hcnt : P.cnt)[pl] : 0u;  // (a split chunk: its self-loops are not visited)
         uint32_t tot;
         const uint32_t ex = wave_excl_scan(t, lane, &tot);
         for (uint32_t b0 = 0; b0 < tot; b0 += 64) {
@@ -2693,6 +2698,9 @@ __global__ __launch_bounds__(1024) void k_nzlist(KParams P) {
     }
 }
 
+// the commit's arrival counters (last_commit_block): CTICK_SUB sub-counters and a top one, each on its own line
+constexpr uint32_t CTICK_SUB = 32, CTICK_STRIDE = 32;
+
 // Chunk summary, by the last block of the commit pass (one wave): {generated, winners, words} (from the
 // winner count pass), the error keys and flags (then re-armed).  In device-loop mode it also
 // records the level and advances the control block to the next one -- or stops the loop.
@@ -2706,6 +2714,17 @@ __device__ void finish_level(const KParams &P) {
     unsigned long long *sm = P.sum;
     unsigned long long G = 0, Wn = 0, Ww = 0;
     LevelCtl c{};
+#ifdef RMC_RACE_PROBE
+    // when the last arriver gets here every block of the launch has arrived and every counter has
+    // re-armed itself (a sub-counter's last re-arms it before it arrives at the top one): a counter
+    // left off by an arrival from another level (the late-block race) shows here
+    if (lane == 0 && P.ctick) {
+        uint32_t off = 0;
+        for (uint32_t i = 0; i <= CTICK_SUB; i++)
+            off |= __hip_atomic_load(P.ctick + i * CTICK_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (off) atomicOr(&P.flags[0], 4u);
+    }
+#endif
     if (lane == 0) {
         G = sm[0];
         Wn = sm[1];
@@ -2785,7 +2804,6 @@ __device__ void finish_level(const KParams &P) {
 // no counter sees more than nb / CTICK_SUB atomics.  No fence: the last
 // block reads nothing that this launch wrote except the error words, and those are atomics that
 // every wave has completed (vmcnt(0)) before its arrival.  Counters re-arm themselves.
-constexpr uint32_t CTICK_SUB = 32, CTICK_STRIDE = 32;
 __device__ __forceinline__ bool last_commit_block(uint32_t *tick, uint32_t nb) {
     if (blockIdx.x >= nb) return false;
 #ifdef RMC_RACE_PROBE
@@ -3047,7 +3065,7 @@ __global__ __launch_bounds__(256) void k_commit_split(KParams P) {
          g0 += nwaves * 64) {
         const uint64_t k = g0 + (uint64_t)lane;
         const uint32_t pl_l = k < nvis ? P.plist[k] : 0u;  // this lane's parent with winners (chunk-local)
-        const uint32_t t = k < nvis ? P.cnt[pl_l] : 0u;
+        const uint32_t t = k < nvis ? (P.hcnt ? P.hcnt : P.cnt)[pl_l] : 0u;
         uint32_t tot;
         const uint32_t ex = wave_excl_scan(t, lane, &tot);
         uint32_t cw = 0, cs = 0;  // winners / record words the previous round gave the group's parent cj
@@ -3169,6 +3187,183 @@ __global__ __launch_bounds__(256) void k_commit_split(KParams P) {
     }
 }
 
+// ---- split chunk / sharded round commit, records staged in LDS ------------------------------------
+// k_commit_split gives each winner a lane but leaves it a chain of dependent global loads: its parent's
+// record offset, then the core words, then -- one load per two ids -- the parent's message ids while it
+// merges them with the ids its action added.  Here a 256-thread block takes 64 parents with winners
+// (plist) at a time and copies their records into LDS first (a lane per record word); then, in rounds
+// of whole parents of at most 256 successor slots, a lane per slot finds the winners (lslot == LS_WIN),
+// stages each one's row in LDS and lists it on its parent, and a lane per winner -- dense, whatever the
+// parents' successor counts -- takes its ordinal and word offset among its parent's winners from that
+// list (TLC order = slot order), rebuilds the state from the LDS core, writes the record (core, then the
+// parent's ids merged with the added ones, read from LDS), its trace entry (or sidecar) and checks the
+// INVARIANTs.  Outputs are k_commit_split's, bit for bit; k_commit_finish follows.
+template <int N, int V, int MR, int MX>
+__global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
+    using S = Spec<N, V, MR>;
+    using Lo = Layout<N, V>;
+    constexpr int PB = 64, NT = XB_THREADS, CCW = S::CCW, RECW = S::RECW_MAX, SW4 = S::SW4;
+    static_assert(MX <= NT, "a parent's successor slots fit one round");
+    __shared__ uint32_t sRec[PB * RECW];        // the batch's parent records
+    __shared__ uint32_t sOff[PB + 1];           // record offsets in sRec (exclusive scan of record words)
+    __shared__ uint32_t sSl[PB + 1];            // successor slots: exclusive scan of cnt
+    __shared__ uint32_t sPl[PB];                // chunk-local parent index
+    __shared__ uint32_t sOut[PB];               // next-level index of the parent's first winner (chunk-relative)
+    __shared__ uint32_t sWd[PB];                // ... and its record's first word (chunk-relative)
+    __shared__ uint32_t sWc[PB];                // the round's winners per parent
+    __shared__ uint32_t sWl[NT];                // per parent at its slots' round offset: (slot << 16) | record words
+    __shared__ uint4 sSt[NT * SW4];             // the round's winners' staged rows, dense
+    __shared__ uint32_t sWr[NT];                // ... and each one's parent | slot << 8
+    __shared__ uint32_t sNW;
+    const int tid = threadIdx.x;
+    const uint64_t nvis = P.sum[SUM_NZ];
+    for (uint64_t k0 = (uint64_t)blockIdx.x * PB; k0 < nvis; k0 += (uint64_t)gridDim.x * PB) {
+        const uint32_t nb = (uint32_t)(nvis - k0 < (uint64_t)PB ? nvis - k0 : (uint64_t)PB);
+        if (tid < 64) {  // wave 0: a lane per parent with winners
+            uint32_t t = 0, words = 0;
+            if ((uint32_t)tid < nb) {
+                const uint32_t pl = P.plist[k0 + tid];
+                const uint32_t tile = pl / WTILE;
+                t = (P.hcnt ? P.hcnt : P.cnt)[pl];  // (self-loops never win)
+                words = (uint32_t)CCW + ((P.pnm[pl] + 1u) >> 1);
+                sPl[tid] = pl;
+                sOut[tid] = P.boff[tile] + P.wpos[pl];
+                sWd[tid] = P.boffw[tile] + P.wposw[pl];
+                sWc[tid] = 0u;
+            }
+            uint32_t ts, tw;
+            const uint32_t xs = wave_excl_scan(t, tid, &ts), xw = wave_excl_scan(words, tid, &tw);
+            if ((uint32_t)tid < nb) { sSl[tid] = xs; sOff[tid] = xw; }
+            if (tid == 0) { sSl[nb] = ts; sOff[nb] = tw; sNW = 0u; }
+        }
+        __syncthreads();
+        // the records, a lane per word
+        for (uint32_t w = (uint32_t)tid; w < sOff[nb]; w += NT) {
+            uint32_t j = 0;
+#pragma unroll
+            for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < nb && sOff[j + st] <= w) ? j + st : j;
+            const uint64_t start = ring_wrap(P.fbase + P.foff[P.p_begin + sPl[j]], P.rcap);
+            sRec[w] = ring_word(P.front, start, w - sOff[j], P.rcap);
+        }
+        __syncthreads();
+        for (uint32_t a = 0; a < nb;) {
+            const uint32_t sbase = sSl[a];
+            uint32_t b = a;  // parents a .. b - 1: at most NT slots
+#pragma unroll
+            for (uint32_t st = PB; st; st >>= 1) b = (b + st <= nb && sSl[b + st] <= sbase + NT) ? b + st : b;
+            const uint32_t nS = sSl[b] - sbase;
+            // (a) a lane per slot: the winners, staged and listed on their parent
+            if ((uint32_t)tid < nS) {
+                const uint32_t i = sbase + (uint32_t)tid;
+                uint32_t j = a;
+#pragma unroll
+                for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < b && sSl[j + st] <= i) ? j + st : j;
+                const uint32_t r = i - sSl[j];
+                const uint64_t q = (uint64_t)sPl[j] * MX + r;
+                if (P.lslot[q] == LS_WIN) {
+                    const uint4 *src = P.score + q * (uint64_t)SW4;
+                    uint4 st4[SW4];
+#pragma unroll
+                    for (int x = 0; x < SW4; x++) st4[x] = src[x];
+                    const uint32_t w = atomicAdd(&sNW, 1u);
+#pragma unroll
+                    for (int x = 0; x < SW4; x++) sSt[w * SW4 + x] = st4[x];
+                    sWr[w] = j | (r << 8);
+                    const uint32_t words = (uint32_t)CCW + ((P.pnm[sPl[j]] + (st4[1].z >> 16) + 1u) >> 1);
+                    sWl[(sSl[j] - sbase) + atomicAdd(&sWc[j], 1u)] = (r << 16) | words;
+                }
+            }
+            __syncthreads();
+            // (b) a lane per winner
+            if ((uint32_t)tid < sNW) {
+                const uint32_t e = sWr[tid], j = e & 0xFFu, r = e >> 8;
+                const uint32_t lb = sSl[j] - sbase, wc = sWc[j];
+                uint32_t ord = 0, wofs = 0;
+                for (uint32_t x = 0; x < wc; x++) {
+                    const uint32_t l = sWl[lb + x];
+                    if ((l >> 16) < r) { ord++; wofs += l & 0xFFFFu; }
+                }
+                const uint4 sa = sSt[tid * SW4], sb = sSt[tid * SW4 + 1];
+                const uint4 sc = SW4 > 2 ? sSt[tid * SW4 + 2] : make_uint4(0u, 0u, 0u, 0u);
+                const uint32_t *rec = sRec + sOff[j];
+                uint32_t pk[CCW], pc[Lo::NW], c[Lo::NW];
+#pragma unroll
+                for (int w = 0; w < CCW; w++) pk[w] = rec[w];
+                decode_core<N, V>(pk, pc);
+                unstage_core<N, V>(pc, sa, sb, c);
+                encode_core<N, V>(c, pk);
+                const uint32_t nm = (pc[Lo::W_MISC] >> 16) & 0xFFu, nadd = sb.z >> 16;
+                const uint32_t size = (uint32_t)CCW + ((nm + nadd + 1u) >> 1);
+                const uint32_t pl = sPl[j];
+                const uint64_t p = P.p_begin + pl;
+                const uint64_t out = P.next_base + sOut[j] + ord;
+                const uint64_t wd = P.next_wbase + sWd[j] + wofs;  // level-relative
+                const uint64_t rs = ring_wrap(P.nbase + wd, P.rcap);
+                P.noff[out] = wd;
+#pragma unroll
+                for (int w = 0; w < CCW; w++) P.next[ring_wrap(rs + (uint32_t)w, P.rcap)] = pk[w];
+                // the parent's sorted ids (LDS) merged with the added ones (sorted here: BecomeCandidate
+                // adds its VoteReqs in peer order), written a word at a time, the last half-word padded
+                uint32_t add[4] = {sb.w & 0xFFFFu, sb.w >> 16, sc.x & 0xFFFFu, sc.x >> 16};
+#pragma unroll
+                for (int x = 0; x < S::NADD; x++)
+#pragma unroll
+                    for (int y = 0; y + 1 < S::NADD - x; y++)
+                        if ((uint32_t)(y + 1) < nadd && add[y + 1] < add[y]) {
+                            const uint32_t t = add[y];
+                            add[y] = add[y + 1];
+                            add[y + 1] = t;
+                        }
+                const uint16_t *pid = reinterpret_cast<const uint16_t *>(rec + CCW);
+                const uint64_t oid = ring_wrap(rs + CCW, P.rcap);
+                uint32_t kk = 0, ai = 0, word = 0;
+                const uint32_t tot_ids = nm + nadd;
+                for (uint32_t o = 0; o < tot_ids; o++) {
+                    uint32_t next_add = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int y = 0; y < S::NADD; y++) next_add = (uint32_t)y == ai ? add[y] : next_add;
+                    const uint32_t pv = kk < nm ? (uint32_t)pid[kk] : 0xFFFFFFFFu;
+                    uint32_t id;
+                    if (ai < nadd && next_add < pv) {
+                        id = next_add;
+                        ai++;
+                    } else {
+                        id = pv;
+                        kk++;
+                    }
+                    if (o & 1u) P.next[ring_wrap(oid + (o >> 1), P.rcap)] = word | (id << 16);
+                    else word = id;
+                }
+                if (tot_ids & 1u) P.next[ring_wrap(oid + (tot_ids >> 1), P.rcap)] = word;
+                const uint32_t key = sb.z & 0xFFFFu;
+                if (P.route) {
+                    // sharded round: the trace entry travels with the record to the state's next-level owner
+                    const uint64_t pref = P.gid_parent_base + p;
+                    P.xside[out] = make_uint4((uint32_t)pref, (uint32_t)(pref >> 32), key, size);
+                } else {
+                    const uint64_t gid = P.gid_next_base + out;
+                    P.par[gid - P.trace_base] = P.gid_parent_base + p;
+                    P.pslot[gid - P.trace_base] = (uint16_t)key;
+                }
+                int which = 0;
+                // (only NoAllCommit, tla:451-481, reads the message set: the ring's copy of the parent's ids)
+                const uint64_t mids = (P.inv_mask & 32u) ? ring_wrap(ring_wrap(P.fbase + P.foff[p], P.rcap) + CCW, P.rcap) : 0;
+                const MsgView mv{P.front, mids, P.rcap, nm, sb.w, sc.x, nadd, P.t.info};
+                const int iv = check_invs<N, V>(c, P.inv_order, &which, mv);
+                if (iv != 1) {
+                    const unsigned long long ek = ((((unsigned long long)p << 16) | key) << 8) | (unsigned long long)which;
+                    atomicMin(&P.err[iv == 0 ? ERR_INV : ERR_EVAL], ek);
+                }
+            }
+            __syncthreads();
+            if (tid == 0) sNW = 0u;
+            if ((uint32_t)tid < b - a) sWc[a + tid] = 0u;  // (parents of this round only: already zero beyond)
+            __syncthreads();
+            a = b;
+        }
+    }
+}
+
 // the chunk summary after k_commit_split (one wave): finish_level
 template <int MX, int RECW_MAX>
 __global__ __launch_bounds__(64) void k_commit_finish(KParams P) {
@@ -3230,6 +3425,15 @@ static bool split_items() {
     return on;
 }
 
+// split-chunk commits: records staged in LDS (k_commit_items; RMC_COMMIT_ITEMS=0: k_commit_split)
+static bool commit_items() {
+    static const bool on = [] {
+        const char *v = std::getenv("RMC_COMMIT_ITEMS");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 static inline unsigned grid_for(uint64_t n) {
     const uint64_t cap = 256ull * RMC_GRID_PER_CU;  // one-wave blocks per CU (default 32) on 256 CUs
     return (unsigned)(n < cap ? (n ? n : 1) : cap);
@@ -3275,6 +3479,15 @@ struct Launch {
     }
     static void commit_split(const KParams &P, uint64_t np, hipStream_t s) {
         const uint64_t blocks = (np + 255) / 256;  // a wave per 64 parents with winners (at most np of them)
+        if constexpr (MX <= XB_THREADS) {
+            if (commit_items()) {  // a block per 64 parents with winners, records in LDS
+                const uint64_t nbat = (np + 63) / 64;
+                hipLaunchKernelGGL((k_commit_items<N, V, MR, MX>), dim3((unsigned)(nbat < 2048 ? (nbat ? nbat : 1) : 2048)),
+                                   dim3(XB_THREADS), 0, s, P);
+                hipLaunchKernelGGL((k_commit_finish<MX, Spec<N, V, MR>::RECW_MAX>), dim3(1), dim3(64), 0, s, P);
+                return;
+            }
+        }
         hipLaunchKernelGGL((k_commit_split<N, V, MR, MX>), dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u),
                            dim3(256), 0, s, P);
         hipLaunchKernelGGL((k_commit_finish<MX, Spec<N, V, MR>::RECW_MAX>), dim3(1), dim3(64), 0, s, P);

@@ -342,18 +342,24 @@ int run_ranks(int N, bool onerank, const rmc_config &base, const std::function<i
 // kernel's teardown of the worker (~110 GB of host trace and the device memory after a Raft.cfg
 // exhaustion: ~4 s) then runs after this process has returned TLC's exit code,
 // so the shell returns as the "Finished" line prints.
+// The worker then frees the device memory itself (hipFree: milliseconds) before
+// the host trace, so a GPU job started right after the shell returns finds the device free.
 int g_report_fd = -1;
 
-void report_and_exit(int code) {
+void report(int code) {  // (a no-op in the one-process mode)
     std::fflush(stdout);
     std::fflush(stderr);
-    if (g_report_fd >= 0) {
-        ::close(1);  // (exit tears memory down before it closes files: tee would wait for the teardown)
-        ::close(2);
-        unsigned char c = (unsigned char)code;
-        io_all(g_report_fd, &c, 1, true);
-        ::close(g_report_fd);
-    }
+    if (g_report_fd < 0) return;
+    ::close(1);  // (exit tears memory down before it closes files: tee would wait for the teardown)
+    ::close(2);
+    unsigned char c = (unsigned char)code;
+    io_all(g_report_fd, &c, 1, true);
+    ::close(g_report_fd);
+    g_report_fd = -1;
+}
+
+[[noreturn]] void report_and_exit(int code) {
+    report(code);
     std::_Exit(code);
 }
 
@@ -627,7 +633,13 @@ int main(int argc, char **argv) {
     std::fflush(stdout);
     std::fflush(stderr);
     const char *fe = std::getenv("RMC_FAST_EXIT");
-    if (!(fe && std::string(fe) == "0")) report_and_exit(exit_code);
+    if (!(fe && std::string(fe) == "0")) {
+        if (g_report_fd >= 0) {  // detached worker: the caller has its code; device memory goes first
+            report(exit_code);
+            rmc_destroy(ctx);
+        }
+        std::_Exit(exit_code);
+    }
     phase_time("destroy");
     rmc_destroy(ctx);
     phase_time("destroyed");
