@@ -55,23 +55,24 @@ TIMED_PHASES = 1 << PHASES.index("expand_hash")  # HIP-event timing of the domin
 TIMING_EVERY = 8
 
 
-def alg_bytes(phase, F, G, N, S, CCWB, slot_bytes=16, SWB=32, split=False, CTXB=112):
+def alg_bytes(phase, F, G, N, S, CCWB, slot_bytes=16, SWB=32, split=False, CTXB=112, Gself=0):
     """Algorithmic HBM bytes of one phase of the fused single-GPU level (DESIGN.md "Kernels"):
     F parents of S-byte records (S = the run's average packed record: CCWB core bytes + message
     ids), G generated successors, N new states; SWB = staging bytes per successor (the acting row),
     slot_bytes = seen-set slot (16 full, 8 compact), CTXB = a split chunk's hash context per parent
-    (ctx_bytes).  split: the host-driven chunk's expansion only stages (k_expand<SPLIT>); the
-    fingerprints, probe and election run in k_hash_probe ("probe")."""
-    if phase == "expand_hash" and split:  # k_expand<SPLIT>: parents in, count + |msgs| + hash context out,
-        # the staged rows out
-        return F * S + F * 8 + F * CTXB + G * SWB
+    (ctx_bytes).  split: the host-driven chunk's expansion only stages (k_expand_items); the
+    fingerprints, probe and election run in k_hash_probe ("probe").  Gself: of the G successors, the
+    self-loops a split chunk sets apart (rmc_level_stats.self_loops): never staged, fingerprinted or probed."""
+    if phase == "expand_hash" and split:  # k_expand_items: parents in, count + |msgs| + hash context out,
+        # the staged rows of the successors other than self-loops out
+        return F * S + F * 8 + F * CTXB + (G - Gself) * SWB
     if phase == "expand_hash":   # k_expand<FUSED>: parents in, count + |msgs| out; per successor: staged row +
         # fp + election slot, one seen-set probe; per new fingerprint at least one election (16-B slot, 8-B word, count)
         return F * S + F * 8 + G * (SWB + 16 + 4) + G * slot_bytes + N * (16 + 8 + 4)
     if phase == "probe":         # k_hash_probe: per parent its count and hash context; per successor its staged
         # row in, fingerprint + verdict out, one seen-set probe; per new fingerprint at least one election
         # (16-B slot, 8-B word, count)
-        return F * (4 + CTXB) + G * (SWB + 16 + 4) + G * slot_bytes + N * (16 + 8 + 4)
+        return F * (4 + CTXB) + (G - Gself) * (SWB + 16 + 4 + slot_bytes) + N * (16 + 8 + 4)
     if phase == "insert":        # k_insert_winners: per parent its count; per successor its slot word; per new
         # state its election word, fingerprint, seen-set insert and verdict
         return F * 4 + G * 4 + N * (8 + 16 + slot_bytes + 4)
@@ -619,7 +620,7 @@ def at_scale(device, workload="raftcfg", probes_per_s=None):
             f = min(cp, F - c0)
             alg += alg_bytes("expand_hash", f, ls.generated * f / F, ls.new_states * f / F, S, CCWB,
                              cold.seen_slot_bytes, staging_bytes(cfg), split=f >= (1 << 16),
-                             CTXB=ctx_bytes(w["n"], w["V"]))
+                             CTXB=ctx_bytes(w["n"], w["V"]), Gself=ls.self_loops * f / F)
     gbs = alg / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     gold = {}
     gpath = os.path.join(ROOT, "tests", "golden", "levels_prefix.json")
@@ -634,6 +635,8 @@ def at_scale(device, workload="raftcfg", probes_per_s=None):
             "depth": res.depth, "verdict": "Inv holds" if res.status == "done" else res.status,
             "seconds_to_exhaust": round(dt, 3), "distinct_per_s": round(res.distinct / dt, 1),
             "generated_per_s": round(res.generated / dt, 1),
+            "self_loops": sum(ls.self_loops for ls in res.levels),
+            "self_loop_frac": round(sum(ls.self_loops for ls in res.levels) / max(1, res.generated), 4),
             "first_run_seconds_incl_allocation": round(dt_cold, 3),
             "matches_c_oracle_prefix_levels": match, "c_oracle_prefix_levels": len(gold.get("levels", [])),
             "seen_set": f"{res.seen_slots} x {res.seen_slot_bytes} B slots",

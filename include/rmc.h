@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RMC_ABI_VERSION 4
+#define RMC_ABI_VERSION 5
 
 /* ---- return codes ---------------------------------------------------------- */
 #define RMC_OK 0
@@ -128,6 +128,9 @@ typedef struct rmc_level_stats {
     double kernel_ms[6];      /* expand-count, expand-hash, dedup, materialize, exchange, other */
     uint64_t kernel_launches[6];
     uint64_t new_bytes;       /* ABI 3: bytes of the new states' frontier records (packed core + message ids) */
+    uint64_t self_loops;      /* ABI 5: generated successors equal to their parent (FollowerAcceptEntry that
+                                 changes nothing), among `generated`, where the run set them apart (single-GPU
+                                 split chunks: never fingerprinted -- the parent is in the seen set); else 0 */
 } rmc_level_stats;
 
 /* Final result of a run: TLC's closing lines. */

@@ -57,7 +57,7 @@ def test_library_exports_every_declared_symbol():
     assert len(decl) >= 14
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.rmc_abi_version() == 4
+    assert lib.rmc_abi_version() == 5
 
 
 def test_parse_shipped_config_equivalent():

@@ -1903,7 +1903,7 @@ struct rmc_ctx {
         st->expanded = s.cur_n;
         const uint64_t gid_cur = s.level_start[L - 1];
         const uint64_t gid_nxt = gid_cur + s.cur_n;
-        uint64_t level_gen = 0;
+        uint64_t level_gen = 0, level_self = 0;
         s.nxt_n = 0;
         s.nxt_words = 0;
         const uint64_t MSW = (uint64_t)ks.maxsucc * (uint64_t)ks.RECW_MAX;
@@ -1948,6 +1948,7 @@ struct rmc_ctx {
                 else ks.fused(params(), stream);
             });
             if (split) timed(PH_OTHER, [&] { ks.hash_probe(params(), np_, stream); });
+            if (split) HIPCHK(hipMemsetAsync(s.sum + SUM_SELF, 0, 8, stream));
             timed(PH_DEDUP, [&] {
                 ks.wincount(params(), np_, stream);
                 if (split && nzlist) launch_nzlist(params(), np_, stream);
@@ -1970,11 +1971,12 @@ struct rmc_ctx {
                 if (split && nzlist && split_insert && split_flags == 7) ks.commit_split(params(), np_, stream);
                 else ks.commit(params(), stream);
             });
-            HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
+            HIPCHK(hipMemcpyAsync(s.hsum, s.sum, (SUM_SELF + 1) * 8, hipMemcpyDeviceToHost, stream));
             HIPCHK(hipStreamSynchronize(stream));
             HIPCHK(hipGetLastError());
             collect_times(st);
             const uint64_t G = s.hsum[0], Wn = s.hsum[1], Ww = s.hsum[SUM_WORDS];
+            if (split) level_self += s.hsum[SUM_SELF];
             if (s.hsum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, flag_msg(s.hsum[2 + ERR_NSLOTS]));
             flush_trace(s, gid_nxt + s.nxt_n + Wn);
             level_gen += G;
@@ -1994,6 +1996,7 @@ struct rmc_ctx {
         total_generated += level_gen;
         total_distinct += s.nxt_n;
         st->generated = level_gen;
+        st->self_loops = level_self;
         st->new_states = s.nxt_n;
         st->new_bytes = s.nxt_words * 4;
         end_level(s, gid_nxt, L);

@@ -69,6 +69,7 @@ constexpr uint32_t WTILE = 1024; // parents per tile of the winner-count scan
 constexpr uint32_t WTILES_MAX = 4096; // tiles per chunk (the last block scans four per thread)
 constexpr int SUM_WORDS = 7;     // chunk summary slot of the new states' record words
 constexpr int SUM_NZ = 16;       // ... and of the parents with winners (KParams::plist)
+constexpr int SUM_SELF = 17;     // ... and the self-loops set apart (KParams::hcnt; zeroed by the host per chunk)
 
 // In device-loop mode the host sizes every grid on a bound of the level's parents (p_end -
 // p_begin of the KParams it passes); the kernels read the real range from the LevelCtl.

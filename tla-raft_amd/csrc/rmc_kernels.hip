@@ -2587,6 +2587,11 @@ __global__ __launch_bounds__(1024) void k_wincount(KParams P) {
         }
         // parents with winners in the tile (for k_nzlist)
         const uint32_t nt = P.plist ? (uint32_t)__syncthreads_count(w != 0u) : 0u;
+        if (P.hcnt) {  // the tile's self-loops (set apart by the split expansion) for the level's statistics
+            uint32_t st;
+            (void)block_excl_scan(pl < np ? t - P.hcnt[pl] : 0u, ws, &st);
+            if (threadIdx.x == 0 && st) atomicAdd(&P.sum[SUM_SELF], (unsigned long long)st);
+        }
         if (ntiles == 1) {  // one tile (small levels): its totals are the chunk's, no arrival round trips
             if (threadIdx.x == 0) {
                 P.boff[0] = 0u;

@@ -62,7 +62,7 @@ class _LevelStats(ctypes.Structure):
         ("generated", ctypes.c_uint64), ("new_states", ctypes.c_uint64), ("total_generated", ctypes.c_uint64),
         ("total_distinct", ctypes.c_uint64), ("queue", ctypes.c_uint64), ("seconds", ctypes.c_double),
         ("kernel_ms", ctypes.c_double * 6), ("kernel_launches", ctypes.c_uint64 * 6),
-        ("new_bytes", ctypes.c_uint64),
+        ("new_bytes", ctypes.c_uint64), ("self_loops", ctypes.c_uint64),
     ]
 
 
@@ -410,6 +410,7 @@ class LevelStats:
     kernel_ms: List[float] = field(default_factory=list)
     kernel_launches: List[int] = field(default_factory=list)
     new_bytes: int = 0
+    self_loops: int = 0  # ABI 5: successors equal to their parent, set apart (single-GPU split chunks)
 
 
 class _LazyLevels(_SeqABC):
@@ -506,7 +507,7 @@ class ModelChecker:
     def _stats(s: _LevelStats) -> LevelStats:
         return LevelStats(s.level, STATUS_NAMES.get(s.status, str(s.status)), s.expanded, s.generated,
                           s.new_states, s.total_generated, s.total_distinct, s.queue, s.seconds,
-                          list(s.kernel_ms), list(s.kernel_launches), s.new_bytes)
+                          list(s.kernel_ms), list(s.kernel_launches), s.new_bytes, s.self_loops)
 
     def init(self) -> LevelStats:
         st = _LevelStats()

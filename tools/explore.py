@@ -54,7 +54,8 @@ while ls.status == "ok" and time.time() - t1 < a.budget and not (a.levels and ls
     ms = " ".join(f"{x * 1e3:.0f}" if a.us else f"{x:.1f}" for x in ls.kernel_ms)
     print(f"L{ls.level:3d} F={ls.expanded:>11d} G={ls.generated:>12d} N={ls.new_states:>11d} "
           f"tot={ls.total_distinct:>12d} {ls.seconds * 1e3:9.1f}ms [{ms}] el={el:.1f}s "
-          f"{ls.total_distinct / el:.3e} ds/s rec={ls.new_bytes / max(1, ls.new_states):.1f}B", flush=True)
+          f"{ls.total_distinct / el:.3e} ds/s rec={ls.new_bytes / max(1, ls.new_states):.1f}B self={ls.self_loops}",
+          flush=True)
     rows.append(ls.__dict__)
 if stopped:
     sys.exit(0)

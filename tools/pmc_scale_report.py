@@ -33,12 +33,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from bench import HBM_PEAK_GBS, VALU_PEAK, alg_bytes, ctx_bytes  # noqa: E402
 
-LEVEL = re.compile(r"^L\s*(\d+) F=\s*(\d+) G=\s*(\d+) N=\s*(\d+) tot=\s*\d+\s+[\d.]+ms \[([^\]]*)\].*rec=([\d.]+)B")
+LEVEL = re.compile(r"^L\s*(\d+) F=\s*(\d+) G=\s*(\d+) N=\s*(\d+) tot=\s*\d+\s+[\d.]+ms \[([^\]]*)\].*rec=([\d.]+)B"
+                   r"(?: self=(\d+))?")
 # name -> (kernel name fragment, explore phase column of its HIP-event time, alg_bytes phase)
 KERNELS = {"expand": ("k_expand", 1, "expand_hash"), "probe": ("k_hash_probe", 5, "probe"),
            "insert": ("k_insert_winners", 5, "insert"),
-           # split chunks commit with k_commit_split (+ its one-wave k_commit_finish, not counted)
-           "commit": ("k_commit_split", 3, "materialize")}
+           # split chunks commit with k_commit_items (+ its one-wave k_commit_finish, not counted)
+           "commit": ("k_commit_items", 3, "materialize")}
 
 
 def levels_of(log):
@@ -46,9 +47,9 @@ def levels_of(log):
     for ln in open(log):
         m = LEVEL.match(ln)
         if m:
-            lv, F, G, N, ph, rec = m.groups()
+            lv, F, G, N, ph, rec, slf = m.groups()
             out.append(dict(level=int(lv), F=int(F), G=int(G), N=int(N), ms=[float(x) for x in ph.split()],
-                            rec=float(rec)))
+                            rec=float(rec), self=int(slf or 0)))
     return out
 
 
@@ -106,7 +107,8 @@ def main():
             # HIP-event columns lump k_probe and k_insert_winners together)
             ms = sum(fetch[i]["_ms"] for i in range(d0, k))
             split = L["F"] >= a.split_min  # (every chunk of such a level is split at Raft.cfg's sizes)
-            alg = alg_bytes(phase, L["F"], L["G"], L["N"], L["rec"], 0, 8, swb, split=split, CTXB=ctx_bytes(a.n, a.V))
+            alg = alg_bytes(phase, L["F"], L["G"], L["N"], L["rec"], 0, 8, swb, split=split, CTXB=ctx_bytes(a.n, a.V),
+                            Gself=L["self"])
             rd = 1024 * sum(fetch[i]["FETCH_SIZE"] for i in range(d0, k))
             wr = 1024 * sum(write[i]["WRITE_SIZE"] for i in range(d0, k))
             hbm = 2 * rd + wr
