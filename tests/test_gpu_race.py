@@ -33,7 +33,7 @@ def cfg_of(g, **kw):
 
 def run_worker(single, runs, tmp_path):
     if not os.path.exists(RACE_LIB):
-        pytest.fail(f"{RACE_LIB} missing: tools/build_variant.sh race (__graft_entry__.build builds it)")
+        pytest.fail(f"{RACE_LIB} missing: make -C tla-raft_amd (__graft_entry__.build) builds it")
     out = tmp_path / "race.json"
     env = dict(os.environ, RMC_LIBRARY=RACE_LIB)
     spec = {"single": single, "runs": runs, "out": str(out)}

@@ -404,6 +404,7 @@ struct Shard {
     // chunk buffers (source side)
     uint32_t *cnt = nullptr, *lslot = nullptr, *wpos = nullptr;
     uint32_t *hcnt = nullptr;   // split chunks: successors per parent to fingerprint (KParams::hcnt)
+    bool chunk_sep = false;     // the chunk being processed set self-loops apart (hcnt valid)
     ulonglong2 *fp = nullptr;
     unsigned long long *L = nullptr;
     ulonglong2 *LXY = nullptr;  // fused path: fingerprint of each election slot (tagged)
@@ -1939,6 +1940,7 @@ struct rmc_ctx {
                 Q.plist = split && nzlist ? s.plist : nullptr;
                 // (a split chunk's self-loops are staged after the successors to fingerprint)
                 Q.hcnt = split && split_insert && split_flags == 7 && nzlist ? s.hcnt : nullptr;
+                s.chunk_sep = Q.hcnt != nullptr;
                 return Q;
             };
             // expand + fingerprint + seen-set probe + staging, one evaluation per parent (a split
@@ -2255,6 +2257,7 @@ struct rmc_ctx {
             unsigned long long best;
             const int kind = first_error(s.hsum + 2, &best);
             if (kind < 0) throw Fail(RMC_E_STATE, "device level loop stopped without an error");
+            s.chunk_sep = false;  // (device-loop levels stage every successor)
             stop_on_error(kind, best, 0, 0, gid_cur, gid_cur + s.cur_n, 0, st);
         }
         HIPCHK(hipStreamSynchronize(stream));
@@ -2278,16 +2281,24 @@ struct rmc_ctx {
             for (uint32_t x : cn) off_p += x;
         }
         const uint64_t wbase = (uint64_t)d2h(s.boff + pl / WTILE) + d2h(s.wpos + pl);
-        // winners among p's first `upto` successor slots
-        auto winners_in = [&](uint32_t upto) -> uint64_t {
-            if (!upto) return 0;
-            std::vector<uint32_t> ls(upto);
-            HIPCHK(hipMemcpy(ls.data(), s.lslot + pl * ks.maxsucc, upto * 4, hipMemcpyDeviceToHost));
+        // p's winners whose slot key is below `bound` (TLC order = slot-key order).  p's staged slots
+        // hold its successors in TLC order -- in a split chunk that set self-loops apart (hcnt) only
+        // the others, which are the only ones that can win -- each with its key (stage_succ, word 6)
+        const uint32_t nslots = s.chunk_sep ? d2h(s.hcnt + pl) : d2h(s.cnt + pl);
+        auto winners_below = [&](uint32_t bound) -> uint64_t {
+            if (!nslots) return 0;
+            std::vector<uint32_t> ls(nslots);
+            std::vector<uint4> st((size_t)nslots * sw4());
+            HIPCHK(hipMemcpy(ls.data(), s.lslot + pl * ks.maxsucc, nslots * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(st.data(), s.score + pl * ks.maxsucc * sw4(), (size_t)nslots * sw4() * 16,
+                             hipMemcpyDeviceToHost));
             uint64_t w = 0;
-            for (uint32_t r = 0; r < upto; r++)
+            for (uint32_t r = 0; r < nslots; r++) {
+                if ((st[(size_t)r * sw4() + 1].z & 0xFFFFu) >= bound) continue;
                 // (LS_WIN: an owner's verdict, or a split chunk's after k_insert_winners)
                 w += ls[r] == LS_WIN ||
                      (!route && ls[r] < LS_ELECT && ((uint32_t)d2h(s.L + ls[r]) >> 2) == (uint32_t)(pl * ks.maxsucc + r));
+            }
             return w;
         };
         // successors of p, in order, to find the sub-action batch boundaries
@@ -2302,8 +2313,9 @@ struct rmc_ctx {
             if ((k >> 7) <= grp) batch_end++;
             if (k < slot) before++;
         }
-        if (kind == ERR_INV || kind == ERR_EVAL) return {off_p + batch_end, wbase + winners_in(before)};
-        if (kind == ERR_ASSERT) return {off_p + cut, wbase + winners_in(cut)};
+        (void)before;
+        if (kind == ERR_INV || kind == ERR_EVAL) return {off_p + batch_end, wbase + winners_below(slot)};
+        if (kind == ERR_ASSERT) return {off_p + cut, wbase + winners_below(grp << 7)};
         return {off_p, wbase};
     }
 
@@ -2932,6 +2944,7 @@ struct rmc_ctx {
             if (s.id == e) {
                 const uint64_t p = s.p0 + (g - s.gblk);
                 const unsigned long long ek = (((p << 16) | slot) << 8) | (gk & 0xFF);
+                s.chunk_sep = false;  // (sharded rounds stage every successor)
                 const ErrCounts ec = error_counts(s, kind, ek, s.p0, true);
                 loc[0] = ec.gen;
                 loc[1] = ec.win;

@@ -8,8 +8,6 @@ set -e
 cd "$(dirname "$0")/../tla-raft_amd"
 case "$1" in
   prof) FLAGS="-DRMC_PHASE_PROF" ;;
-  # forced worst-case schedules at every in-launch hand-off (tests/test_gpu_race.py)
-  race) FLAGS="-DRMC_RACE_PROBE" ;;
   w1) FLAGS="-DRMC_WIDE_WAVES=1" ;;
   # the split (no fingerprint) expansion: waves / SIMD its registers are cut for (e.g. sw5)
   sw*) FLAGS="-DRMC_SPLIT_WAVES=${1#sw}" ;;
@@ -20,7 +18,7 @@ case "$1" in
   # n = 3 occupancy: expansion waves / SIMD, commit waves / SIMD, grid blocks / CU (e.g. n3w6c4g32)
   n3w*) X=${1#n3w}; W=${X%%c*}; X=${X#*c}; C=${X%%g*}; G=${X#*g}
         FLAGS="-DRMC_N3_WAVES=$W -DRMC_N3_COMMIT_WAVES=$C -DRMC_GRID_PER_CU=$G" ;;
-  *) echo "usage: $0 prof|race|w1|sw<W>|iw<W>|pb<P>|n3w<W>c<C>g<G>" >&2; exit 2 ;;
+  *) echo "usage: $0 prof|w1|sw<W>|iw<W>|pb<P>|n3w<W>c<C>g<G>" >&2; exit 2 ;;
 esac
 OUT=build_$1
 mkdir -p "$OUT"
