@@ -2364,6 +2364,7 @@ struct rmc_ctx {
     // TLC order (the fused winner count + commit), and the winners go to the shards that own their
     // global next-level indices, appended in source order -- the level's order.  Levels, counters
     // at an error and traces are those of W = 1.
+    bool round_sep(const Shard &s) const { return split_min && s.np >= split_min && env_int("RMC_NZLIST", 1, 0, 1); }
     KParams round_params(const Shard &s, uint64_t gbase) const {
         KParams Q = chunk_params(s);
         Q.p_begin = s.p0;
@@ -2378,8 +2379,12 @@ struct rmc_ctx {
         Q.xside = s.oside;
         Q.gid_next_base = 0;
         // a round of many parents: the commit visits only those with winners (k_nzlist, as a split
-        // chunk of the single-GPU path; same switches)
-        if (split_min && s.np >= split_min && env_int("RMC_NZLIST", 1, 0, 1)) Q.plist = s.plist;
+        // chunk of the single-GPU path; same switches), and its self-loops are set apart -- known seen
+        // (the parent's fingerprint is in its owner's seen set), they are neither fingerprinted nor routed
+        if (round_sep(s)) {
+            Q.plist = s.plist;
+            Q.hcnt = s.hcnt;
+        }
         Q.trace_base = 0;
         return Q;
     }
@@ -2498,6 +2503,7 @@ struct rmc_ctx {
                 s.gblk = (c * (uint64_t)W + (uint64_t)s.id) * B;
                 HIPCHK(hipMemsetAsync(s.ocnt, 0, 64 * 4, stream));
                 HIPCHK(hipMemsetAsync(s.sum + 9, 0, 8, stream));
+                HIPCHK(hipMemsetAsync(s.sum + SUM_SELF, 0, 8, stream));
                 // (before any skip: a shard with no parents this round receives items, and they must
                 // not bid in LXY / L under an earlier round's tag)
                 s.lx_bid = false;
@@ -2585,7 +2591,7 @@ struct rmc_ctx {
                     for (int d = 0; d < W; d++) hc[d] = (uint32_t)xp[li].send_off[d];
                     HIPCHK(hipMemcpyAsync(s.ocnt, hc, W * 4, hipMemcpyHostToDevice, stream));
                     timed(PH_XCHG, [&] {
-                        launch_route_place(s.fp, s.cnt, s.np, (uint32_t)MS, (uint32_t)W, s.ocnt, s.gblk, s.xs, s.perm,
+                        launch_route_place(s.fp, round_sep(s) ? s.hcnt : s.cnt, s.np, (uint32_t)MS, (uint32_t)W, s.ocnt, s.gblk, s.xs, s.perm,
                                            (uint32_t)s.id, stream);
                     });
                 }
@@ -2944,7 +2950,7 @@ struct rmc_ctx {
             if (s.id == e) {
                 const uint64_t p = s.p0 + (g - s.gblk);
                 const unsigned long long ek = (((p << 16) | slot) << 8) | (gk & 0xFF);
-                s.chunk_sep = false;  // (sharded rounds stage every successor)
+                s.chunk_sep = round_sep(s);  // (a split round stages its successors but its self-loops)
                 const ErrCounts ec = error_counts(s, kind, ek, s.p0, true);
                 loc[0] = ec.gen;
                 loc[1] = ec.win;

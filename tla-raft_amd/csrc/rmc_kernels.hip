@@ -181,6 +181,7 @@ struct Succ {
     uint32_t key;  // KEY_NONE = disabled
     uint32_t s;    // acting server (row of the structured hash that changed)
     uint32_t lw, mirow, nirow;  // logs[s], matchIndex[s][*], nextIndex[s][*] of the successor
+    bool self;  // the parent itself (FollowerAcceptEntry changing nothing): in the seen set already
 };
 
 template <int N, int V, int MR>
@@ -665,9 +666,11 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
         ob.key = KEY_NONE;
         ob.nadd = 0;
         ob.s = 0;
+        ob.self = false;
 #pragma unroll
         for (int a = 0; a < Spec<N, V, MR>::NADD; a++) ob.add[a] = 0;
     }
+    o.self = false;
     const uint32_t k = (uint32_t)(r * 64 + lane);
     if (k >= W.nm) return;
     const uint32_t m = W.inf[r];
@@ -750,10 +753,12 @@ __device__ __forceinline__ void eval_msg(const KParams &P, const Wave<N, V, MR> 
                 o.lw = nlw;
                 o.c[Lo::W_LL] = setnib(o.c[Lo::W_LL], s, nl);
             }
-            if (!in_msgs(W.bm, resp)) {
+            const bool has = in_msgs(W.bm, resp);
+            if (!has) {
                 o.add[0] = resp; o.nadd = 1;
                 if (ainf) ainf[0] = minfo(ARESP, s, src, mt, pli + ent, 1, 0, 0, 0, 0);
             }
+            o.self = has && !(truncated || append_new) && nci == ci;  // (the parent itself)
             o.key = slot_key(s, FAE, k);
         } else {
             const uint32_t resp = pid;  // nat2id[nat_aresp(s, src, mt, pli, FALSE)]
@@ -804,6 +809,7 @@ __device__ __forceinline__ void eval_slot(const KParams &P, const Wave<N, V, MR>
     o.key = KEY_NONE;
     o.nadd = 0;
     o.s = 0;
+    o.self = false;
 #pragma unroll
     for (int a = 0; a < S::NADD; a++) o.add[a] = 0;
     if (lane >= N * S::SLOTS_PER_SERVER) return;
@@ -1377,6 +1383,7 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
     __shared__ uint32_t sW1[HX], sW2[HX];
     __shared__ uint16_t sCa[HX];
     __shared__ uint8_t sS[HX], sNa[HX];
+    __shared__ uint16_t sRq[HX];                        // fused level: the TLC rank of each successor hashed
     // per batch successor: its acting row's contents, tie ranks, first task, running minimum;
     // per task lane: its partial minimum and successor
     __shared__ uint64_t sC[2][HASH ? HB * N : 1];
@@ -1476,6 +1483,33 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
                 for (int r = 0; r < NC; r++) rank[r] += kt < cand[r].key ? 1u : 0u;
             }
         }
+        // fused level: a self-loop (the parent itself, FollowerAcceptEntry changing nothing -- ~40 % of
+        // configs[1]'s successors) is in the seen set already: it takes its slot with LS_SEEN and no
+        // fingerprint, probe or election; the others are hashed in TLC order at hrank (sharded rounds
+        // route every successor's fingerprint: none set apart)
+        constexpr bool SKIPSELF = MODE == M_FUSED;
+        uint32_t hrank[NC], htotal = total;
+        uint64_t sm[NC];
+#pragma unroll
+        for (int r = 0; r < NC; r++) {
+            hrank[r] = rank[r];
+            sm[r] = 0;
+        }
+        if (SKIPSELF && !P.route) {
+#pragma unroll
+            for (int r = 0; r < NC; r++) {
+                sm[r] = __ballot(cand[r].key != KEY_NONE && cand[r].self);
+                htotal -= (uint32_t)__popcll(sm[r]);
+            }
+#pragma unroll
+            for (int q = 0; q < NC; q++) {
+                for (uint64_t m = sm[q]; m; m &= m - 1) {
+                    const uint32_t kt = rdlane(cand[q].key, __ffsll((unsigned long long)m) - 1);
+#pragma unroll
+                    for (int r = 0; r < NC; r++) hrank[r] -= kt < cand[r].key ? 1u : 0u;
+                }
+            }
+        }
         const uint64_t pl = p - P.p_begin;  // chunk-local parent index
         uint64_t am = 0;
         {
@@ -1507,6 +1541,10 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
             for (int r = 0; r < NC; r++) {
                 if (cand[r].key == KEY_NONE) continue;
                 const uint64_t q = pl * (uint64_t)MX + rank[r];
+                if (SKIPSELF && ((sm[r] >> lane) & 1u)) {  // a self-loop: decided here, never committed
+                    P.lslot[q] = LS_SEEN;
+                    continue;
+                }
                 stage_succ<N, V, MR>(cand[r], W.nm, P.score + q * (uint64_t)S::SW4);
             }
         }
@@ -1539,12 +1577,13 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
             pC[f][t * N + j] = content<N>(f, (uint32_t)t, (uint32_t)j, W.c, pcore[Lo::W_LOG + t], pcore[Lo::W_MI + t],
                                           pcore[Lo::W_NI + t], f ? M1[t * N + j] : M0[t * N + j]);
         }
-        // (b) every enabled successor's row inputs at its TLC rank
+        // (b) every enabled successor's row inputs at its TLC rank (self-loops apart: hrank)
 #pragma unroll
         for (int r = 0; r < NC; r++) {
-            if (cand[r].key == KEY_NONE) continue;
+            if (cand[r].key == KEY_NONE || ((sm[r] >> lane) & 1u)) continue;
             const Succ<N, V, MR> &o = cand[r];
-            const uint32_t g = rank[r];
+            const uint32_t g = hrank[r];
+            sRq[g] = (uint16_t)rank[r];
             const uint32_t vfs = nib(o.c[Lo::W_VF], o.s);
             sUg[g] = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI], o.c[Lo::W_LL], o.lw,
                                  o.mirow, o.nirow, o.s);
@@ -1567,7 +1606,7 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
             const ulonglong2 f = make_ulonglong2(best.x | 1ull, best.y);
             if (MODE == M_FUSED) {
                 // the seen set is read-only in this launch (commit inserts)
-                const uint64_t q = pl * (uint64_t)MX + lo;
+                const uint64_t q = pl * (uint64_t)MX + sRq[lo];
                 P.fp[q] = f;
                 if (P.route) return;  // sharded round: the fingerprint's owner probes and elects
                 const uint32_t e = ((uint32_t)sNa[lo] + (W.nm & 1u) + 1u) >> 1;
@@ -1582,8 +1621,8 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
             }
         };
         // (c) per batch of HB successors (by TLC rank)
-        for (uint32_t b0 = 0; b0 < total; b0 += (uint32_t)HB) {
-            const uint32_t nb = total - b0 < (uint32_t)HB ? total - b0 : (uint32_t)HB;
+        for (uint32_t b0 = 0; b0 < htotal; b0 += (uint32_t)HB) {
+            const uint32_t nb = htotal - b0 < (uint32_t)HB ? htotal - b0 : (uint32_t)HB;
             {  // (c1) the acting row's contents: lane (half, successor) when FH == 2, else both halves
                 const uint32_t l = (uint32_t)lane % HB, g = b0 + l;
                 if (l < nb) {
