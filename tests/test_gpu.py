@@ -310,7 +310,7 @@ def test_sharded_commit_list_matches_golden_levels(name, mode, monkeypatch):
 @pytest.mark.parametrize("mode", ["virtual2", "rccl1"])
 @pytest.mark.parametrize("name", ["n3_v1_e2_r3", "seeded_n3_v2_e2_r3", "n4_v1_e1_r3"])
 def test_sharded_run_then_reset_reruns_golden(name, mode, monkeypatch):
-    """A sharded run whose split rounds used the fused election table (LXY / L) as their owner table,
+    """A sharded run whose split rounds used the fused election table (ET) as their owner table,
     then rmc_reset, then a second run whose first levels are replicated (the fused election again):
     both runs give the golden levels, counters and traces (the owner keys a sharded round leaves in L
     are smaller than any fused election word; reset must clear them)."""

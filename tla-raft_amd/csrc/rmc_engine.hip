@@ -406,11 +406,10 @@ struct Shard {
     uint32_t *hcnt = nullptr;   // split chunks: successors per parent to fingerprint (KParams::hcnt)
     bool chunk_sep = false;     // the chunk being processed set self-loops apart (hcnt valid)
     ulonglong2 *fp = nullptr;
-    unsigned long long *L = nullptr;
-    ulonglong2 *LXY = nullptr;  // fused path: fingerprint of each election slot (tagged)
+    ESlot *E = nullptr;         // election table: tagged fingerprint + election word per slot (32 B)
     uint32_t epoch = 0;
-    uint32_t lxy_epoch0 = 0;    // epoch of the last LXY clear (16-bit tags repeat after 65535 epochs)
-    uint64_t gslots = 0, lcap = 0;  // successor slots of fp / lslot / score, election slots of L / LXY
+    uint32_t lxy_epoch0 = 0;    // epoch of the last E clear (16-bit tags repeat after 65535 epochs)
+    uint64_t gslots = 0, lcap = 0;  // successor slots of fp / lslot / score, election slots of E
     // fused single-shard level: sparse successor staging (slot q = chunk parent * maxsucc + rank)
     uint4 *score = nullptr;
     uint32_t *wcnt = nullptr, *wacc = nullptr, *pnm = nullptr, *wposw = nullptr, *ctick = nullptr;
@@ -430,11 +429,10 @@ struct Shard {
     XItem *xs = nullptr, *xr = nullptr;
     uint64_t xs_cap = 0, xr_cap = 0;
     uint32_t *perm = nullptr, *sflag = nullptr, *rslot = nullptr, *rflag = nullptr, *ocnt = nullptr;
-    ulonglong2 *OT = nullptr;
-    unsigned long long *OK = nullptr;
+    ESlot *OT = nullptr;
     uint64_t ot_cap = 0;
     uint32_t ot_round = 0;  // rounds on the owner table since it was last cleared (its tag, k_owner_elect)
-    // split rounds: the fused election table (LXY / L, unused once the run is sharded) is the owner
+    // split rounds: the fused election table (E, unused once the run is sharded) is the owner
     // table, so k_hash_probe bids the shard's own successors as it fingerprints them; rounds on it
     // since its last clear (0: not yet cleared for this use), and whether this round's own bids went in
     uint32_t lx_round = 0;
@@ -577,7 +575,7 @@ struct rmc_ctx {
         Q.wposw = s.wposw; Q.bw = s.bw; Q.bg = s.bg; Q.boff = s.boff; Q.bww = s.bww; Q.boffw = s.boffw;
         Q.bn = s.bn; Q.boffn = s.boffn;
         Q.tickets = s.tickets; Q.ctick = s.ctick; Q.sum = s.sum;
-        Q.score = s.score; Q.lslot = s.lslot; Q.L = s.L; Q.LXY = s.LXY; Q.hctx = s.hctx;
+        Q.score = s.score; Q.lslot = s.lslot; Q.ET = s.E; Q.hctx = s.hctx;
         return Q;
     }
 
@@ -881,7 +879,7 @@ struct rmc_ctx {
             HIPCHK(hipMemGetInfo(&fr, &tot));
             // (per slot: fingerprint, verdict, staging, scan word, ~2 election slots; an RCCL rank also its
             // route / owner words and items out and in)
-            const uint64_t per_slot = 16 + 4 + 16 * (uint64_t)sw4() + 4 + 2 * 24 +
+            const uint64_t per_slot = 16 + 4 + 16 * (uint64_t)sw4() + 4 + 2 * 32 +
                                       ((rccl || hostx) ? 4 + 4 + 2 * sizeof(XItem) + 8 : 0);
             // beside the budgets: the live levels' record offsets (8 B a state; the two widest levels
             // of configs[3] hold about a third of its seen set's states) and some slack
@@ -945,13 +943,11 @@ struct rmc_ctx {
         }
         s.gslots = g;
         if (lc > s.lcap) {
-            dfree(s.L); dfree(s.LXY);
-            s.L = nullptr; s.LXY = nullptr;
-            s.L = dmalloc<unsigned long long>(lc);
-            // an all-ones election word is older than every epoch's (elect_key)
-            HIPCHK(hipMemsetAsync(s.L, 0xFF, lc * 8, stream));
-            s.LXY = dmalloc<ulonglong2>(lc);
-            HIPCHK(hipMemsetAsync(s.LXY, 0, lc * 16, stream));
+            dfree(s.E);
+            s.E = nullptr;
+            s.E = dmalloc<ESlot>(lc);
+            // free slots; an all-ones election word is older than every epoch's (elect_key)
+            launch_eslot_clear(s.E, lc, stream);
             s.lcap = lc;
             s.lxy_epoch0 = s.epoch;
         }
@@ -1018,9 +1014,9 @@ struct rmc_ctx {
     void free_shard(Shard &s) {
         dfree(s.R); dfree(s.cur_off); dfree(s.nxt_off); dfree(s.T); dfree(s.Tc); dfree(s.par); dfree(s.pslot);
         dfree(s.cnt);
-        dfree(s.lslot); dfree(s.wpos); dfree(s.fp); dfree(s.L); dfree(s.LXY); dfree(s.tmp);
+        dfree(s.lslot); dfree(s.wpos); dfree(s.fp); dfree(s.E); dfree(s.tmp);
         dfree(s.xs); dfree(s.xr); dfree(s.perm); dfree(s.sflag); dfree(s.rslot); dfree(s.rflag); dfree(s.ocnt);
-        dfree(s.OT); dfree(s.OK); dfree(s.ob); dfree(s.ib); dfree(s.oside); dfree(s.iside); dfree(s.ooff);
+        dfree(s.OT); dfree(s.ob); dfree(s.ib); dfree(s.oside); dfree(s.iside); dfree(s.ooff);
         dfree(s.isz); dfree(s.ioff);
         dfree(s.err); dfree(s.sum); dfree(s.flags);
         dfree(s.score); dfree(s.wcnt); dfree(s.wacc); dfree(s.pnm); dfree(s.hcnt); dfree(s.wposw); dfree(s.ctick);
@@ -1270,15 +1266,14 @@ struct rmc_ctx {
     // also across rmc_reset, so a stale slot never reads as current and its key is never smaller.
     // rounds between clears of the owner table (RMC_OT_CLEAR_ROUNDS: tests take it down to a few)
     const uint32_t ot_clear_rounds = (uint32_t)env_int("RMC_OT_CLEAR_ROUNDS", 0xFFFD, 1, 0xFFFD);
-    // split sharded rounds: 1 = the own successors bid in LXY / L inside k_hash_probe (when the table
+    // split sharded rounds: 1 = the own successors bid in E inside k_hash_probe (when the table
     // fits them), 0 = never (k_local_elect into the owner table), 2 = bid there but always redo the
     // bids in the owner table (a test of that fallback)
     const int owner_lxy = env_int("RMC_OWNER_LXY", 1, 0, 2);
-    // the round's tag on LXY / L as the owner table (cleared on first use and every ot_clear_rounds)
+    // the round's tag on E as the owner table (cleared on first use and every ot_clear_rounds)
     uint32_t lx_table(Shard &s) {
         if (s.lx_round == 0 || s.lx_round >= ot_clear_rounds) {
-            HIPCHK(hipMemsetAsync(s.LXY, 0, s.lcap * 16, stream));
-            HIPCHK(hipMemsetAsync(s.L, 0xFF, s.lcap * 8, stream));
+            launch_eslot_clear(s.E, s.lcap, stream);
             s.lx_round = 1;
         } else {
             ++s.lx_round;
@@ -1292,15 +1287,12 @@ struct rmc_ctx {
         if (need > o.ot_cap) {
             HIPCHK(hipStreamSynchronize(stream));
             dfree(o.OT);
-            dfree(o.OK);
-            o.OT = dmalloc<ulonglong2>(need);
-            o.OK = dmalloc<unsigned long long>(need);
+            o.OT = dmalloc<ESlot>(need);
             o.ot_cap = need;
             clear = true;
         }
         if (clear || o.ot_round >= ot_clear_rounds) {  // tags 2 .. 0xFFFE, increasing between clears
-            HIPCHK(hipMemsetAsync(o.OT, 0, o.ot_cap * 16, stream));
-            HIPCHK(hipMemsetAsync(o.OK, 0xFF, o.ot_cap * 8, stream));
+            launch_eslot_clear(o.OT, o.ot_cap, stream);
             o.ot_round = 1;
         } else {
             ++o.ot_round;
@@ -1877,10 +1869,10 @@ struct rmc_ctx {
     }
 
     // The fused path's election slots carry 16-bit epoch tags (elect_tag): before the next
-    // `ahead` epochs could reuse a tag still in LXY, clear it (all tags are nonzero).
+    // `ahead` epochs could reuse a tag still in E, clear it (all tags are nonzero).
     void renew_election_tags(Shard &s, uint32_t ahead) {
-        if (!s.LXY || s.epoch + ahead - s.lxy_epoch0 < 0xFFFFu) return;
-        HIPCHK(hipMemsetAsync(s.LXY, 0, s.lcap * 16, stream));
+        if (!s.E || s.epoch + ahead - s.lxy_epoch0 < 0xFFFFu) return;
+        launch_eslot_clear(s.E, s.lcap, stream);
         s.lxy_epoch0 = s.epoch;
     }
 
@@ -2297,7 +2289,7 @@ struct rmc_ctx {
                 if ((st[(size_t)r * sw4() + 1].z & 0xFFFFu) >= bound) continue;
                 // (LS_WIN: an owner's verdict, or a split chunk's after k_insert_winners)
                 w += ls[r] == LS_WIN ||
-                     (!route && ls[r] < LS_ELECT && ((uint32_t)d2h(s.L + ls[r]) >> 2) == (uint32_t)(pl * ks.maxsucc + r));
+                     (!route && ls[r] < LS_ELECT && ((uint32_t)d2h(&s.E[ls[r]].k) >> 2) == (uint32_t)(pl * ks.maxsucc + r));
             }
             return w;
         };
@@ -2505,12 +2497,12 @@ struct rmc_ctx {
                 HIPCHK(hipMemsetAsync(s.sum + 9, 0, 8, stream));
                 HIPCHK(hipMemsetAsync(s.sum + SUM_SELF, 0, 8, stream));
                 // (before any skip: a shard with no parents this round receives items, and they must
-                // not bid in LXY / L under an earlier round's tag)
+                // not bid in E under an earlier round's tag)
                 s.lx_bid = false;
                 if (!s.np || fail[li]) continue;
                 const bool split = split_min && s.np >= split_min;
                 // (the fused election table holds a round's successors at load <= 1/2: ensure_chunk)
-                s.lx_bid = owner_lxy && split && s.L && s.lcap >= 2 * s.np * MS;
+                s.lx_bid = owner_lxy && split && s.E && s.lcap >= 2 * s.np * MS;
                 timed(PH_HASH, [&] {
                     KParams Q = round_params(s, gbase);
                     if (split) {  // fingerprints a lane per successor (route: no probe), counted per owner
@@ -2518,8 +2510,7 @@ struct rmc_ctx {
                         Q.nown = (uint32_t)W;
                         if (s.lx_bid) {  // ... and the shard's own successors' bids
                             Q.ot_round = lx_table(s);
-                            Q.OT = s.LXY;
-                            Q.OK = s.L;
+                            Q.OT = s.E;
                             Q.ot_mask = s.lcap - 1;
                             Q.self = (uint32_t)s.id;
                             Q.gblk = s.gblk;
@@ -2610,30 +2601,28 @@ struct rmc_ctx {
                 guard(li, [&] {
                     inject(3, o.id, c, L);
                     grow_seen(o, o.T_count + R + Rl);
-                    // the own successors' bids are in LXY / L already (k_hash_probe) if the received
+                    // the own successors' bids are in E already (k_hash_probe) if the received
                     // ones fit beside them at load <= 1/2; otherwise every bid goes to the owner table
                     const bool lx = o.lx_bid && 2 * (R + Rl) <= o.lcap && owner_lxy != 2;
-                    ulonglong2 *OT = o.LXY;
-                    unsigned long long *OK = o.L;
+                    ESlot *OT = o.E;
                     uint64_t mask = o.lcap - 1;
                     uint32_t rnd = o.lx_round;
                     if (!lx) {
                         mask = owner_table(o, R + Rl) - 1;
                         OT = o.OT;
-                        OK = o.OK;
                         rnd = o.ot_round;
                     }
                     timed(PH_DEDUP, [&] {
                         const KParams Q = round_params(o, gbase);
                         if (Rl && !lx)
-                            ks.local_elect(Q, o.np, o.seen(), OT, OK, mask, rnd, (uint32_t)W, (uint32_t)o.id, o.gblk,
+                            ks.local_elect(Q, o.np, o.seen(), OT, mask, rnd, (uint32_t)W, (uint32_t)o.id, o.gblk,
                                            stream);
                         if (R) {
-                            launch_owner_elect(o.xr, R, o.seen(), OT, OK, mask, rnd, o.rslot, stream);
-                            launch_owner_flags(o.xr, R, o.rslot, OK, rnd, o.seen(), o.rflag, o.sum + 9, stream);
+                            launch_owner_elect(o.xr, R, o.seen(), OT, mask, rnd, o.rslot, stream);
+                            launch_owner_flags(o.xr, R, o.rslot, OT, rnd, o.seen(), o.rflag, o.sum + 9, stream);
                         }
                         if (Rl)
-                            ks.local_flags(Q, o.np, o.seen(), OK, rnd, (uint32_t)W, (uint32_t)o.id, o.gblk,
+                            ks.local_flags(Q, o.np, o.seen(), OT, rnd, (uint32_t)W, (uint32_t)o.id, o.gblk,
                                            o.sum + 9, stream);
                     });
                 });
@@ -3386,14 +3375,13 @@ struct rmc_ctx {
             s.hpar.n = s.hslot.n = 0;
             s.level_start.clear();
             if (s.lx_round) {
-                // LXY / L served as a sharded run's owner table: its owner keys (top 16 bits <= 0xFFFD)
-                // are smaller than any fused election word (elect_key: 0xFFFF...), so the next run's
-                // fused levels would keep them and drop states -- back to the fused table's empty state
-                HIPCHK(hipMemsetAsync(s.LXY, 0, s.lcap * 16, stream));
-                HIPCHK(hipMemsetAsync(s.L, 0xFF, s.lcap * 8, stream));
+                // E served as a sharded run's owner table: its owner keys (top 16 bits <= 0xFFFD) are
+                // smaller than any fused election word (elect_key: 0xFFFF...), so the next run's fused
+                // levels would keep them and drop states -- back to the fused table's empty state
+                launch_eslot_clear(s.E, s.lcap, stream);
                 s.lxy_epoch0 = s.epoch;
             }
-            s.lx_round = 0;  // the fused levels of the next run use LXY / L again
+            s.lx_round = 0;  // the fused levels of the next run use E again
         }
         // (the clears are stream-ordered before the next run's first kernel: no wait here)
         trace.clear();

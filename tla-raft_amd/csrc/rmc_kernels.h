@@ -17,6 +17,16 @@ struct Tables {
     uint32_t bmw;             // 32-bit words of a bitmap over the universe's ids: ceil(U / 32)
 };
 
+// An election slot (the fused / split chunk's election table, a sharded round's owner table): the
+// fingerprint a slot holds, both words tagged in their low 16 bits, and the slot's election word -- in
+// one 32-B sector, so a candidate's claim and its bid touch one line (round 4 kept x / y and the word in
+// two arrays: two random lines per new fingerprint).
+struct ESlot {
+    unsigned long long x, y;  // the fingerprint, tagged (elect_tag / the owner table's round tag)
+    unsigned long long k;     // the election word (elect_key / owner_key): the smallest bid wins
+    unsigned long long pad;
+};
+
 // Seen set (TLC's FPSet): open addressing over 128-bit fingerprints {x | 1, y}.
 //   full:    16-B slots {x, y} (T != nullptr), grown x4 by rehash while small;
 //   compact:  8-B slots holding x only (Tc != nullptr): the slot's probe run, which starts at the
@@ -124,8 +134,7 @@ struct KParams {
     uint32_t nown;             // ... of that many owners (W)
     // ... and, with OT set, the shard's own successors bid in its owner table (k_local_elect's work):
     // lslot = LS_ELECT (another shard's), LS_SEEN, or the table slot; key (gblk + pl) << 10 | rank
-    ulonglong2 *OT;
-    unsigned long long *OK;
+    ESlot *OT;
     uint64_t ot_mask, gblk;
     uint32_t ot_round, self;
     // split chunk (host-driven chunks of many parents): the expansion (M_SPLIT) stages the successors
@@ -145,11 +154,10 @@ struct KParams {
     // the exclusive scans of winners / their record words per parent inside each WTILE-parent
     // tile, and a parent's first winner lands at boff[tile] + wpos (words boffw[tile] + wposw).
     uint4 *score;
-    uint32_t *lslot;           // LS_SEEN, LS_ELECT, or the election slot in L
-    unsigned long long *L;     // chunk election table: sharded path (epoch << 32) | q; fused path
-                               // the election word ((0xFFFFFFFF - epoch) << 32) | q << 2 | e (elect_key)
-    ulonglong2 *LXY;           // fused path: the fingerprint each election slot holds, both words
-                               // tagged with the chunk's 16-bit tag (elect_tag) in their low bits
+    uint32_t *lslot;           // LS_SEEN, LS_ELECT, or the election slot in ET
+    ESlot *ET;                 // chunk election table: per slot the fingerprint, both words tagged with the
+                               // chunk's 16-bit tag (elect_tag) in their low bits, and the election word
+                               // ((0xFFFFFFFF - epoch) << 32) | q << 2 | e (elect_key)
     uint64_t Lmask;
     uint32_t epoch;
     uint32_t *wcnt;            // winners per parent (chunk-local)
@@ -191,9 +199,9 @@ struct KernelSet {
                                                             // with winners (plist; LS_WIN verdicts) + summary
     // sharded round, the successors the shard owns itself: bids in the round's owner table, then
     // (every bid in) verdicts in lslot, winners into the seen set and onto wacc
-    void (*local_elect)(const KParams &, uint64_t np, Seen, ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
+    void (*local_elect)(const KParams &, uint64_t np, Seen, ESlot *OT, uint64_t mask,
                         uint32_t round, uint32_t W, uint32_t self, uint64_t g0, hipStream_t);
-    void (*local_flags)(const KParams &, uint64_t np, Seen, const unsigned long long *OK, uint32_t round, uint32_t W,
+    void (*local_flags)(const KParams &, uint64_t np, Seen, const ESlot *OT, uint32_t round, uint32_t W,
                         uint32_t self, uint64_t g0, unsigned long long *inserted, hipStream_t);
     void (*fp_states)(const KParams &, uint64_t n, hipStream_t);  // fp of front[0..n) -> fp
     void (*inv_states)(const KParams &, uint64_t n, int32_t *out, hipStream_t); // per state: 1/0/-1 for inv_mask bits
@@ -210,6 +218,8 @@ bool get_kernels(int N, int V, int msg_cap, bool become_follower, KernelSet *ks)
 constexpr uint32_t LS_SEEN = 0xFFFFFFFFu, LS_ELECT = 0xFFFFFFFEu, LS_WIN = 0xFFFFFFFDu;
 // full-slot table -> (full or compact) table
 void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, Seen dst, hipStream_t s);
+// every slot free: fingerprint words 0, election word all ones (older than every epoch / round)
+void launch_eslot_clear(ESlot *t, uint64_t n, hipStream_t s);
 void launch_insert_fps(const ulonglong2 *fp, uint64_t n, Seen seen, hipStream_t s);
 // the control block of a device-driven batch, passed by value (no copy-engine hand-off)
 void launch_set_ctl(LevelCtl *dst, const LevelCtl &v, hipStream_t s);
@@ -229,9 +239,9 @@ void launch_route_count(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, 
                         uint32_t *ocnt, hipStream_t s);
 void launch_route_place(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
                         uint32_t *cursor, uint64_t g0, XItem *items, uint32_t *perm, uint32_t self, hipStream_t s);
-void launch_owner_elect(const XItem *it, uint64_t R, Seen seen, ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
+void launch_owner_elect(const XItem *it, uint64_t R, Seen seen, ESlot *OT, uint64_t mask,
                         uint32_t round, uint32_t *rslot, hipStream_t s);
-void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const unsigned long long *OK, uint32_t round,
+void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const ESlot *OT, uint32_t round,
                         Seen seen, uint32_t *flag, unsigned long long *inserted, hipStream_t s);
 void launch_scatter_win(const uint32_t *perm, const uint32_t *flag, uint64_t G, const uint4 *score, uint32_t sw4,
                         const uint32_t *pnm, uint32_t maxsucc, uint32_t *lslot, uint32_t *wacc, hipStream_t s);

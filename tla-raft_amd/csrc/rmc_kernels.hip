@@ -65,6 +65,9 @@ extern "C" int rmc_debug_phases(unsigned long long *out, int reset) {
 #ifndef RMC_WIDE_WAVES
 #define RMC_WIDE_WAVES 2
 #endif
+#ifndef RMC_FUSED_SKIPSELF  // the fused expansion sets self-loops apart (0: hashes and probes them, round 4)
+#define RMC_FUSED_SKIPSELF 1
+#endif
 #ifndef RMC_SPLIT_WAVES  // the split expansion (no fingerprints): waves per SIMD its registers are cut for
 #define RMC_SPLIT_WAVES 6
 #endif
@@ -1237,9 +1240,10 @@ __device__ __forceinline__ uint32_t fp_owner(const ulonglong2 f, uint32_t W) {
 
 // ---- in-launch election (fused single-GPU level) -------------------------------------------
 // The first successor in TLC order (smallest slot q) per new fingerprint wins.  Election slot g
-// holds the fingerprint in LXY[g] -- both words carry the chunk's 16-bit tag in their low bits,
+// holds the fingerprint in E[g].x / .y -- both words carry the chunk's 16-bit tag in their low bits,
 // so slots of earlier chunks read as free and the table is never cleared (the host clears it
-// once every 65535 epochs) -- and the election word L[g] = elect_key(epoch, smallest q, its e).
+// once every 65535 epochs) -- and the election word E[g].k = elect_key(epoch, smallest q, its e), in the
+// same 32-B sector.
 // The word of a newer epoch is smaller than any older one (and than the all-ones initial value),
 // so every candidate just takes the minimum.  All accesses are agent-scope atomics on the slot's
 // own words: a claimer CASes x then stores y; a candidate that finds x equal but y not yet
@@ -1257,14 +1261,14 @@ __device__ __forceinline__ uint32_t elect_q(unsigned long long w) { return (uint
 // minimum the atomic returns) off its parent: once the launch is done, wacc per parent is exact
 // (the packed sum of adds and subtracts is exact mod 2^32 whatever their order).
 template <int MAXS>
-__device__ __forceinline__ uint32_t elect_slot(ulonglong2 *LXY, unsigned long long *L, uint32_t *wacc, uint64_t mask,
+__device__ __forceinline__ uint32_t elect_slot(ESlot *E, uint32_t *wacc, uint64_t mask,
                                                uint32_t epoch, const ulonglong2 f, uint64_t q, uint32_t e, uint64_t g,
                                                unsigned long long v) {
     // g = l_index(f, mask) and v = its x word, loaded by the caller together with the seen-set probe
     const unsigned long long tag = elect_tag(epoch);
     const unsigned long long xk = (f.x & ~0xFFFFull) | tag, yk = (f.y & ~0xFFFFull) | tag;
     for (;;) {
-        unsigned long long *px = &LXY[g].x, *py = &LXY[g].y;
+        unsigned long long *px = &E[g].x, *py = &E[g].y;
         if ((v & 0xFFFFull) != tag) {
             const unsigned long long prev = atomicCAS(px, v, xk);
             if (prev == v) {
@@ -1286,10 +1290,10 @@ __device__ __forceinline__ uint32_t elect_slot(ulonglong2 *LXY, unsigned long lo
             if (y == yk) break;
         }
         g = (g + 1) & mask;
-        v = __hip_atomic_load(&LXY[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = __hip_atomic_load(&E[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const unsigned long long mine = elect_key(epoch, q, e);
-    const unsigned long long old = atomicMin(&L[g], mine);
+    const unsigned long long old = atomicMin(&E[g].k, mine);
     if (old > mine) {
         atomicAdd(&wacc[q / MAXS], 1u + (e << 12));
         if ((old >> 32) == (mine >> 32)) atomicSub(&wacc[elect_q(old) / MAXS], 1u + ((uint32_t)(old & 3u) << 12));
@@ -1487,7 +1491,7 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
         // configs[1]'s successors) is in the seen set already: it takes its slot with LS_SEEN and no
         // fingerprint, probe or election; the others are hashed in TLC order at hrank (sharded rounds
         // route every successor's fingerprint: none set apart)
-        constexpr bool SKIPSELF = MODE == M_FUSED;
+        constexpr bool SKIPSELF = MODE == M_FUSED && RMC_FUSED_SKIPSELF;
         uint32_t hrank[NC], htotal = total;
         uint64_t sm[NC];
 #pragma unroll
@@ -1613,9 +1617,9 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
                 // the election slot's first word goes out with the seen-set probe: one round trip
                 // fewer for a new fingerprint
                 const uint64_t g0 = l_index(f, P.Lmask);
-                const unsigned long long v0 = __hip_atomic_load(&P.LXY[g0].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned long long v0 = __hip_atomic_load(&P.ET[g0].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 P.lslot[q] = seen_contains(P.seen, f) ? LS_SEEN
-                                                      : elect_slot<MX>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g0, v0);
+                                                      : elect_slot<MX>(P.ET, P.wacc, P.Lmask, P.epoch, f, q, e, g0, v0);
             } else {
                 P.fp[lo] = f;
             }
@@ -2366,7 +2370,7 @@ __device__ __forceinline__ void each_successor(const KParams &P, F &&f) {
 __device__ __forceinline__ unsigned long long owner_key(uint32_t tag, uint64_t key) {
     return ((unsigned long long)(0xFFFFu - tag) << 48) | key;  // key = global parent index << 10 | rank < 2^48
 }
-__device__ __forceinline__ uint32_t owner_bid(ulonglong2 *OT, unsigned long long *OK, uint64_t mask, uint32_t tag32,
+__device__ __forceinline__ uint32_t owner_bid(ESlot *OT, uint64_t mask, uint32_t tag32,
                                               const ulonglong2 f, uint64_t key) {
     const unsigned long long tag = tag32;
     const unsigned long long xk = (f.x & ~0xFFFFull) | tag, yk = (f.y & ~0xFFFFull) | tag;
@@ -2405,7 +2409,7 @@ __device__ __forceinline__ uint32_t owner_bid(ulonglong2 *OT, unsigned long long
             v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    atomicMin(&OK[g], owner_key(tag32, key));
+    atomicMin(&OT[g].k, owner_key(tag32, key));
     return (uint32_t)g;
 }
 
@@ -2502,15 +2506,15 @@ __global__ __launch_bounds__(256) void k_hash_probe(KParams P) {
                 P.lslot[q] = o != P.self ? LS_ELECT
                              : seen_contains(P.seen, f)
                                  ? LS_SEEN
-                                 : owner_bid(P.OT, P.OK, P.ot_mask, P.ot_round + 1u, f, ((P.gblk + pl) << 10) | r);
+                                 : owner_bid(P.OT, P.ot_mask, P.ot_round + 1u, f, ((P.gblk + pl) << 10) | r);
             return;
         }
         const uint32_t nm = (pc[Lo::W_MISC] >> 16) & 0xFFu;
         const uint32_t e = (nadd + (nm & 1u) + 1u) >> 1;  // record words a winner adds (elect_key)
         const uint64_t g = l_index(f, P.Lmask);
-        const unsigned long long v0 = __hip_atomic_load(&P.LXY[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long v0 = __hip_atomic_load(&P.ET[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         P.lslot[q] = seen_contains(P.seen, f) ? LS_SEEN
-                                              : elect_slot<MX>(P.LXY, P.L, P.wacc, P.Lmask, P.epoch, f, q, e, g, v0);
+                                              : elect_slot<MX>(P.ET, P.wacc, P.Lmask, P.epoch, f, q, e, g, v0);
     });
     if (P.route && P.ocnt) {
         __syncthreads();
@@ -2528,7 +2532,7 @@ __global__ __launch_bounds__(256) void k_insert_winners(KParams P) {
         const uint64_t q = pl * (uint64_t)MX + r;
         const uint32_t g = P.lslot[q];
         if (g >= LS_ELECT) return;
-        const bool w = elect_q(P.L[g]) == (uint32_t)q;
+        const bool w = elect_q(P.ET[g].k) == (uint32_t)q;
         if (w) seen_insert(P.seen, P.fp[q]);
         if (P.split & 4) P.lslot[q] = w ? LS_WIN : LS_SEEN;  // the verdict: the commit needs no election word
     });
@@ -2964,7 +2968,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
         // (slots past the parent's t successors hold a stale lslot from an earlier chunk: never an index)
         // (verdicts in lslot -- sharded round, or a split chunk after k_insert_winners -- need no election word)
         const bool verdict = P.route || (P.split & 4);
-        const unsigned long long L0 = (!verdict && (uint32_t)lane < t && g0 < LS_ELECT) ? P.L[g0] : 0ull;
+        const unsigned long long L0 = (!verdict && (uint32_t)lane < t && g0 < LS_ELECT) ? P.ET[g0].k : 0ull;
         // and the staged rows of the first 64 slots that may win (new fingerprints; in a sharded
         // round the owner's verdict is already known): a speculative read instead of a third round
         // trip once the election words are in
@@ -3003,7 +3007,7 @@ __global__ __launch_bounds__(64, (N <= 3 && MR == 1) ? RMC_N3_COMMIT_WAVES : 1) 
             bool win = false;
             if (r < t) {
                 const uint32_t g = r0 == 0 ? g0 : P.lslot[q];
-                win = verdict ? g == LS_WIN : (g < LS_ELECT && elect_q(r0 == 0 ? L0 : P.L[g]) == (uint32_t)q);
+                win = verdict ? g == LS_WIN : (g < LS_ELECT && elect_q(r0 == 0 ? L0 : P.ET[g].k) == (uint32_t)q);
             }
             const uint64_t m = __ballot(win);
             PHASE(2);
@@ -3421,7 +3425,7 @@ __global__ __launch_bounds__(64) void k_commit_finish(KParams P) {
 // waits in lslot for k_local_flags.  Successors other shards own are marked LS_ELECT and left to
 // the exchange (their verdicts arrive by k_scatter_win).
 template <int MX>
-__global__ __launch_bounds__(256) void k_local_elect(KParams P, Seen seen, ulonglong2 *OT, unsigned long long *OK,
+__global__ __launch_bounds__(256) void k_local_elect(KParams P, Seen seen, ESlot *OT,
                                                      uint64_t mask, uint32_t round, uint32_t W, uint32_t self,
                                                      uint64_t g0) {
     each_successor<MX>(P, [&](uint64_t pl, uint32_t r) {
@@ -3429,7 +3433,7 @@ __global__ __launch_bounds__(256) void k_local_elect(KParams P, Seen seen, ulong
         const ulonglong2 f = P.fp[q];
         P.lslot[q] = fp_owner(f, W) != self ? LS_ELECT
                      : seen_contains(seen, f) ? LS_SEEN
-                                              : owner_bid(OT, OK, mask, round + 1u, f, ((g0 + pl) << 10) | r);
+                                              : owner_bid(OT, mask, round + 1u, f, ((g0 + pl) << 10) | r);
     });
 }
 
@@ -3437,7 +3441,7 @@ __global__ __launch_bounds__(256) void k_local_elect(KParams P, Seen seen, ulong
 // LS_SEEN), each winner into the seen set and counted on its parent as k_scatter_win counts a
 // received verdict (wacc = winners | extra words << 12), *inserted counting them.
 template <int MX, int SW4>
-__global__ __launch_bounds__(256) void k_local_flags(KParams P, Seen seen, const unsigned long long *OK, uint32_t round,
+__global__ __launch_bounds__(256) void k_local_flags(KParams P, Seen seen, const ESlot *OT, uint32_t round,
                                                      uint32_t W, uint32_t self, uint64_t g0,
                                                      unsigned long long *inserted) {
     const uint32_t tag = round + 1u;
@@ -3446,7 +3450,7 @@ __global__ __launch_bounds__(256) void k_local_flags(KParams P, Seen seen, const
         const uint64_t q = pl * (uint64_t)MX + r;
         const uint32_t g = P.lslot[q];
         if (g == LS_ELECT || g == LS_SEEN) return;  // another shard's, or seen: nothing to decide
-        const bool w = OK[g] == owner_key(tag, ((g0 + pl) << 10) | r);
+        const bool w = OT[g].k == owner_key(tag, ((g0 + pl) << 10) | r);
         P.lslot[q] = w ? LS_WIN : LS_SEEN;
         if (w) {
             seen_insert(seen, P.fp[q]);
@@ -3536,18 +3540,18 @@ struct Launch {
                            dim3(256), 0, s, P);
         hipLaunchKernelGGL((k_commit_finish<MX, Spec<N, V, MR>::RECW_MAX>), dim3(1), dim3(64), 0, s, P);
     }
-    static void local_elect(const KParams &P, uint64_t np, Seen seen, ulonglong2 *OT, unsigned long long *OK,
+    static void local_elect(const KParams &P, uint64_t np, Seen seen, ESlot *OT,
                             uint64_t mask, uint32_t round, uint32_t W, uint32_t self, uint64_t g0, hipStream_t s) {
         const uint64_t blocks = (np + 255) / 256;  // a wave per 64 parents (each_successor)
         hipLaunchKernelGGL((k_local_elect<MX>), dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u),
-                           dim3(256), 0, s, P, seen, OT, OK, mask, round, W, self, g0);
+                           dim3(256), 0, s, P, seen, OT, mask, round, W, self, g0);
     }
-    static void local_flags(const KParams &P, uint64_t np, Seen seen, const unsigned long long *OK, uint32_t round,
+    static void local_flags(const KParams &P, uint64_t np, Seen seen, const ESlot *OT, uint32_t round,
                             uint32_t W, uint32_t self, uint64_t g0, unsigned long long *inserted, hipStream_t s) {
         const uint64_t blocks = (np + 255) / 256;
         hipLaunchKernelGGL((k_local_flags<MX, Spec<N, V, MR>::SW4>),
                            dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u), dim3(256), 0, s, P,
-                           seen, OK, round, W, self, g0, inserted);
+                           seen, OT, round, W, self, g0, inserted);
     }
     static void fps(const KParams &P, uint64_t n, hipStream_t s) {
         hipLaunchKernelGGL((k_fp_states<N, V, MR>), dim3(grid_for(n)), dim3(64), 0, s, P, n);
@@ -3620,6 +3624,14 @@ __global__ __launch_bounds__(256) void k_rebase(const uint64_t *__restrict__ in,
 static inline unsigned grid256(uint64_t n) {
     const uint64_t b = (n + 255) / 256, cap = 256ull * 16ull;
     return (unsigned)(b < cap ? (b ? b : 1) : cap);
+}
+
+__global__ __launch_bounds__(256) void k_eslot_clear(ESlot *t, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        t[i] = ESlot{0ull, 0ull, ~0ull, 0ull};
+}
+void launch_eslot_clear(ESlot *t, uint64_t n, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(k_eslot_clear, dim3(grid256(n)), dim3(256), 0, s, t, n);
 }
 
 void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, Seen dst, hipStream_t s) {
@@ -3715,12 +3727,12 @@ __global__ __launch_bounds__(256) void k_route_place(const ulonglong2 *__restric
 // Owner: the received successors of the round -- bids (owner_bid) by k_owner_elect, and by the
 // owner's own successors in k_local_elect.
 __global__ __launch_bounds__(256) void k_owner_elect(const XItem *__restrict__ it, uint64_t R, Seen seen,
-                                                     ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
+                                                     ESlot *OT, uint64_t mask,
                                                      uint32_t round, uint32_t *__restrict__ rslot) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
         const XItem e = it[i];
         const ulonglong2 f = make_ulonglong2(e.x, e.y);
-        rslot[i] = seen_contains(seen, f) ? LS_SEEN : owner_bid(OT, OK, mask, round + 1u, f, e.key);
+        rslot[i] = seen_contains(seen, f) ? LS_SEEN : owner_bid(OT, mask, round + 1u, f, e.key);
     }
 }
 
@@ -3728,14 +3740,14 @@ __global__ __launch_bounds__(256) void k_owner_elect(const XItem *__restrict__ i
 // before); each winner goes into the seen set, *inserted counts them.
 __global__ __launch_bounds__(256) void k_owner_flags(const XItem *__restrict__ it, uint64_t R,
                                                      const uint32_t *__restrict__ rslot,
-                                                     const unsigned long long *__restrict__ OK, uint32_t round, Seen seen,
+                                                     const ESlot *__restrict__ OT, uint32_t round, Seen seen,
                                                      uint32_t *__restrict__ flag, unsigned long long *inserted) {
     const uint32_t tag = round + 1u;
     uint32_t mine = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t g = rslot[i];
         const XItem e = it[i];
-        const bool w = g != LS_SEEN && OK[g] == owner_key(tag, e.key);
+        const bool w = g != LS_SEEN && OT[g].k == owner_key(tag, e.key);
         flag[i] = w ? 1u : 0u;
         if (w) {
             seen_insert(seen, make_ulonglong2(e.x, e.y));
@@ -3798,14 +3810,14 @@ void launch_route_place(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, 
         hipLaunchKernelGGL(k_route_place, dim3(grid256(np)), dim3(256), 0, s, fp, cnt, np, maxsucc, W, cursor, g0, items,
                            perm, self);
 }
-void launch_owner_elect(const XItem *it, uint64_t R, Seen seen, ulonglong2 *OT, unsigned long long *OK, uint64_t mask,
+void launch_owner_elect(const XItem *it, uint64_t R, Seen seen, ESlot *OT, uint64_t mask,
                         uint32_t round, uint32_t *rslot, hipStream_t s) {
-    if (R) hipLaunchKernelGGL(k_owner_elect, dim3(grid256(R)), dim3(256), 0, s, it, R, seen, OT, OK, mask, round, rslot);
+    if (R) hipLaunchKernelGGL(k_owner_elect, dim3(grid256(R)), dim3(256), 0, s, it, R, seen, OT, mask, round, rslot);
 }
-void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const unsigned long long *OK, uint32_t round,
+void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const ESlot *OT, uint32_t round,
                         Seen seen, uint32_t *flag, unsigned long long *inserted, hipStream_t s) {
     if (R)
-        hipLaunchKernelGGL(k_owner_flags, dim3(grid256(R)), dim3(256), 0, s, it, R, rslot, OK, round, seen, flag,
+        hipLaunchKernelGGL(k_owner_flags, dim3(grid256(R)), dim3(256), 0, s, it, R, rslot, OT, round, seen, flag,
                            inserted);
 }
 void launch_scatter_win(const uint32_t *perm, const uint32_t *flag, uint64_t G, const uint4 *score, uint32_t sw4,

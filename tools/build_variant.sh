@@ -15,10 +15,12 @@ case "$1" in
   iw*) FLAGS="-DRMC_ITEMS_WAVES=${1#iw}" ;;
   # ... and its parents per batch (e.g. pb32)
   pb*) FLAGS="-DRMC_ITEMS_PB=${1#pb}" ;;
+  # the fused expansion without its self-loop shortcut (round 4's behaviour)
+  noskip) FLAGS="-DRMC_FUSED_SKIPSELF=0" ;;
   # n = 3 occupancy: expansion waves / SIMD, commit waves / SIMD, grid blocks / CU (e.g. n3w6c4g32)
   n3w*) X=${1#n3w}; W=${X%%c*}; X=${X#*c}; C=${X%%g*}; G=${X#*g}
         FLAGS="-DRMC_N3_WAVES=$W -DRMC_N3_COMMIT_WAVES=$C -DRMC_GRID_PER_CU=$G" ;;
-  *) echo "usage: $0 prof|w1|sw<W>|iw<W>|pb<P>|n3w<W>c<C>g<G>" >&2; exit 2 ;;
+  *) echo "usage: $0 prof|w1|sw<W>|iw<W>|pb<P>|noskip|n3w<W>c<C>g<G>" >&2; exit 2 ;;
 esac
 OUT=build_$1
 mkdir -p "$OUT"
