@@ -2884,6 +2884,9 @@ struct rmc_ctx {
                 flush_trace(o, gid + n);
                 o.nxt_n += n;
                 o.nxt_words += words;
+                // the live frontier after the append: the current level's words not yet reused (a ring at its
+                // budget reuses the expanded rounds' words, consumed_) plus the next level's so far
+                o.peak_words = std::max(o.peak_words, o.cur_words - consumed_[li] + o.nxt_words);
             }
             // an append failure rides on the next round's gathered matrix; after the level's last
             // round it is agreed here
@@ -2905,7 +2908,7 @@ struct rmc_ctx {
         st->new_bytes = level_words * 4;
         for (Shard &s : sh) {
             const uint64_t gid_nxt = s.level_start[L - 1] + s.cur_n;
-            s.peak_words = std::max(s.peak_words, s.cur_words + s.nxt_words);
+            s.peak_words = std::max(s.peak_words, s.nxt_words);  // (the level's rounds counted the rest)
             end_level(s, gid_nxt, L);
             if (!s.cur_n) s.level_start.push_back(gid_nxt);  // every shard keeps the same level count
         }

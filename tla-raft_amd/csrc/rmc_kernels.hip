@@ -3418,6 +3418,18 @@ __global__ __launch_bounds__(64) void k_commit_finish(KParams P) {
     finish_level<MX, RECW_MAX>(P);
 }
 
+// a block's counts into one global counter: one atomic per block, not per wave (every block of a
+// launch adds into the same word -- per-wave atomics on it cost ~0.7 s over Raft.cfg's rounds)
+__device__ __forceinline__ void block_count_add(uint32_t mine, unsigned long long *total) {
+    __shared__ uint32_t blk;
+    if (threadIdx.x == 0) blk = 0u;
+    __syncthreads();
+    for (int d = 32; d >= 1; d >>= 1) mine += __shfl_xor(mine, d, 64);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&blk, mine);
+    __syncthreads();
+    if (threadIdx.x == 0 && blk) atomicAdd(total, (unsigned long long)blk);
+}
+
 // ---- sharded round: the owner's election (W > 1, and the one-rank rehearsal) -------------------
 
 // Owner's own successors (fingerprint owner == self), a lane each: they bid in the round's table
@@ -3460,8 +3472,7 @@ __global__ __launch_bounds__(256) void k_local_flags(KParams P, Seen seen, const
             mine++;
         }
     });
-    for (int d = 32; d >= 1; d >>= 1) mine += __shfl_xor(mine, d, 64);
-    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(inserted, (unsigned long long)mine);
+    block_count_add(mine, inserted);
 }
 
 // split chunks: the item-parallel expansion (k_expand_items; RMC_SPLIT_ITEMS=0: the wave-per-parent one)
@@ -3754,8 +3765,7 @@ __global__ __launch_bounds__(256) void k_owner_flags(const XItem *__restrict__ i
             mine++;
         }
     }
-    for (int d = 32; d >= 1; d >>= 1) mine += __shfl_xor(mine, d, 64);
-    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(inserted, (unsigned long long)mine);
+    block_count_add(mine, inserted);
 }
 
 // Source: the owners' verdicts back on the successor slots (lslot = LS_WIN / LS_SEEN), and each

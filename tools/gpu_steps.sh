@@ -6,6 +6,7 @@
 #   prof_raftcfg rocprofv3 kernel stats of the same
 #   bench        bench.py default line              prof_bench  rocprofv3 kernel stats of bench (configs[1])
 #   c4           configs[3] as deep as one GPU goes  rccl1       Raft.cfg through a one-rank RCCL communicator
+#   prof_rccl1   rocprofv3 kernel stats of the rccl1 run
 #   c4split      configs[3] on one GPU with the 48 GB seen set / 200 GB ring split
 #   n4e3         4 servers, 1 value, MaxElection 3 as deep as one GPU goes (DESIGN.md section 9's E2->E3 factor)
 #   pmc_raftcfg  PMC passes over Raft.cfg's first 40 expansions + tools/pmc_scale_report.py
@@ -41,6 +42,8 @@ for s in "$@"; do
            tail -4 "$O/n4e3.log" ;;
     n4e3split) timeout -k 10 420 python -u tools/explore.py 4 1 3 3 --seen-mem-gb ${SEEN_GB:-120} --frontier-mem-gb ${RING_GB:-140} --budget 360 > "$O/n4e3split.log" 2>&1 || { tail -20 "$O/n4e3split.log"; exit 1; }
            tail -4 "$O/n4e3split.log" ;;
+    prof_rccl1) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof_rccl1" -o run -- python3 "$R/tools/explore.py" 3 2 3 3 --rccl1 --budget 200 > "$O/prof_rccl1.log" 2>&1 || { tail -20 "$O/prof_rccl1.log"; exit 1; }
+           grep RESULT "$O/prof_rccl1.log"; find "$O/prof_rccl1" -name '*kernel_stats.csv' -exec head -24 {} \; ;;
     rccl1) timeout -k 10 300 python -u tools/explore.py 3 2 3 3 --rccl1 --budget 200 > "$O/rccl1.log" 2>&1 || { tail -5 "$O/rccl1.log"; exit 1; }
            tail -4 "$O/rccl1.log" ;;
     pmc_raftcfg) OUT=$O/pmc_raftcfg CFG="3 2 3 3 --levels 40" LIMIT=150 bash tools/pmc_scale.sh || exit 1
