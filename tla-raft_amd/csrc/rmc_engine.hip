@@ -1922,16 +1922,19 @@ struct rmc_ctx {
             trace_restart(s);
             // chunks of many parents probe and elect in a pass of their own, a lane per successor
             const bool split = split_min && np_ >= split_min;
+            // a split chunk's winners go into the seen set in its commit (k_commit_items reads the
+            // election words itself: no k_insert_winners pass) when the items commit takes its slots
+            const bool fold = split && nzlist && fold_insert && ks.maxsucc <= 256;
             auto params = [&] {
                 KParams Q = chunk_params(s);
                 Q.p_begin = p0; Q.p_end = p1; Q.next_base = s.nxt_n; Q.next_wbase = s.nxt_words;
                 Q.gid_next_base = gid_nxt; Q.gid_parent_base = gid_cur;
                 Q.Lmask = Lcap - 1;
                 Q.epoch = s.epoch;
-                Q.split = split ? (split_insert ? split_flags : 1) : 0;
+                Q.split = split ? (fold ? 1 : (split_insert ? split_flags : 1)) : 0;
                 Q.plist = split && nzlist ? s.plist : nullptr;
                 // (a split chunk's self-loops are staged after the successors to fingerprint)
-                Q.hcnt = split && split_insert && split_flags == 7 && nzlist ? s.hcnt : nullptr;
+                Q.hcnt = split && nzlist && (fold || (split_insert && split_flags == 7)) ? s.hcnt : nullptr;
                 s.chunk_sep = Q.hcnt != nullptr;
                 return Q;
             };
@@ -1959,10 +1962,10 @@ struct rmc_ctx {
             }
             trace_fence(s);
             // (timed with the winner count: PH_OTHER stays the probe pass alone)
-            if (split && split_insert) timed(PH_DEDUP, [&] { ks.insert(params(), np_, stream); });
+            if (split && split_insert && !fold) timed(PH_DEDUP, [&] { ks.insert(params(), np_, stream); });
             // + chunk summary; a split chunk's winners a lane per successor slot of its parents with winners
             timed(PH_MAT, [&] {
-                if (split && nzlist && split_insert && split_flags == 7) ks.commit_split(params(), np_, stream);
+                if (split && nzlist && (fold || (split_insert && split_flags == 7))) ks.commit_split(params(), np_, stream);
                 else ks.commit(params(), stream);
             });
             HIPCHK(hipMemcpyAsync(s.hsum, s.sum, (SUM_SELF + 1) * 8, hipMemcpyDeviceToHost, stream));
@@ -2034,6 +2037,9 @@ struct rmc_ctx {
     // KParams.split of such chunks (measurement knob): 7 = verdicts in lslot for the commit, 3 = the
     // commit reads the election words itself
     const int split_flags = env_int("RMC_SPLIT_FLAGS", 7, 3, 7) == 3 ? 3 : 7;
+    // split chunks whose commit is k_commit_items: the commit tests the election words and inserts the
+    // winners itself (RMC_FOLD_INSERT=0: the k_insert_winners pass and verdicts, as round 4)
+    const bool fold_insert = env_int("RMC_FOLD_INSERT", 1, 0, 1) != 0;
     const int dl_group = env_int("RMC_DL_GROUP", 2, 1, 64);
     const int dl_ahead = env_int("RMC_DL_AHEAD", 2, 1, 64);
     const int dl_query_us = env_int("RMC_DL_QUERY_US", 2000, 0, 1 << 30);

@@ -3308,7 +3308,11 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
                 for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < b && sSl[j + st] <= i) ? j + st : j;
                 const uint32_t r = i - sSl[j];
                 const uint64_t q = (uint64_t)sPl[j] * MX + r;
-                if (P.lslot[q] == LS_WIN) {
+                // the verdict (LS_WIN: k_insert_winners', an owner's), or -- no insert pass -- the election word
+                const uint32_t g = P.lslot[q];
+                const bool win = (P.route || (P.split & 4)) ? g == LS_WIN
+                                                            : (g < LS_ELECT && elect_q(P.ET[g].k) == (uint32_t)q);
+                if (win) {
                     const uint4 *src = P.score + q * (uint64_t)SW4;
                     uint4 st4[SW4];
 #pragma unroll
@@ -3345,6 +3349,7 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
                 const uint32_t pl = sPl[j];
                 const uint64_t p = P.p_begin + pl;
                 const uint64_t out = P.next_base + sOut[j] + ord;
+                if (!P.route && !(P.split & 2)) seen_insert(P.seen, P.fp[(uint64_t)pl * MX + r]);  // (no insert pass)
                 const uint64_t wd = P.next_wbase + sWd[j] + wofs;  // level-relative
                 const uint64_t rs = ring_wrap(P.nbase + wd, P.rcap);
                 P.noff[out] = wd;
@@ -3484,15 +3489,6 @@ static bool split_items() {
     return on;
 }
 
-// split-chunk commits: records staged in LDS (k_commit_items; RMC_COMMIT_ITEMS=0: k_commit_split)
-static bool commit_items() {
-    static const bool on = [] {
-        const char *v = std::getenv("RMC_COMMIT_ITEMS");
-        return !(v && v[0] == '0');
-    }();
-    return on;
-}
-
 static inline unsigned grid_for(uint64_t n) {
     const uint64_t cap = 256ull * RMC_GRID_PER_CU;  // one-wave blocks per CU (default 32) on 256 CUs
     return (unsigned)(n < cap ? (n ? n : 1) : cap);
@@ -3539,7 +3535,7 @@ struct Launch {
     static void commit_split(const KParams &P, uint64_t np, hipStream_t s) {
         const uint64_t blocks = (np + 255) / 256;  // a wave per 64 parents with winners (at most np of them)
         if constexpr (MX <= XB_THREADS) {
-            if (commit_items()) {  // a block per 64 parents with winners, records in LDS
+            {  // a block per 64 parents with winners, records in LDS
                 const uint64_t nbat = (np + 63) / 64;
                 hipLaunchKernelGGL((k_commit_items<N, V, MR, MX>), dim3((unsigned)(nbat < 2048 ? (nbat ? nbat : 1) : 2048)),
                                    dim3(XB_THREADS), 0, s, P);
