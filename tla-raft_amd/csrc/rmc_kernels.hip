@@ -1358,6 +1358,74 @@ __device__ __forceinline__ uint64_t msg_hash_half(uint32_t info, int f) {
              : mix64(body * 0x9e3779b97f4a7c15ULL + SEED_MSG);
 }
 
+// A staged successor's fingerprint (rmc_spec.h): its content matrix rebuilt from the parent's decoded
+// core pc, the parent's message-hash sums per server pair (mp(pi) = {M_0, M_1} of pair pi) and the
+// staged row (sa, sb, sc: the acting server's row and the added messages), then the coset minimum
+// (ai(a, id): the info word of added message a, id its message id)
+template <int N, int V, int MR, class FM, class FA>
+__device__ __forceinline__ ulonglong2 staged_fp(const KParams &P, const uint32_t *pc, FM mp, FA ai, const uint4 sa,
+                                                const uint4 sb, const uint4 sc, const uint64_t (*sK)[N * N]) {
+    using S = Spec<N, V, MR>;
+    using Lo = Layout<N, V>;
+    uint32_t c[Lo::NW];
+    unstage_core<N, V>(pc, sa, sb, c);
+    const uint32_t sv = sa.x >> 20, nadd = sb.z >> 16;
+    // the added messages' hashes toward each destination (all from the acting server)
+    uint64_t ad0[N], ad1[N];
+#pragma unroll
+    for (int j = 0; j < N; j++) { ad0[j] = 0; ad1[j] = 0; }
+    const uint32_t aid[4] = {sb.w & 0xFFFFu, sb.w >> 16, sc.x & 0xFFFFu, sc.x >> 16};
+#pragma unroll
+    for (int a = 0; a < S::NADD; a++) {
+        if ((uint32_t)a >= nadd) break;
+        const uint32_t inf = ai(a, aid[a]);
+        const uint64_t g0 = msg_hash_half(inf, 0), g1 = msg_hash_half(inf, 1);  // (= the table's gmsg)
+        const uint32_t d = mi_dst(inf);
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            ad0[j] += (uint32_t)j == d ? g0 : 0ull;
+            ad1[j] += (uint32_t)j == d ? g1 : 0ull;
+        }
+    }
+    // the successor's content matrix and its servers' signatures
+    uint64_t C0[N * N], C1[N * N], sig[N];
+#pragma unroll
+    for (int t = 0; t < N; t++) {
+        sig[t] = 0;
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            uint64_t m0 = 0, m1 = 0;
+            if (t != j) {
+                const ulonglong2 m = mp(pair_index(N, t, j));
+                m0 = m.x + ((uint32_t)t == sv ? ad0[j] : 0ull);
+                m1 = m.y + ((uint32_t)t == sv ? ad1[j] : 0ull);
+            }
+            C0[t * N + j] = content<N>(0, t, j, c, c[Lo::W_LOG + t], c[Lo::W_MI + t], c[Lo::W_NI + t], m0);
+            C1[t * N + j] = content<N>(1, t, j, c, c[Lo::W_LOG + t], c[Lo::W_MI + t], c[Lo::W_NI + t], m1);
+            sig[t] += C1[t * N + j];
+        }
+    }
+    const uint32_t rk = P.t.np > 1 ? coset_ranks<N>(sig) : coset_ident<N>(), K = coset_size<N>(rk);
+    ulonglong2 best = make_ulonglong2(~0ull, ~0ull);
+    for (uint32_t k = 0; k < K; k++) {
+        const ulonglong2 h = hash_at<N>(
+            coset_img<N>(rk, k), [&](int f, int a, int b) { return f ? C1[a * N + b] : C0[a * N + b]; },
+            [&](int f, uint32_t a, uint32_t b) { return sK[f][a * N + b]; });
+        if (lex_less(h, best)) best = h;
+    }
+    return make_ulonglong2(best.x | 1ull, best.y);
+}
+
+// The fused election of a new fingerprint (the seen set is read-only in the launch): its slot q's
+// verdict LS_SEEN, or the election slot it bid in.  e: the record words a winner adds (elect_key)
+template <int MX>
+__device__ __forceinline__ uint32_t probe_elect(const KParams &P, const ulonglong2 f, uint64_t q, uint32_t e) {
+    // the election slot's first word goes out with the seen-set probe: one round trip fewer
+    const uint64_t g = l_index(f, P.Lmask);
+    const unsigned long long v0 = __hip_atomic_load(&P.ET[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return seen_contains(P.seen, f) ? LS_SEEN : elect_slot<MX>(P.ET, P.wacc, P.Lmask, P.epoch, f, q, e, g, v0);
+}
+
 template <int N, int MR, int MODE, bool BFV>
 constexpr int expand_waves() {
     return MODE == M_SPLIT ? ((MR == 1 && !BFV) ? RMC_SPLIT_WAVES : RMC_WIDE_WAVES)
@@ -1613,13 +1681,7 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
                 const uint64_t q = pl * (uint64_t)MX + sRq[lo];
                 P.fp[q] = f;
                 if (P.route) return;  // sharded round: the fingerprint's owner probes and elects
-                const uint32_t e = ((uint32_t)sNa[lo] + (W.nm & 1u) + 1u) >> 1;
-                // the election slot's first word goes out with the seen-set probe: one round trip
-                // fewer for a new fingerprint
-                const uint64_t g0 = l_index(f, P.Lmask);
-                const unsigned long long v0 = __hip_atomic_load(&P.ET[g0].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                P.lslot[q] = seen_contains(P.seen, f) ? LS_SEEN
-                                                      : elect_slot<MX>(P.ET, P.wacc, P.Lmask, P.epoch, f, q, e, g0, v0);
+                P.lslot[q] = probe_elect<MX>(P, f, q, ((uint32_t)sNa[lo] + (W.nm & 1u) + 1u) >> 1);
             } else {
                 P.fp[lo] = f;
             }
@@ -1778,6 +1840,16 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
 #define RMC_ITEMS_PB 64
 #endif
 constexpr int XB_PARENTS = RMC_ITEMS_PB;  // parents per batch (<= 64: a lane of wave 0 each)
+// ... of a fused level: levels of a few thousand parents (configs[1]) need more blocks than 64-parent
+// batches make to fill 256 CUs
+#ifndef RMC_FUSED_PB
+#define RMC_FUSED_PB 16
+#endif
+constexpr int XF_PARENTS = RMC_FUSED_PB;
+#ifndef RMC_FUSED_WAVES
+#define RMC_FUSED_WAVES 4  // n <= 3: registers cut for 4 waves per SIMD, 4 blocks per CU (the compiler's choice: 3;
+                           // n >= 4 would spill)
+#endif
 constexpr int XB_THREADS = 256;  // threads per block = items per evaluation round at most
 
 // votedFor, currentTerm, role, commitIndex, Len(logs) of server s and s itself: staging word 0
@@ -1803,6 +1875,7 @@ struct RowSucc {
     uint32_t key;  // KEY_NONE: disabled
     uint32_t nadd;
     uint32_t add[NADD];
+    uint32_t ainf[NADD];  // the added messages' info words (a fused level hashes them; dead code in a split chunk)
     bool self;     // the successor is the parent itself (FollowerAcceptEntry changing nothing)
 };
 
@@ -1868,6 +1941,7 @@ __device__ __forceinline__ void item_msg(const KParams &P, const uint32_t *pc, c
         if (ids_contain<S::MCAP>(ids, nm, pid)) return;
         o.w0 = row_w0(src, ct, role, ci, ll, s);
         o.add[0] = pid; o.nadd = 1;
+        o.ainf[0] = minfo(VRESP, s, src, mt, 0, 0, 0, 0, 0, 0);
         o.key = slot_key(s, RV, k);
         return;
     }
@@ -1893,12 +1967,14 @@ __device__ __forceinline__ void item_msg(const KParams &P, const uint32_t *pc, c
             o.w0 = row_w0(vf, ct, role, nci, nll, s);
             const bool has = ids_contain<S::MCAP>(ids, nm, pid);
             if (!has) { o.add[0] = pid; o.nadd = 1; }
+            o.ainf[0] = minfo(ARESP, s, src, mt, pli + ent, 1, 0, 0, 0, 0);
             // (no new entry, no truncation, no commit, the response already sent: the parent itself)
             o.self = has && !(truncated || append_new) && nci == ci;
             o.key = slot_key(s, FAE, k);
         } else {
             if (ids_contain<S::MCAP>(ids, nm, pid)) return;
             o.add[0] = pid; o.nadd = 1;
+            o.ainf[0] = minfo(ARESP, s, src, mt, pli, 0, 0, 0, 0, 0);
             o.key = slot_key(s, FRE, k);
         }
         return;
@@ -1972,8 +2048,13 @@ __device__ __forceinline__ void item_slot(const KParams &P, const uint32_t *pc, 
 #pragma unroll
         for (int i = 0; i < N - 1; i++) {
             if (!ids_contain<S::MCAP>(ids, nm, sid[i])) {
+                const uint32_t p = (uint32_t)i < s ? (uint32_t)i : (uint32_t)i + 1u;
+                const uint32_t inf = minfo(VREQ, s, p, term, ll, llt, 0, 0, 0, 0);
 #pragma unroll
-                for (int a = 0; a < S::NADD; a++) o.add[a] = ((uint32_t)a == na) ? sid[i] : o.add[a];
+                for (int a = 0; a < S::NADD; a++) {
+                    o.add[a] = ((uint32_t)a == na) ? sid[i] : o.add[a];
+                    o.ainf[a] = ((uint32_t)a == na) ? inf : o.ainf[a];
+                }
                 na++;
             }
         }
@@ -2024,6 +2105,7 @@ __device__ __forceinline__ void item_slot(const KParams &P, const uint32_t *pc, 
         if (ids_contain<S::MCAP>(ids, nm, id)) return;  // m \notin msgs
         o.pend = pend | (1u << pb);
         o.add[0] = id;
+        o.ainf[0] = minfo(AREQ, s, dst, ct, pli, plt, ci, ent, eb & 15u, eb >> 4);
         o.nadd = 1;
         o.key = slot_key(s, LAE, dst);
         return;
@@ -2087,11 +2169,12 @@ __device__ __forceinline__ uint32_t slot_class(uint32_t t) {
          : t == 2 + (uint32_t)V + (N - 1) ? IC_LCC : IC_RS;
 }
 
-template <int N, int V, int MR, bool BFV>
-__global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KParams P) {
+template <int N, int V, int MR, bool BFV, bool FUSE, int PB>
+__global__ __launch_bounds__(XB_THREADS, FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) : RMC_ITEMS_WAVES) void k_expand_items(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
-    constexpr int PB = XB_PARENTS, NT = XB_THREADS;
+    constexpr int NT = XB_THREADS;
+    static_assert(PB >= 2 && PB <= 64 && (PB & (PB - 1)) == 0, "parents per batch: a power of two, a lane of wave 0 each");
     constexpr int CCW = S::CCW, RECW = S::RECW_MAX, NW = Lo::NW, NWP = (NW + 3) / 4 * 4;
     constexpr int MX = S::MAXS + (BFV ? S::MCAP : 0);
     constexpr int NCI = BFV ? 2 : 1;  // candidates of a message item
@@ -2102,6 +2185,7 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
     __shared__ uint32_t sRec[PB * RECW];           // the batch's records, as in the ring
     __shared__ uint32_t sCore[PB * NWP];           // their nibble cores
     __shared__ uint8_t sMI[PB * S::MCAP];          // per message of the batch: its class (15: none)
+    __shared__ uint32_t sInf[FUSE ? PB * S::MCAP : 1];  // fused level: ... and its info word (one round trip less)
     __shared__ uint32_t sVp[PB * N];               // per parent and server: VoteResps to it in its term (tla:160-164)
     __shared__ uint32_t sOff[PB];                  // record's first word in sRec
     __shared__ uint32_t sItm[PB + 1], sMsc[PB + 1];  // items / messages: exclusive scans over the batch
@@ -2111,13 +2195,27 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
     __shared__ uint32_t sSelf[PB];                 // self-loops (P.hcnt: staged nowhere, never fingerprinted)
     __shared__ uint32_t sCc[IC_N];                 // the round's items per class
     // the batch's hash sums (until the hash context is written), then the rounds' item lists and keys
-    constexpr int UM = 2 * PB * NPR * 8, UQ = IC_N * NT * 2 + NT * NCI * 2;
+    // (a fused level keeps the sums to the end: its lanes fingerprint their successors themselves)
+    constexpr int UM = FUSE ? 0 : 2 * PB * NPR * 8, UQ = IC_N * NT * 2 + NT * NCI * 2;
     __shared__ __attribute__((aligned(16))) unsigned char sU[UM > UQ ? UM : UQ];
-    unsigned long long *sM0 = reinterpret_cast<unsigned long long *>(sU), *sM1 = sM0 + PB * NPR;
+    __shared__ unsigned long long sMh[FUSE ? 2 * PB * NPR : 1];
+    __shared__ uint64_t sK[2][FUSE ? N * N : 1];   // fused level: position constants K_f[a][b]
+    unsigned long long *sM0 = FUSE ? sMh : reinterpret_cast<unsigned long long *>(sU), *sM1 = sM0 + PB * NPR;
     uint16_t *sQ = reinterpret_cast<uint16_t *>(sU);   // [IC_N][NT] item codes by class
     uint16_t *sKey = sQ + IC_N * NT;                    // [NT * NCI] the round's enabled keys, per parent at its items' offset
     __shared__ uint32_t sSpan;
     const int tid = threadIdx.x;
+    if constexpr (FUSE) {
+        // device loop: the level from the control block, the levels committed so far to the host as
+        // this one starts (as k_expand<M_FUSED>); grids are sized on a bound of the level
+        if (!level_args(P)) return;
+        if (P.hloop && blockIdx.x == 0 && tid == 0)
+            __hip_atomic_store(&P.hloop->done, P.done_levels, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (tid < 2 * N * N) {  // (read after the batch loop's first barrier)
+            const int f = tid / (N * N), a = (tid / N) % N, b = tid % N;
+            sK[f][a * N + b] = P.t.seeds[f * SEEDS_PER_F + a * MAXN + b];
+        }
+    }
     const uint64_t np = P.p_end - P.p_begin;
     PHASE_DECL
     for (uint64_t b0 = (uint64_t)blockIdx.x * PB; b0 < np; b0 += (uint64_t)gridDim.x * PB) {
@@ -2199,13 +2297,14 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
             if (mi_type(inf) == VRESP && mi_term(inf) == ct) atomicAdd(&sVp[j * N + dst], 1u);
             const uint32_t c = msg_class(inf, ct, nib(pc[Lo::W_ROLE], dst));
             sMI[m] = (uint8_t)(c == IC_DEAD ? 15u : c);
+            if constexpr (FUSE) sInf[m] = inf;
             if (c != IC_DEAD) atomicAdd(&sLive[j], 1u);
         }
         __syncthreads();
         PHASE(2);
         // the batch's hash contexts (k_hash_probe): packed core padded to 16 B, then per server pair its
         // sums {M_0 lo, hi, M_1 lo, hi}; the batch's parents are consecutive, so one coalesced range
-        for (uint32_t w = (uint32_t)tid; w < nb * (uint32_t)CTXW; w += NT) {
+        for (uint32_t w = (uint32_t)tid; !FUSE && w < nb * (uint32_t)CTXW; w += NT) {
             const uint32_t j = w / CTXW, k = w % CTXW;
             uint32_t v = 0u;
             if (k < (uint32_t)CC) {
@@ -2279,7 +2378,7 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
                 uint32_t akey = KEY_NONE;
                 if (!(code & 0x80u)) {
                     const uint32_t k = code & 0x7Fu;
-                    const uint32_t inf = P.t.info[ids[k]];
+                    const uint32_t inf = FUSE ? sInf[sMsc[j] + k] : P.t.info[ids[k]];
                     const uint32_t nat = item_msg_nat<N, V>(P, pc, inf);
                     const uint32_t pid = nat != NAT_NONE ? (uint32_t)P.t.nat2id[nat] : 0u;
                     item_msg<N, V, MR, BFV>(P, pc, ids, nmj, k, inf, pid, o, ob, akey);
@@ -2289,7 +2388,7 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
                 }
                 if (akey != KEY_NONE) atomicMin(&sAk[j], akey);
                 const uint32_t kb = (sItm[j] - ibase) * NCI;  // the parent's key list
-                if (o.key != KEY_NONE && o.self && P.hcnt) atomicAdd(&sSelf[j], 1u);
+                if (!FUSE && o.key != KEY_NONE && o.self && P.hcnt) atomicAdd(&sSelf[j], 1u);
                 else if (o.key != KEY_NONE) sKey[kb + atomicAdd(&sCnt[j], 1u)] = (uint16_t)o.key;
                 if (BFV && ob.key != KEY_NONE) sKey[kb + atomicAdd(&sCnt[j], 1u)] = (uint16_t)ob.key;
                 if ((o.key != KEY_NONE && nmj + o.nadd > (uint32_t)S::MCAP)) atomicOr(&P.flags[0], 1u);
@@ -2302,10 +2401,33 @@ __global__ __launch_bounds__(XB_THREADS, RMC_ITEMS_WAVES) void k_expand_items(KP
 #pragma unroll
                 for (int c = 0; c < NCI; c++) {
                     const RowSucc<S::NADD> &x = c ? ob : o;
-                    if (x.key == KEY_NONE || (x.self && P.hcnt)) continue;
+                    if (x.key == KEY_NONE || (!FUSE && x.self && P.hcnt)) continue;
                     uint32_t rank = 0;
                     for (uint32_t e = 0; e < cn; e++) rank += (uint32_t)sKey[kb + e] < x.key ? 1u : 0u;
-                    row_stage<S::NADD>(x, nmj, S::SW4, P.score + (pl * (uint64_t)MX + rank) * (uint64_t)S::SW4);
+                    const uint64_t q = pl * (uint64_t)MX + rank;
+                    if constexpr (FUSE) {
+                        // a fused level: a self-loop takes its slot as seen (the parent is in the seen set);
+                        // any other successor is staged for the commit, fingerprinted from the parent's core
+                        // and hash sums in LDS, probed and elected right here (k_hash_probe's work)
+                        if (x.self) {
+                            P.lslot[q] = LS_SEEN;
+                            continue;
+                        }
+                        uint4 st4[S::SW4];
+                        row_stage<S::NADD>(x, nmj, S::SW4, st4);
+                        uint4 *dst = P.score + q * (uint64_t)S::SW4;
+#pragma unroll
+                        for (int w = 0; w < S::SW4; w++) dst[w] = st4[w];
+                        const unsigned long long *m0 = sM0 + j * NPR, *m1 = sM1 + j * NPR;
+                        const ulonglong2 f = staged_fp<N, V, MR>(
+                            P, sCore + j * NWP, [&](int pi) { return make_ulonglong2(m0[pi], m1[pi]); },
+                            [&](int a, uint32_t) { return x.ainf[a]; }, st4[0], st4[1],
+                            S::SW4 > 2 ? st4[S::SW4 > 2 ? 2 : 0] : make_uint4(0u, 0u, 0u, 0u), sK);
+                        P.fp[q] = f;
+                        P.lslot[q] = probe_elect<MX>(P, f, q, (x.nadd + (nmj & 1u) + 1u) >> 1);
+                    } else {
+                        row_stage<S::NADD>(x, nmj, S::SW4, P.score + q * (uint64_t)S::SW4);
+                    }
                 }
             }
             PHASE(5);
@@ -2448,54 +2570,13 @@ __global__ __launch_bounds__(256) void k_hash_probe(KParams P) {
         uint4 mp[N * (N - 1)];
 #pragma unroll
         for (int k = 0; k < N * (N - 1); k++) mp[k] = cx[CC4 + k];
-        uint32_t pc[Lo::NW], c[Lo::NW];
+        uint32_t pc[Lo::NW];
         decode_core<N, V>(pk, pc);
-        unstage_core<N, V>(pc, sa, sb, c);
-        const uint32_t sv = sa.x >> 20, nadd = sb.z >> 16;
-        // the added messages' hashes toward each destination (all from the acting server)
-        uint64_t ad0[N], ad1[N];
-#pragma unroll
-        for (int j = 0; j < N; j++) { ad0[j] = 0; ad1[j] = 0; }
-        const uint32_t aid[4] = {sb.w & 0xFFFFu, sb.w >> 16, sc.x & 0xFFFFu, sc.x >> 16};
-#pragma unroll
-        for (int a = 0; a < S::NADD; a++) {
-            if ((uint32_t)a >= nadd) break;
-            const uint32_t inf = P.t.info[aid[a]];
-            const ulonglong2 g = P.t.gmsg[aid[a]];
-            const uint32_t d = mi_dst(inf);
-#pragma unroll
-            for (int j = 0; j < N; j++) {
-                ad0[j] += (uint32_t)j == d ? g.x : 0ull;
-                ad1[j] += (uint32_t)j == d ? g.y : 0ull;
-            }
-        }
-        // the successor's content matrix and its servers' signatures
-        uint64_t C0[N * N], C1[N * N], sig[N];
-#pragma unroll
-        for (int t = 0; t < N; t++) {
-            sig[t] = 0;
-#pragma unroll
-            for (int j = 0; j < N; j++) {
-                uint64_t m0 = 0, m1 = 0;
-                if (t != j) {
-                    const uint4 m = mp[pair_index(N, t, j)];
-                    m0 = ((uint64_t)m.y << 32 | m.x) + ((uint32_t)t == sv ? ad0[j] : 0ull);
-                    m1 = ((uint64_t)m.w << 32 | m.z) + ((uint32_t)t == sv ? ad1[j] : 0ull);
-                }
-                C0[t * N + j] = content<N>(0, t, j, c, c[Lo::W_LOG + t], c[Lo::W_MI + t], c[Lo::W_NI + t], m0);
-                C1[t * N + j] = content<N>(1, t, j, c, c[Lo::W_LOG + t], c[Lo::W_MI + t], c[Lo::W_NI + t], m1);
-                sig[t] += C1[t * N + j];
-            }
-        }
-        const uint32_t rk = P.t.np > 1 ? coset_ranks<N>(sig) : coset_ident<N>(), K = coset_size<N>(rk);
-        ulonglong2 best = make_ulonglong2(~0ull, ~0ull);
-        for (uint32_t k = 0; k < K; k++) {
-            const ulonglong2 h = hash_at<N>(
-                coset_img<N>(rk, k), [&](int f, int a, int b) { return f ? C1[a * N + b] : C0[a * N + b]; },
-                [&](int f, uint32_t a, uint32_t b) { return sK[f][a * N + b]; });
-            if (lex_less(h, best)) best = h;
-        }
-        const ulonglong2 f = make_ulonglong2(best.x | 1ull, best.y);
+        const ulonglong2 f = staged_fp<N, V, MR>(P, pc, [&](int pi) {
+            const uint4 m = mp[pi];
+            return make_ulonglong2((uint64_t)m.y << 32 | m.x, (uint64_t)m.w << 32 | m.z);
+        }, [&](int, uint32_t id) { return P.t.info[id]; }, sa, sb, sc, sK);
+        const uint32_t nadd = sb.z >> 16;
         P.fp[q] = f;
         if (P.route) {  // the owners probe and elect; the round's counts per owner (k_route_count's)
             const uint32_t o = fp_owner(f, P.nown);
@@ -2510,11 +2591,7 @@ __global__ __launch_bounds__(256) void k_hash_probe(KParams P) {
             return;
         }
         const uint32_t nm = (pc[Lo::W_MISC] >> 16) & 0xFFu;
-        const uint32_t e = (nadd + (nm & 1u) + 1u) >> 1;  // record words a winner adds (elect_key)
-        const uint64_t g = l_index(f, P.Lmask);
-        const unsigned long long v0 = __hip_atomic_load(&P.ET[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        P.lslot[q] = seen_contains(P.seen, f) ? LS_SEEN
-                                              : elect_slot<MX>(P.ET, P.wacc, P.Lmask, P.epoch, f, q, e, g, v0);
+        P.lslot[q] = probe_elect<MX>(P, f, q, (nadd + (nm & 1u) + 1u) >> 1);
     });
     if (P.route && P.ocnt) {
         __syncthreads();
@@ -3489,6 +3566,16 @@ static bool split_items() {
     return on;
 }
 
+// fused levels (device loop, chunks below the split size): the item-parallel expansion with the
+// fingerprints and election in the same launch (RMC_FUSED_ITEMS=0: k_expand<M_FUSED>, round 4's)
+static bool fused_items() {
+    static const bool on = [] {
+        const char *v = std::getenv("RMC_FUSED_ITEMS");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 static inline unsigned grid_for(uint64_t n) {
     const uint64_t cap = 256ull * RMC_GRID_PER_CU;  // one-wave blocks per CU (default 32) on 256 CUs
     return (unsigned)(n < cap ? (n ? n : 1) : cap);
@@ -3502,13 +3589,19 @@ struct Launch {
         hipLaunchKernelGGL((k_expand<N, V, MR, M_SINGLE, BFV>), dim3(1), dim3(64), bm_bytes(P), s, P);
     }
     static void fused(const KParams &P, hipStream_t s) {
+        if (fused_items() && !P.route) {  // a block per 64 parents, fingerprints and election in the same launch
+            const uint64_t nbat = (P.p_end - P.p_begin + XF_PARENTS - 1) / XF_PARENTS;
+            hipLaunchKernelGGL((k_expand_items<N, V, MR, BFV, true, XF_PARENTS>), dim3((unsigned)(nbat < 8192 ? (nbat ? nbat : 1) : 8192)),
+                               dim3(XB_THREADS), 0, s, P);
+            return;
+        }
         hipLaunchKernelGGL((k_expand<N, V, MR, M_FUSED, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64),
                            bm_bytes(P), s, P);
     }
     static void split(const KParams &P, hipStream_t s) {
         if (split_items()) {
             const uint64_t nbat = (P.p_end - P.p_begin + XB_PARENTS - 1) / XB_PARENTS;
-            hipLaunchKernelGGL((k_expand_items<N, V, MR, BFV>), dim3((unsigned)(nbat < 2048 ? (nbat ? nbat : 1) : 2048)),
+            hipLaunchKernelGGL((k_expand_items<N, V, MR, BFV, false, XB_PARENTS>), dim3((unsigned)(nbat < 2048 ? (nbat ? nbat : 1) : 2048)),
                                dim3(XB_THREADS), 0, s, P);
             return;
         }

@@ -6,22 +6,29 @@
 # Select it with RMC_LIBRARY=<path> (raftmc.load_library).  Needs the default build (make -C tla-raft_amd).
 set -e
 cd "$(dirname "$0")/../tla-raft_amd"
-case "$1" in
-  prof) FLAGS="-DRMC_PHASE_PROF" ;;
-  w1) FLAGS="-DRMC_WIDE_WAVES=1" ;;
+FLAGS=""
+for part in ${1//+/ }; do  # several specs joined by '+', e.g. fpb16+fw4
+case "$part" in
+  prof) FLAGS="$FLAGS -DRMC_PHASE_PROF" ;;
+  w1) FLAGS="$FLAGS -DRMC_WIDE_WAVES=1" ;;
   # the split (no fingerprint) expansion: waves / SIMD its registers are cut for (e.g. sw5)
-  sw*) FLAGS="-DRMC_SPLIT_WAVES=${1#sw}" ;;
+  sw*) FLAGS="$FLAGS -DRMC_SPLIT_WAVES=${part#sw}" ;;
   # the item-parallel split expansion: waves / SIMD its registers are cut for (e.g. iw6)
-  iw*) FLAGS="-DRMC_ITEMS_WAVES=${1#iw}" ;;
+  iw*) FLAGS="$FLAGS -DRMC_ITEMS_WAVES=${part#iw}" ;;
   # ... and its parents per batch (e.g. pb32)
-  pb*) FLAGS="-DRMC_ITEMS_PB=${1#pb}" ;;
+  pb*) FLAGS="$FLAGS -DRMC_ITEMS_PB=${part#pb}" ;;
+  # the fused item-parallel expansion's parents per batch (RMC_FUSED_ITEMS=1; e.g. fpb8)
+  fpb*) FLAGS="$FLAGS -DRMC_FUSED_PB=${part#fpb}" ;;
+  # ... and the waves / SIMD its registers are cut for (e.g. fw4)
+  fw*) FLAGS="$FLAGS -DRMC_FUSED_WAVES=${part#fw}" ;;
   # the fused expansion without its self-loop shortcut (round 4's behaviour)
-  noskip) FLAGS="-DRMC_FUSED_SKIPSELF=0" ;;
+  noskip) FLAGS="$FLAGS -DRMC_FUSED_SKIPSELF=0" ;;
   # n = 3 occupancy: expansion waves / SIMD, commit waves / SIMD, grid blocks / CU (e.g. n3w6c4g32)
-  n3w*) X=${1#n3w}; W=${X%%c*}; X=${X#*c}; C=${X%%g*}; G=${X#*g}
-        FLAGS="-DRMC_N3_WAVES=$W -DRMC_N3_COMMIT_WAVES=$C -DRMC_GRID_PER_CU=$G" ;;
-  *) echo "usage: $0 prof|w1|sw<W>|iw<W>|pb<P>|noskip|n3w<W>c<C>g<G>" >&2; exit 2 ;;
+  n3w*) X=${part#n3w}; W=${X%%c*}; X=${X#*c}; C=${X%%g*}; G=${X#*g}
+        FLAGS="$FLAGS -DRMC_N3_WAVES=$W -DRMC_N3_COMMIT_WAVES=$C -DRMC_GRID_PER_CU=$G" ;;
+  *) echo "usage: $0 prof|w1|sw<W>|iw<W>|pb<P>|fpb<P>|fw<W>|noskip|n3w<W>c<C>g<G>[+...]" >&2; exit 2 ;;
 esac
+done
 OUT=build_$1
 mkdir -p "$OUT"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
