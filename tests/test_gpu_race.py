@@ -81,8 +81,12 @@ def test_single_control_block_fails_under_the_forced_late_block(tmp_path):
     late commit block forced: configs[1] (3 servers, 1 value, MaxElection 2) must fail -- the late block
     takes the next level's parent count, arrives at the next level's counters and leaves them off by
     one (the probe build checks that every counter has re-armed itself when a level finishes; a
-    violation found at that level could otherwise go to the wrong level's summary, round 4's symptom)."""
+    violation found at that level could otherwise go to the wrong level's summary, round 4's symptom).
+    With the item-parallel commit (16 parents a block) the late block's extra arrival can also fire a
+    level's finish before that level's blocks are all in, and the run ends early with wrong counts
+    before any re-arm check: either way the run is not the golden one."""
     g = LEVELS["n3_v1_e2_r3"]
     res = run_worker(1, [{"name": "n3_v1_e2_r3", "cfg": cfg_of(g)}], tmp_path)
     assert not matches(g, res[0], "n3_v1_e2_r3"), "the forced late block went unnoticed"
-    assert "arrival counters" in res[0].get("error", ""), res[0]
+    r = res[0]
+    assert "arrival counters" in r.get("error", "") or (r.get("distinct"), r.get("depth")) != (g["distinct"], g["depth"]), r

@@ -3323,12 +3323,16 @@ __global__ __launch_bounds__(256) void k_commit_split(KParams P) {
 // list (TLC order = slot order), rebuilds the state from the LDS core, writes the record (core, then the
 // parent's ids merged with the added ones, read from LDS), its trace entry (or sidecar) and checks the
 // INVARIANTs.  Outputs are k_commit_split's, bit for bit; k_commit_finish follows.
-template <int N, int V, int MR, int MX>
+// FUSE: a fused level's commit (device loop, chunks below the split size; k_commit's outputs): PB
+// consecutive parents at a time, those without winners skipped, the level from the control block, and
+// the last block to arrive finishes the level (finish_level).
+template <int N, int V, int MR, int MX, bool FUSE, int PB>
 __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
-    constexpr int PB = 64, NT = XB_THREADS, CCW = S::CCW, RECW = S::RECW_MAX, SW4 = S::SW4;
+    constexpr int NT = XB_THREADS, CCW = S::CCW, RECW = S::RECW_MAX, SW4 = S::SW4;
     static_assert(MX <= NT, "a parent's successor slots fit one round");
+    static_assert(PB >= 2 && PB <= 64 && (PB & (PB - 1)) == 0, "parents per batch: a power of two, a lane of wave 0 each");
     __shared__ uint32_t sRec[PB * RECW];        // the batch's parent records
     __shared__ uint32_t sOff[PB + 1];           // record offsets in sRec (exclusive scan of record words)
     __shared__ uint32_t sSl[PB + 1];            // successor slots: exclusive scan of cnt
@@ -3341,16 +3345,33 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
     __shared__ uint32_t sWr[NT];                // ... and each one's parent | slot << 8
     __shared__ uint32_t sNW;
     const int tid = threadIdx.x;
-    const uint64_t nvis = P.sum[SUM_NZ];
+    if constexpr (FUSE) {
+#ifdef RMC_RACE_PROBE
+        if (P.ctl) {  // the first block without a parent reads its block after the level advanced (k_commit)
+            const LevelCtl *c = ctl_cur(P);
+            const uint32_t lv = c->level;
+            if (c->stop == CTL_RUN && (uint64_t)blockIdx.x == (c->cur_n + PB - 1) / PB) {
+                race_wait(4000, [&] {
+                    return __hip_atomic_load(&ctl_nxt(P)->level, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == lv;
+                });
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            }
+        }
+#endif
+        if (!level_args(P)) return;
+    }
+    // the parents visited: a split chunk's or sharded round's with winners (plist), a fused level's all
+    const uint64_t nvis = FUSE ? P.p_end - P.p_begin : P.sum[SUM_NZ];
     for (uint64_t k0 = (uint64_t)blockIdx.x * PB; k0 < nvis; k0 += (uint64_t)gridDim.x * PB) {
         const uint32_t nb = (uint32_t)(nvis - k0 < (uint64_t)PB ? nvis - k0 : (uint64_t)PB);
         if (tid < 64) {  // wave 0: a lane per parent with winners
             uint32_t t = 0, words = 0;
             if ((uint32_t)tid < nb) {
-                const uint32_t pl = P.plist[k0 + tid];
+                const uint32_t pl = FUSE ? (uint32_t)(k0 + tid) : P.plist[k0 + tid];
                 const uint32_t tile = pl / WTILE;
-                t = (P.hcnt ? P.hcnt : P.cnt)[pl];  // (self-loops never win)
-                words = (uint32_t)CCW + ((P.pnm[pl] + 1u) >> 1);
+                const bool has = !FUSE || P.wcnt[pl] != 0u;  // (a fused level: parents without winners copy nothing)
+                t = has ? (P.hcnt ? P.hcnt : P.cnt)[pl] : 0u;  // (self-loops never win)
+                words = has ? (uint32_t)CCW + ((P.pnm[pl] + 1u) >> 1) : 0u;
                 sPl[tid] = pl;
                 sOut[tid] = P.boff[tile] + P.wpos[pl];
                 sWd[tid] = P.boffw[tile] + P.wposw[pl];
@@ -3492,6 +3513,14 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
             a = b;
         }
     }
+    if constexpr (FUSE) {
+        // the last block to arrive finishes the level (k_commit's protocol); every wave's atomics and
+        // stores are complete before its block's arrival (the barrier)
+        __syncthreads();
+        const uint64_t nbat = (nvis + PB - 1) / PB;
+        const uint32_t nbb = nbat < gridDim.x ? (nbat ? (uint32_t)nbat : 1u) : gridDim.x;
+        if (tid < 64 && last_commit_block(P.ctick, nbb)) finish_level<MX, S::RECW_MAX>(P);
+    }
 }
 
 // the chunk summary after k_commit_split (one wave): finish_level
@@ -3576,6 +3605,15 @@ static bool fused_items() {
     return on;
 }
 
+// ... and their commit: k_commit_items<FUSE> (RMC_FUSED_COMMIT=0: k_commit, a wave per parent)
+static bool fused_commit() {
+    static const bool on = [] {
+        const char *v = std::getenv("RMC_FUSED_COMMIT");
+        return fused_items() && !(v && v[0] == '0');
+    }();
+    return on;
+}
+
 static inline unsigned grid_for(uint64_t n) {
     const uint64_t cap = 256ull * RMC_GRID_PER_CU;  // one-wave blocks per CU (default 32) on 256 CUs
     return (unsigned)(n < cap ? (n ? n : 1) : cap);
@@ -3623,6 +3661,14 @@ struct Launch {
         hipLaunchKernelGGL((k_wincount<N, V, MR>), dim3(tiles ? (unsigned)tiles : 1u), dim3(1024), 0, s, P);
     }
     static void commit(const KParams &P, hipStream_t s) {
+        if constexpr (MX <= XB_THREADS) {
+            if (fused_commit() && !P.route && !P.split && !P.plist) {  // a block per 16 parents, records in LDS
+                const uint64_t nbat = (P.p_end - P.p_begin + XF_PARENTS - 1) / XF_PARENTS;
+                hipLaunchKernelGGL((k_commit_items<N, V, MR, MX, true, XF_PARENTS>),
+                                   dim3((unsigned)(nbat < 8192 ? (nbat ? nbat : 1) : 8192)), dim3(XB_THREADS), 0, s, P);
+                return;
+            }
+        }
         hipLaunchKernelGGL((k_commit<N, V, MR, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64), 0, s, P);
     }
     static void commit_split(const KParams &P, uint64_t np, hipStream_t s) {
@@ -3630,7 +3676,7 @@ struct Launch {
         if constexpr (MX <= XB_THREADS) {
             {  // a block per 64 parents with winners, records in LDS
                 const uint64_t nbat = (np + 63) / 64;
-                hipLaunchKernelGGL((k_commit_items<N, V, MR, MX>), dim3((unsigned)(nbat < 2048 ? (nbat ? nbat : 1) : 2048)),
+                hipLaunchKernelGGL((k_commit_items<N, V, MR, MX, false, 64>), dim3((unsigned)(nbat < 2048 ? (nbat ? nbat : 1) : 2048)),
                                    dim3(XB_THREADS), 0, s, P);
                 hipLaunchKernelGGL((k_commit_finish<MX, Spec<N, V, MR>::RECW_MAX>), dim3(1), dim3(64), 0, s, P);
                 return;
