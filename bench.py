@@ -66,9 +66,10 @@ def alg_bytes(phase, F, G, N, S, CCWB, slot_bytes=16, SWB=32, split=False, CTXB=
     if phase == "expand_hash" and split:  # k_expand_items: parents in, count + |msgs| + hash context out,
         # the staged rows of the successors other than self-loops out
         return F * S + F * 8 + F * CTXB + (G - Gself) * SWB
-    if phase == "expand_hash":   # k_expand<FUSED>: parents in, count + |msgs| out; per successor: staged row +
-        # fp + election slot, one seen-set probe; per new fingerprint at least one election (16-B slot, 8-B word, count)
-        return F * S + F * 8 + G * (SWB + 16 + 4) + G * slot_bytes + N * (16 + 8 + 4)
+    if phase == "expand_hash":   # k_expand_items<FUSE>: parents in, count + |msgs| out; per successor other than
+        # a self-loop: staged row + fp + election slot, one seen-set probe (a self-loop: its slot word only); per
+        # new fingerprint at least one election (16-B slot, 8-B word, count)
+        return F * S + F * 8 + (G - Gself) * (SWB + 16 + 4 + slot_bytes) + Gself * 4 + N * (16 + 8 + 4)
     if phase == "probe":         # k_hash_probe: per parent its count and hash context; per successor its staged
         # row in, fingerprint + verdict out, one seen-set probe; per new fingerprint at least one election
         # (16-B slot, 8-B word, count)
@@ -407,7 +408,7 @@ def main():
 
     phase_ms = [0.0] * 6
     launches = [0] * 6
-    Fs = Gs = Ns = 0
+    Fs = Gs = Ns = Gself = 0
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -427,6 +428,7 @@ def main():
             Fs += ls.expanded
             Gs += ls.generated
             Ns += ls.new_states
+            Gself += ls.self_loops
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -446,7 +448,7 @@ def main():
     slot_b = res.seen_slot_bytes or 16
     dom = max(range(4), key=lambda i: phase_ms[i])
     per_launch_ms = phase_ms[dom] / max(1, launches[dom])
-    bytes_total = alg_bytes(PHASES[dom], Fs, Gs, Ns, S, CCWB, slot_b, staging_bytes(mc.cfg))
+    bytes_total = alg_bytes(PHASES[dom], Fs, Gs, Ns, S, CCWB, slot_b, staging_bytes(mc.cfg), Gself=Gself)
     achieved = bytes_total / max(1, launches[dom]) / (per_launch_ms / 1e3) / 1e9 if per_launch_ms > 0 else 0.0
     pmc = pmc_kernel(mc, PHASES[dom], args.workload, res.depth)
     roof = {"bound": "hbm", "kernel": PHASES[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -648,10 +650,13 @@ def at_scale(device, workload="raftcfg", probes_per_s=None):
             "survey_roofline": survey_roofline(res.levels, S, dt, probes_per_s)}
 
 
-KERNEL_NAME = {"expand_hash": ["void rmc::k_expand<{n}, {V}, {mr}, 4, false>(rmc::KParams)",
+# kernel-name prefixes per phase: the item-parallel fused kernels (round 5) first, then round 4's
+KERNEL_NAME = {"expand_hash": ["void rmc::k_expand_items<{n}, {V}, {mr}, false, true,",
+                               "void rmc::k_expand<{n}, {V}, {mr}, 4, false>(rmc::KParams)",
                                "void rmc::k_expand<{n}, {V}, {mr}, 4>(rmc::KParams)"],
                "dedup": ["void rmc::k_wincount<{n}, {V}, {mr}>(rmc::KParams)"],
-               "materialize": ["void rmc::k_commit<{n}, {V}, {mr}, false>(rmc::KParams)",
+               "materialize": ["void rmc::k_commit_items<{n}, {V}, {mr}, ",
+                               "void rmc::k_commit<{n}, {V}, {mr}, false>(rmc::KParams)",
                                "void rmc::k_commit<{n}, {V}, {mr}>(rmc::KParams)"]}
 
 
@@ -671,8 +676,9 @@ def pmc_kernel(mc, phase, workload, depth):
     mr = 1 if (mc.cfg.msg_cap or (64 if n <= 3 else 128)) <= 64 else 2
     d = json.load(open(files[-1]))
     e = None
-    for name in KERNEL_NAME[phase]:  # kernel names before / after the spec-variant template argument
-        e = e or d.get(name.format(n=n, V=V, mr=mr))
+    for name in KERNEL_NAME[phase]:  # kernel-name prefixes, newest first
+        pre = name.format(n=n, V=V, mr=mr)
+        e = e or next((d[k] for k in sorted(d) if k.startswith(pre) and isinstance(d[k], dict)), None)
     if not e:
         return {}
     # the device-driven level loop enqueues a few levels past the last one, whose launches

@@ -130,7 +130,8 @@ typedef struct rmc_level_stats {
     uint64_t new_bytes;       /* ABI 3: bytes of the new states' frontier records (packed core + message ids) */
     uint64_t self_loops;      /* ABI 5: generated successors equal to their parent (FollowerAcceptEntry that
                                  changes nothing), among `generated`, where the run set them apart (single-GPU
-                                 split chunks: never fingerprinted -- the parent is in the seen set); else 0 */
+                                 levels -- split chunks and the item-parallel fused levels: never fingerprinted,
+                                 the parent is in the seen set); else 0 (sharded rounds) */
 } rmc_level_stats;
 
 /* Final result of a run: TLC's closing lines. */

@@ -31,14 +31,14 @@ def cfg_of(g, **kw):
     return c
 
 
-def run_worker(single, runs, tmp_path):
+def run_worker(single, runs, tmp_path, **extra_env):
     if not os.path.exists(RACE_LIB):
         pytest.fail(f"{RACE_LIB} missing: make -C tla-raft_amd (__graft_entry__.build) builds it")
     out = tmp_path / "race.json"
-    env = dict(os.environ, RMC_LIBRARY=RACE_LIB)
+    env = dict(os.environ, RMC_LIBRARY=RACE_LIB, **extra_env)
     spec = {"single": single, "runs": runs, "out": str(out)}
     p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "race_worker.py"), json.dumps(spec)], env=env,
-                       capture_output=True, text=True, timeout=600)
+                       capture_output=True, text=True, timeout=150)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
     return json.load(open(out))
 
@@ -90,3 +90,4 @@ def test_single_control_block_fails_under_the_forced_late_block(tmp_path):
     assert not matches(g, res[0], "n3_v1_e2_r3"), "the forced late block went unnoticed"
     r = res[0]
     assert "arrival counters" in r.get("error", "") or (r.get("distinct"), r.get("depth")) != (g["distinct"], g["depth"]), r
+

@@ -1000,6 +1000,7 @@ struct rmc_ctx {
         HIPCHK(hipMemsetAsync(s.err, 0xFF, ERR_NSLOTS * 8, stream));
         HIPCHK(hipMemsetAsync(s.flags, 0, 16, stream));
         s.sum = dmalloc<unsigned long long>(160);
+        HIPCHK(hipMemsetAsync(s.sum, 0, 160 * 8, stream));  // (the self-loop stripes are 0 between launches)
         HIPCHK(hipHostMalloc((void **)&s.hsum, 160 * 8, hipHostMallocDefault));
         s.rcap = 1ull << 14;
         s.R = dmalloc<uint32_t>(s.rcap);
@@ -1940,12 +1941,13 @@ struct rmc_ctx {
             };
             // expand + fingerprint + seen-set probe + staging, one evaluation per parent (a split
             // chunk: expand + staging + hash context, then fingerprint + probe + election a lane per successor)
+            // (the chunk's self-loops: counted by the fused expansion or the split chunk's winner count)
+            HIPCHK(hipMemsetAsync(s.sum + SUM_SELF, 0, 8, stream));
             timed(PH_HASH, [&] {
                 if (split) ks.split(params(), stream);
                 else ks.fused(params(), stream);
             });
             if (split) timed(PH_OTHER, [&] { ks.hash_probe(params(), np_, stream); });
-            if (split) HIPCHK(hipMemsetAsync(s.sum + SUM_SELF, 0, 8, stream));
             timed(PH_DEDUP, [&] {
                 ks.wincount(params(), np_, stream);
                 if (split && nzlist) launch_nzlist(params(), np_, stream);
@@ -1973,7 +1975,7 @@ struct rmc_ctx {
             HIPCHK(hipGetLastError());
             collect_times(st);
             const uint64_t G = s.hsum[0], Wn = s.hsum[1], Ww = s.hsum[SUM_WORDS];
-            if (split) level_self += s.hsum[SUM_SELF];
+            level_self += s.hsum[SUM_SELF];
             if (s.hsum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, flag_msg(s.hsum[2 + ERR_NSLOTS]));
             flush_trace(s, gid_nxt + s.nxt_n + Wn);
             level_gen += G;
@@ -2100,8 +2102,7 @@ struct rmc_ctx {
         h.batch = (uint32_t)K;
         __atomic_store_n(&s.hloop->done, 0u, __ATOMIC_RELAXED);
         __atomic_store_n(&s.hloop->stop, (uint32_t)CTL_RUN, __ATOMIC_RELEASE);
-        launch_set_ctl(s.ctl, h, stream);
-        launch_set_ctl(s.ctl + 1, h, stream);
+        launch_set_ctl(s.ctl, 2, h, s.sum, stream);
         uint64_t *offs[2] = {s.cur_off, s.nxt_off};
         std::vector<size_t> mark(K);
         // Levels go in groups of GL.  The loop's progress is mirrored into pinned host memory
@@ -2201,6 +2202,7 @@ struct rmc_ctx {
         for (int i = 0; i < D; i++) {
             const LevelRec &r = s.hlrec[i];
             rmc_level_stats *st = &out[i];
+            st->self_loops = r.self_loops;
             const int L = L0 + i;
             const uint64_t gid_nxt = s.level_start[L - 1] + r.expanded;
             total_generated += r.generated;

@@ -62,7 +62,7 @@ struct LevelCtl {
     uint32_t batch;              // levels the host enqueued: the loop hands back after that many
     uint32_t pad_;
 };
-struct LevelRec { unsigned long long expanded, generated, new_states, words; };
+struct LevelRec { unsigned long long expanded, generated, new_states, words, self_loops; };
 constexpr int LREC_CAP = 1024;   // levels per batch at most
 // Device-loop mirror in pinned, mapped host memory: finish_level writes each level's record and
 // the control block here, then the level count and (once the loop stops) the stop code with
@@ -79,7 +79,11 @@ constexpr uint32_t WTILE = 1024; // parents per tile of the winner-count scan
 constexpr uint32_t WTILES_MAX = 4096; // tiles per chunk (the last block scans four per thread)
 constexpr int SUM_WORDS = 7;     // chunk summary slot of the new states' record words
 constexpr int SUM_NZ = 16;       // ... and of the parents with winners (KParams::plist)
-constexpr int SUM_SELF = 17;     // ... and the self-loops set apart (KParams::hcnt; zeroed by the host per chunk)
+constexpr int SUM_SELF = 17;     // ... and the self-loops set apart (KParams::hcnt, or a host-driven fused chunk's;
+                                 // zeroed by the host per chunk)
+// the fused expansion's self-loop counters: SELF_STRIPES words a 128-B line apart (block b adds to stripe
+// b % SELF_STRIPES), folded by finish_level (k_set_ctl zeroes them for the device loop; 0 between levels)
+constexpr int SUM_SELF_STRIPE = 32, SELF_STRIDE = 16, SELF_STRIPES = 8;  // sum[32 .. 144]
 
 // In device-loop mode the host sizes every grid on a bound of the level's parents (p_end -
 // p_begin of the KParams it passes); the kernels read the real range from the LevelCtl.
@@ -222,7 +226,7 @@ void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, Seen dst, hipStream
 void launch_eslot_clear(ESlot *t, uint64_t n, hipStream_t s);
 void launch_insert_fps(const ulonglong2 *fp, uint64_t n, Seen seen, hipStream_t s);
 // the control block of a device-driven batch, passed by value (no copy-engine hand-off)
-void launch_set_ctl(LevelCtl *dst, const LevelCtl &v, hipStream_t s);
+void launch_set_ctl(LevelCtl *dst, int n, const LevelCtl &v, unsigned long long *gen, hipStream_t s);
 // Init's level from the cached Init record and fingerprint: record into the ring at word 0, its
 // offset 0, its fingerprint into the seen set
 void launch_init_level(uint32_t *ring, const uint32_t *rec, uint32_t words, uint64_t *off,

@@ -2204,7 +2204,9 @@ __global__ __launch_bounds__(XB_THREADS, FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) :
     uint16_t *sQ = reinterpret_cast<uint16_t *>(sU);   // [IC_N][NT] item codes by class
     uint16_t *sKey = sQ + IC_N * NT;                    // [NT * NCI] the round's enabled keys, per parent at its items' offset
     __shared__ uint32_t sSpan;
+    __shared__ uint32_t sSelfN;                    // fused level: the block's self-loops (finish_level adds them up)
     const int tid = threadIdx.x;
+    if (tid == 0) sSelfN = 0u;
     if constexpr (FUSE) {
         // device loop: the level from the control block, the levels committed so far to the host as
         // this one starts (as k_expand<M_FUSED>); grids are sized on a bound of the level
@@ -2253,9 +2255,15 @@ __global__ __launch_bounds__(XB_THREADS, FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) :
 #pragma unroll
                 for (int k = 0; k < CCW; k++) pk[k] = rec[k];
                 decode_core<N, V>(pk, c);
+                nmj = (c[Lo::W_MISC] >> 16) & 0xFFu;
+                if (nmj > (uint32_t)S::MCAP) {  // never a real record (commits flag the overflow): a
+                    // corrupted one stops the level with the msg_cap error instead of overrunning LDS
+                    atomicOr(&P.flags[0], 1u);
+                    nmj = S::MCAP;
+                    c[Lo::W_MISC] = (c[Lo::W_MISC] & ~0xFF0000u) | (nmj << 16);
+                }
 #pragma unroll
                 for (int w = 0; w < NW; w++) sCore[tid * NWP + w] = c[w];
-                nmj = (c[Lo::W_MISC] >> 16) & 0xFFu;
                 const uint32_t ec = c[Lo::W_MISC] & 15u, rc = (c[Lo::W_MISC] >> 4) & 15u;
                 unsigned long long sl = 0;
 #pragma unroll
@@ -2339,7 +2347,8 @@ __global__ __launch_bounds__(XB_THREADS, FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) :
             uint32_t b = a;  // the last parent b with sItm[b] <= ibase + NT: parents a .. b - 1 fit
 #pragma unroll
             for (uint32_t st = PB; st; st >>= 1) b = (b + st <= nb && sItm[b + st] <= ibase + NT) ? b + st : b;
-            const uint32_t nI = sItm[b] - ibase;
+            b = b > a ? b : a + 1;  // (a parent's items always fit a round: MCAP + N * SLOTS_PER_SERVER <= NT)
+            const uint32_t nI = sItm[b] - ibase < (uint32_t)NT ? sItm[b] - ibase : (uint32_t)NT;
             // the round's items into their class lists: live messages, then each parent's slots
             for (uint32_t m = sMsc[a] + (uint32_t)tid; m < sMsc[b]; m += NT) {
                 const uint32_t c = sMI[m];
@@ -2411,6 +2420,7 @@ __global__ __launch_bounds__(XB_THREADS, FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) :
                         // and hash sums in LDS, probed and elected right here (k_hash_probe's work)
                         if (x.self) {
                             P.lslot[q] = LS_SEEN;
+                            atomicAdd(&sSelfN, 1u);
                             continue;
                         }
                         uint4 st4[S::SW4];
@@ -2448,6 +2458,11 @@ __global__ __launch_bounds__(XB_THREADS, FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) :
             PHASE(6);
             a = b;
         }
+    }
+    if constexpr (FUSE) {
+        __syncthreads();
+        if (tid == 0 && sSelfN)
+            atomicAdd(&P.sum[SUM_SELF_STRIPE + SELF_STRIDE * (blockIdx.x % SELF_STRIPES)], (unsigned long long)sSelfN);
     }
     PHASE_FLUSH;
 }
@@ -2856,6 +2871,15 @@ __device__ void finish_level(const KParams &P) {
         Ww = sm[SUM_WORDS];
         if (P.ctl) c = *ctl_cur(P);
     }
+    // the fused expansion's self-loops, striped over SELF_STRIPES lines (one atomic per block each):
+    // into the level's record (device loop) or the chunk's sum[SUM_SELF] (host-driven), re-armed
+    unsigned long long Sf = 0;
+    if (lane < SELF_STRIPES) {
+        Sf = __hip_atomic_exchange(&sm[SUM_SELF_STRIPE + SELF_STRIDE * lane], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int o = SELF_STRIPES / 2; o; o >>= 1) Sf += __shfl_xor(Sf, o, SELF_STRIPES);
+        if (lane == 0 && !P.ctl && Sf) atomicAdd(&sm[SUM_SELF], Sf);
+    }
     unsigned long long e = 0;
     if (lane < ERR_NSLOTS)
         e = __hip_atomic_exchange(&P.err[lane], ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2882,6 +2906,7 @@ __device__ void finish_level(const KParams &P) {
         r.generated = G;
         r.new_states = Wn;
         r.words = Ww;
+        r.self_loops = Sf;
         P.lrec[c.done_levels] = r;
         if (P.hloop) P.hloop->rec[c.done_levels] = r;
     }
@@ -3362,6 +3387,7 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
     }
     // the parents visited: a split chunk's or sharded round's with winners (plist), a fused level's all
     const uint64_t nvis = FUSE ? P.p_end - P.p_begin : P.sum[SUM_NZ];
+    const uint32_t nbat = (uint32_t)((nvis + PB - 1) / PB);
     for (uint64_t k0 = (uint64_t)blockIdx.x * PB; k0 < nvis; k0 += (uint64_t)gridDim.x * PB) {
         const uint32_t nb = (uint32_t)(nvis - k0 < (uint64_t)PB ? nvis - k0 : (uint64_t)PB);
         if (tid < 64) {  // wave 0: a lane per parent with winners
@@ -3371,6 +3397,7 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
                 const uint32_t tile = pl / WTILE;
                 const bool has = !FUSE || P.wcnt[pl] != 0u;  // (a fused level: parents without winners copy nothing)
                 t = has ? (P.hcnt ? P.hcnt : P.cnt)[pl] : 0u;  // (self-loops never win)
+                t = t < (uint32_t)MX ? t : (uint32_t)MX;
                 words = has ? (uint32_t)CCW + ((P.pnm[pl] + 1u) >> 1) : 0u;
                 sPl[tid] = pl;
                 sOut[tid] = P.boff[tile] + P.wpos[pl];
@@ -3397,7 +3424,8 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
             uint32_t b = a;  // parents a .. b - 1: at most NT slots
 #pragma unroll
             for (uint32_t st = PB; st; st >>= 1) b = (b + st <= nb && sSl[b + st] <= sbase + NT) ? b + st : b;
-            const uint32_t nS = sSl[b] - sbase;
+            b = b > a ? b : a + 1;  // (a parent's slots always fit a round: MX <= NT)
+            const uint32_t nS = sSl[b] - sbase < (uint32_t)NT ? sSl[b] - sbase : (uint32_t)NT;
             // (a) a lane per slot: the winners, staged and listed on their parent
             if ((uint32_t)tid < nS) {
                 const uint32_t i = sbase + (uint32_t)tid;
@@ -3517,8 +3545,7 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
         // the last block to arrive finishes the level (k_commit's protocol); every wave's atomics and
         // stores are complete before its block's arrival (the barrier)
         __syncthreads();
-        const uint64_t nbat = (nvis + PB - 1) / PB;
-        const uint32_t nbb = nbat < gridDim.x ? (nbat ? (uint32_t)nbat : 1u) : gridDim.x;
+        const uint32_t nbb = nbat < gridDim.x ? (nbat ? nbat : 1u) : gridDim.x;
         if (tid < 64 && last_commit_block(P.ctick, nbb)) finish_level<MX, S::RECW_MAX>(P);
     }
 }
@@ -3720,7 +3747,7 @@ static void fill(KernelSet *ks) {
     ks->hash_probe = &Launch<N, V, MR, BFV>::hash_probe;
     ks->ctxw = ctx_words<N, V>();
     ks->insert = &Launch<N, V, MR, BFV>::insert;
-    ks->wincount = &Launch<N, V, MR>::wincount;
+    ks->wincount = &Launch<N, V, MR, BFV>::wincount;
     ks->commit = &Launch<N, V, MR, BFV>::commit;
     ks->commit_split = &Launch<N, V, MR, BFV>::commit_split;
     ks->local_elect = &Launch<N, V, MR, BFV>::local_elect;
@@ -3783,11 +3810,17 @@ void launch_eslot_clear(ESlot *t, uint64_t n, hipStream_t s) {
 void launch_rehash(const ulonglong2 *Told, uint64_t old_cap, Seen dst, hipStream_t s) {
     hipLaunchKernelGGL(k_rehash, dim3(grid256(old_cap)), dim3(256), 0, s, Told, old_cap, dst);
 }
-__global__ __launch_bounds__(64) void k_set_ctl(LevelCtl *dst, LevelCtl v) {
-    if (threadIdx.x == 0) *dst = v;
+// the device loop's control blocks (both of the pair) and the fused expansion's self-loop counters
+// (each level's finish_level re-arms them for the next)
+__global__ __launch_bounds__(64) void k_set_ctl(LevelCtl *dst, int n, LevelCtl v, unsigned long long *sum) {
+    if (threadIdx.x < (unsigned)n) dst[threadIdx.x] = v;
+    if (threadIdx.x == 0 && sum) {
+#pragma unroll
+        for (int k = 0; k < SELF_STRIPES; k++) sum[SUM_SELF_STRIPE + SELF_STRIDE * k] = 0ull;  // (fused self-loops)
+    }
 }
-void launch_set_ctl(LevelCtl *dst, const LevelCtl &v, hipStream_t s) {
-    hipLaunchKernelGGL(k_set_ctl, dim3(1), dim3(64), 0, s, dst, v);
+void launch_set_ctl(LevelCtl *dst, int n, const LevelCtl &v, unsigned long long *gen, hipStream_t s) {
+    hipLaunchKernelGGL(k_set_ctl, dim3(1), dim3(64), 0, s, dst, n, v, gen);
 }
 
 __global__ __launch_bounds__(64) void k_init_level(uint32_t *ring, const uint32_t *rec, uint32_t words,
