@@ -38,8 +38,9 @@ LEVEL = re.compile(r"^L\s*(\d+) F=\s*(\d+) G=\s*(\d+) N=\s*(\d+) tot=\s*\d+\s+[\
 # name -> (kernel name fragment, explore phase column of its HIP-event time, alg_bytes phase)
 KERNELS = {"expand": ("k_expand", 1, "expand_hash"), "probe": ("k_hash_probe", 5, "probe"),
            "insert": ("k_insert_winners", 5, "insert"),
-           # split chunks commit with k_commit_items (+ its one-wave k_commit_finish, not counted)
-           "commit": ("k_commit_items", 3, "materialize")}
+           # split chunks commit with k_commit_items<..., false, 64> (+ its one-wave k_commit_finish, not
+           # counted; the fused levels' k_commit_items<..., true, 16> is not a split chunk's)
+           "commit": ("k_commit_items|, false, 64>", 3, "materialize")}
 
 
 def levels_of(log):
@@ -57,8 +58,9 @@ def per_dispatch(csvf, kname):
     """Per dispatch of the kernel, in dispatch order: its counters and its duration in ms (the
     collection record's start / end timestamps)."""
     vals = collections.defaultdict(lambda: collections.defaultdict(float))
+    frags = kname.split("|")  # every fragment in the kernel's name
     for r in csv.DictReader(open(csvf)):
-        if kname in r["Kernel_Name"]:
+        if all(f in r["Kernel_Name"] for f in frags):
             d = vals[int(r["Dispatch_Id"])]
             d[r["Counter_Name"]] += float(r["Counter_Value"])
             d["_ms"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
@@ -131,7 +133,7 @@ def main():
                "hbm_frac": round(tot["hbm"] / tot["ms"] / 1e6 / HBM_PEAK_GBS, 5),
                "valu_frac": round(tot["valu"] / (tot["ms"] / 1e3) / VALU_PEAK, 4),
                "valu_per_successor": round(tot["valu"] / max(1, tot["G"]), 1)}
-        report["kernels"][key] = {"kernel": kname, "levels_with_parents_ge": a.min_parents, "aggregate": agg,
+        report["kernels"][key] = {"kernel": kname.replace("|", " "), "levels_with_parents_ge": a.min_parents, "aggregate": agg,
                                   "per_level": rows}
         print(f"{key}: {agg}")
     with open(a.out, "w") as f:
