@@ -1846,6 +1846,10 @@ constexpr int XB_PARENTS = RMC_ITEMS_PB;  // parents per batch (<= 64: a lane of
 #define RMC_FUSED_PB 16
 #endif
 constexpr int XF_PARENTS = RMC_FUSED_PB;
+#ifndef RMC_FUSED_CPB
+#define RMC_FUSED_CPB RMC_FUSED_PB  // ... and per block of their commit
+#endif
+constexpr int XC_PARENTS = RMC_FUSED_CPB;
 #ifndef RMC_FUSED_WAVES
 #define RMC_FUSED_WAVES 4  // n <= 3: registers cut for 4 waves per SIMD, 4 blocks per CU (the compiler's choice: 3;
                            // n >= 4 would spill)
@@ -3690,8 +3694,8 @@ struct Launch {
     static void commit(const KParams &P, hipStream_t s) {
         if constexpr (MX <= XB_THREADS) {
             if (fused_commit() && !P.route && !P.split && !P.plist) {  // a block per 16 parents, records in LDS
-                const uint64_t nbat = (P.p_end - P.p_begin + XF_PARENTS - 1) / XF_PARENTS;
-                hipLaunchKernelGGL((k_commit_items<N, V, MR, MX, true, XF_PARENTS>),
+                const uint64_t nbat = (P.p_end - P.p_begin + XC_PARENTS - 1) / XC_PARENTS;
+                hipLaunchKernelGGL((k_commit_items<N, V, MR, MX, true, XC_PARENTS>),
                                    dim3((unsigned)(nbat < 8192 ? (nbat ? nbat : 1) : 8192)), dim3(XB_THREADS), 0, s, P);
                 return;
             }

@@ -19,6 +19,8 @@ case "$part" in
   pb*) FLAGS="$FLAGS -DRMC_ITEMS_PB=${part#pb}" ;;
   # the fused item-parallel expansion's parents per batch (RMC_FUSED_ITEMS=1; e.g. fpb8)
   fpb*) FLAGS="$FLAGS -DRMC_FUSED_PB=${part#fpb}" ;;
+  # ... its commit's parents per block (e.g. fcpb8)
+  fcpb*) FLAGS="$FLAGS -DRMC_FUSED_CPB=${part#fcpb}" ;;
   # ... and the waves / SIMD its registers are cut for (e.g. fw4)
   fw*) FLAGS="$FLAGS -DRMC_FUSED_WAVES=${part#fw}" ;;
   # the fused expansion without its self-loop shortcut (round 4's behaviour)
@@ -26,7 +28,7 @@ case "$part" in
   # n = 3 occupancy: expansion waves / SIMD, commit waves / SIMD, grid blocks / CU (e.g. n3w6c4g32)
   n3w*) X=${part#n3w}; W=${X%%c*}; X=${X#*c}; C=${X%%g*}; G=${X#*g}
         FLAGS="$FLAGS -DRMC_N3_WAVES=$W -DRMC_N3_COMMIT_WAVES=$C -DRMC_GRID_PER_CU=$G" ;;
-  *) echo "usage: $0 prof|w1|sw<W>|iw<W>|pb<P>|fpb<P>|fw<W>|noskip|n3w<W>c<C>g<G>[+...]" >&2; exit 2 ;;
+  *) echo "usage: $0 prof|w1|sw<W>|iw<W>|pb<P>|fpb<P>|fcpb<P>|fw<W>|noskip|n3w<W>c<C>g<G>[+...]" >&2; exit 2 ;;
 esac
 done
 OUT=build_$1
