@@ -4,6 +4,7 @@ Bit-exact bar: identical successor lists (TLC order, keys and concrete states), 
 symmetry classes, identical invariant values, identical per-level distinct/generated
 counts, depth, verdict and counterexample traces (tests/golden/, from oracle/)."""
 import dataclasses
+import functools
 import gzip
 import json
 import os
@@ -919,3 +920,37 @@ def test_become_follower_sharded_identical(name, shards):
     check_levels(g, res)
     mc.close()
 
+
+
+SELF_LOOP_CASES = ["n3_v1_e1_r3", "n2_v1_e2_r3", "n3_v2_e1_r3"]
+
+
+@functools.lru_cache(maxsize=None)
+def _oracle_self_loops(name):
+    """Per expanded level, the oracle's successors identical to their parent (n3 V2 E1: ~11 s)."""
+    g = LEVELS[name]
+    cfg = R.Config(n=g["n"], V=g["V"], max_election=g["E"], max_restart=g["R"])
+    ref = R.bfs(cfg, keep_states=True)
+    want = [0] * max(ref.state_levels)
+    for st, lv in zip(ref.states, ref.state_levels):
+        want[lv - 1] += sum(1 for _, t in R.successors(cfg, st) if t == st)
+    return want
+
+
+@pytest.mark.parametrize("mode", ["device_loop", "host_fused", "split"])
+@pytest.mark.parametrize("name", SELF_LOOP_CASES)
+def test_self_loops_per_level_match_oracle(name, mode, monkeypatch):
+    """rmc_level_stats.self_loops (ABI 5): per expanded level, the successors equal to their parent
+    (FollowerAcceptEntry changing nothing, tla:275-300) -- counted by the item-parallel fused expansion
+    (device loop and host-driven chunks) and by a split chunk's winner count -- equal the oracle's count
+    of successors identical to their parent (oracle/raft_ref.py successors, exact state equality)."""
+    g = LEVELS[name]
+    want = _oracle_self_loops(name)
+    if mode == "split":
+        monkeypatch.setenv("RMC_SPLIT_MIN", "1")
+    mc, res = run_cfg(g, **({} if mode == "device_loop" else {"device_levels": 1}))
+    check_levels(g, res)
+    got = [ls.self_loops for ls in res.levels[1:]]
+    assert got == want[:len(got)] and sum(got) == sum(want), (got, want)
+    assert sum(want) > 0
+    mc.close()
