@@ -1,30 +1,29 @@
 #!/usr/bin/env python3
 """bench.py -- distinct states/sec of the MI355X model checker on BASELINE.json's workload.
 
-One "step" = one complete breadth-first exhaustion of the workload's state space from
-Init (TLC's whole myrun.sh run, minus JVM start-up): successor generation, symmetry +
-VIEW fingerprinting, seen-set dedup in TLC -workers 1 order, invariant checks.  The
-state space starts empty and every step re-explores it (rmc_reset keeps only device
-buffers; inputs = the compiled spec tables, resident in HBM).
+One "step" = one complete breadth-first exhaustion of the workload's state space from Init (TLC's
+whole myrun.sh run, minus JVM start-up): successor generation, symmetry + VIEW fingerprinting,
+seen-set dedup in TLC -workers 1 order, invariant checks.  The state space starts empty and every
+step re-explores it (rmc_reset keeps only device buffers; inputs = the compiled spec tables,
+resident in HBM).
 
-Workload at N=1: BASELINE.json configs[1] ("3 servers, 1 value, MaxTerm=2, MaxLogLen=2 on
-one MI355X") = Raft.tla with Servers={s1,s2,s3}, Vals={v1}, MaxElection=2, MaxRestart=3,
-SYMMETRY symmServers, VIEW view, INVARIANT Inv, -deadlock (MaxTerm is
-MaxElection, MaxLogLen is |Vals|+1).  The `at_scale` key exhausts configs[0]/[2] -- Raft.cfg as
-shipped (3 servers, 2 values, MaxElection 3: 10,946,499,503 distinct states, depth 72) -- on the
-same GPU and reports its wall time and distinct states/s (N = 1 only).
+Headline workload: BASELINE.json configs[0]/[2] -- Raft.cfg as shipped (myrun.sh:3), the
+configuration the metric ("distinct states/sec (whole node) + wall-time to exhaust, 1/2/4/8
+MI355X") is quoted on: Raft.tla with Servers = {s1, s2, s3}, Vals = {v1, v2}, MaxElection 3,
+MaxRestart 3, SYMMETRY symmServers, VIEW view, INVARIANT Inv, -deadlock -- 10,946,499,503 distinct
+states, depth 72, on one GPU in ~13 s.  `value` = its distinct states / the time of one
+exhaustion, `ms_per_step` = that time.  The `roofline` block is its dominant kernel, the split
+chunks' item-parallel expansion (k_expand_items<..., false, 64>), timed with HIP events on the
+engine's stream.  BASELINE configs[1] (3 servers, 1 value, MaxElection 2: 223,437 states in ~1.8 ms)
+is reported under the `configs1` key (N = 1).
 
-N>1 (torchrun, one process per GPU): the same workload is exhausted ONCE by all ranks
-together through the engine's multi-GPU mode: levels below
-rmc_config.shard_min_states (default 2^20 states) are expanded whole on every rank --
-replicated, no exchange, TLC order -- and from the first level that reaches it the seen
-set and frontier are sharded by fingerprint owner with one RCCL exchange of fingerprints /
-winner flags / winner records per chunk.  configs[1]'s levels never exceed ~2*10^4 states,
-so at this workload every level is replicated and the whole-node rate is the one-GPU rate
-(a per-level exchange would cost more than the level: tools/shard_timing.py).  value =
-distinct states of the run / max-over-ranks time, scaling "strong" (total work fixed).  If
-the RCCL communicator fails to initialise, each rank exhausts its own copy instead and the
-line says "replicas" with the error.
+N > 1 (torchrun, one process per GPU): the same Raft.cfg exhaustion by all ranks together through
+the engine's multi-GPU mode: levels below rmc_config.shard_min_states (2^20)
+are expanded whole on every rank, and from the first level that reaches it the frontier is
+block-cyclic over the ranks and the seen set sharded by fingerprint owner, the successors, verdicts
+and winner records exchanged over RCCL each round.  value = distinct states of the exhaustion /
+max-over-ranks time, scaling "strong" (total work fixed).  If the RCCL communicator fails to
+initialise, each rank exhausts its own copy instead and the line says "replicas" with the error.
 """
 import argparse
 import ctypes
@@ -51,8 +50,9 @@ WORKLOADS = {
 # HBM peak from /opt/skills/guides/MI355X_MICROARCH.md (spec 8.0 TB/s)
 HBM_PEAK_GBS = 8000.0
 PHASES = ["expand_count", "expand_hash", "dedup", "materialize", "exchange", "other"]
-TIMED_PHASES = 1 << PHASES.index("expand_hash")  # HIP-event timing of the dominant kernel only
-TIMING_EVERY = 8
+PH_EXPAND = PHASES.index("expand_hash")
+TIMED_PHASES = 1 << PH_EXPAND  # HIP-event timing of the expansion kernels only
+SPLIT_MIN = 1 << 16            # rmc_engine.hip split_min: chunks of this many parents run the split pipeline
 
 
 def alg_bytes(phase, F, G, N, S, CCWB, slot_bytes=16, SWB=32, split=False, CTXB=112, Gself=0):
@@ -116,17 +116,22 @@ def cpu_model():
     return "unknown"
 
 
+def host_threads():
+    # the host cores this job may use: the box's share (OMP_NUM_THREADS is set to it on the GPU boxes;
+    # the affinity mask there shows the whole machine)
+    return int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+
+
 def cpu_baseline(w, budget_s=12.0):
     """oracle/raft_mt.c -- the C restatement of Raft.tla + TLC -workers 1 BFS semantics, level-
-    synchronous on every host core this process may use -- exhausting the same workload."""
+    synchronous on every host core this process may use -- exhausting the same workload (configs[1]:
+    a full exhaustion takes ~0.15 s on 16 threads, so the sample is as many as fit in budget_s)."""
     so = os.path.join(ROOT, "oracle", "build", "libraft_mt.so")
     if not os.path.exists(so):
         return None
     lib = ctypes.CDLL(so)
     lib.orc_mt_run.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_uint64)] * 2 + [ctypes.POINTER(ctypes.c_int)]
-    # the host cores this job may use: the box's share (OMP_NUM_THREADS is set to it on the GPU
-    # boxes; the affinity mask there shows the whole machine)
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
+    threads = host_threads()
     runs, states = 0, 0
     d, g, dep = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
     t0 = time.perf_counter()
@@ -144,9 +149,58 @@ def cpu_baseline(w, budget_s=12.0):
                       f"box), {dt:.1f} s"}
 
 
-SHARDED_TIMEOUT_S = 420  # the multi-GPU Raft.cfg exhaustion (child processes) must finish within this
-SHARDED_TOTAL_S = 480    # ... and both sharded legs (Raft.cfg, then configs[3] as deep as it goes) within this
-C4_BUDGET_S = 120        # levels of configs[3] are started until this much time has passed
+def cpu_baseline_raftcfg(device, max_states=20_000_000):
+    """The CPU restatement (oracle/raft_mt.c, every host thread this job may use) on Raft.cfg's first
+    levels -- up to the first level boundary past max_states (24 levels, 21.6 M states: a bounded 10-30 s
+    sample of the headline workload; the whole exhaustion would take over an hour) -- and the GPU over the
+    same levels (a fresh checker, Init + one rmc_step per level): same workload, same host, same levels."""
+    import raftmc
+    so = os.path.join(ROOT, "oracle", "build", "libraft_mt.so")
+    if not os.path.exists(so):
+        return None
+    w = WORKLOADS["raftcfg"]
+    lib = ctypes.CDLL(so)
+    P64 = ctypes.POINTER(ctypes.c_uint64)
+    lib.orc_mt_levels.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint64, P64, P64, ctypes.c_int, P64, P64,
+                                                       ctypes.POINTER(ctypes.c_int)]
+    threads = host_threads()
+    cap = 256
+    d, g = (ctypes.c_uint64 * cap)(), (ctypes.c_uint64 * cap)()
+    dist, gen, depth = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
+    t0 = time.perf_counter()
+    v = lib.orc_mt_levels(w["n"], w["V"], w["E"], w["R"], threads, max_states, d, g, cap, ctypes.byref(dist),
+                          ctypes.byref(gen), ctypes.byref(depth))
+    dt = time.perf_counter() - t0
+    D = depth.value
+    cpu_levels = list(d[:D])
+    # the GPU's levels 1..D: Init plus the expansions of levels 1..D-1
+    cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
+                             invariants=("Inv",), check_deadlock=False, device=device)
+    with raftmc.ModelChecker(cfg) as mc:
+        mc.init()  # (buffers grow on the way: one untimed pass first)
+        for _ in range(D - 1):
+            mc.step()
+        mc.reset()
+        t0 = time.perf_counter()
+        gpu_levels = [mc.init().new_states]
+        for _ in range(D - 1):
+            gpu_levels.append(mc.step().new_states)
+        gpu_s = time.perf_counter() - t0
+    return {"value": round(dist.value / dt, 1), "unit": "distinct states/s", "cores": threads, "cpu_model": cpu_model(),
+            "kind": "port", "levels": D, "distinct_states": dist.value, "seconds": round(dt, 3),
+            "gpu_seconds_same_levels": round(gpu_s, 4),
+            "gpu_distinct_per_s_same_levels": round(dist.value / gpu_s, 1) if gpu_s > 0 else None,
+            "gpu_over_cpu_same_levels": round(dt / gpu_s, 1) if gpu_s > 0 else None,
+            "levels_match_gpu": cpu_levels == gpu_levels, "verdict_code": v,
+            "sample": f"Raft.cfg levels 1-{D} ({dist.value} distinct states) by oracle/raft_mt.c on {threads} threads "
+                      f"(C restatement of Raft.tla, exact canonical forms, level-synchronous first-wins BFS; not TLC: no "
+                      f"JVM/tla2tools.jar on the box), {dt:.1f} s; the GPU's seconds are those of the same levels run "
+                      f"level by level (the small early levels are latency-bound on the GPU, so the ratio over the whole "
+                      f"exhaustion is larger)"}
+
+
+C4_TIMEOUT_S = 240  # --configs3 at N > 1: the configs[3] child must finish within this
+C4_BUDGET_S = 120   # levels of configs[3] are started until this much time has passed
 C4_ONE_GPU_LEVELS = 30   # configs[3] on one MI355X, single-GPU path, 48 GB seen set / 200 GB ring: levels 1-30 (DESIGN.md 9)
 
 
@@ -161,65 +215,34 @@ def xgmi_model(levels, world, shard_min=1 << 20):
     for ls in levels:
         on = on or ls.expanded >= shard_min
         if on:
-            total += ls.generated * (24 + 4) + ls.new_bytes + 16 * ls.new_states
+            total += (ls.generated - ls.self_loops) * (24 + 4) + ls.new_bytes + 16 * ls.new_states
     return int(total * (world - 1) / world)
 
 
 def sharded_child(args):
-    """One rank of the multi-GPU Raft.cfg exhaustion (configs[2] at N GPUs), run in a child process of
-    each bench rank before the bench touches the GPU: the levels are sharded over the N GPUs (RCCL,
-    block-cyclic frontier, fingerprint-owner seen set) from the first level of
-    >= 2^20 states.  Rank 0 writes the result to args.sharded_out."""
+    """One rank of configs[3] sharded over the N GPUs (--configs3 at N > 1), run in a child process of
+    each bench rank before the bench touches the GPU.  Rank 0 writes the result to args.sharded_out."""
     import torch
     import torch.distributed as dist
     import raftmc
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # a port of its own per child (the Raft.cfg child's store may still hold its port when the next starts)
-    port = int(os.environ.get("MASTER_PORT", "29500")) + (17 if args.child_workload == "raftcfg" else 19)
+    port = int(os.environ.get("MASTER_PORT", "29500")) + 19  # a port of the child's own
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     idt = torch.zeros(128, dtype=torch.uint8)
     if rank == 0:
         idt = torch.tensor(list(raftmc.comm_unique_id()), dtype=torch.uint8)
     dist.broadcast(idt, 0)
-    w = WORKLOADS[args.child_workload]
+    w = WORKLOADS["c4"]
     cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
                              invariants=("Inv",), check_deadlock=False, device=local, rank=rank, world_size=world,
                              comm_unique_id=bytes(idt.tolist()))
-    if args.child_workload == "c4":
-        # per GPU: a 48 GB seen-set shard (6.4 G compact slots) and a 160 GB frontier ring, ~80 GB
-        # left for the rounds' buffers; the default gives the seen set half of HBM, far more than
-        # this configuration's levels fill before the ring does (DESIGN.md section 9)
-        cfg.seen_mem_bytes, cfg.frontier_mem_bytes = 48 << 30, 160 << 30
-        cfg.chunk_successors = 1 << 27  # rounds of 2^27 slots: the rounds' buffers stay within the ~80 GB left
-        c4_child(args, cfg, w, rank, world)
-        dist.destroy_process_group()
-        return
-    with raftmc.ModelChecker(cfg) as mc:
-        dist.barrier()
-        t0 = time.perf_counter()
-        res = mc.run()
-        dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    if rank == 0:
-        gold = {}
-        gpath = os.path.join(ROOT, "tests", "golden", "levels_prefix.json")
-        if os.path.exists(gpath):
-            gold = json.load(open(gpath)).get("n3_v2_e3_r3", {})
-        got = [ls.new_states for ls in res.levels]
-        out = {"workload": w["desc"], "n_gpus": world, "parallelism": f"rccl-{world}: block-cyclic levels, "
-               "fingerprint-owner seen set, TLC-order global-key election, from the first level of >= 2^20 states",
-               "distinct_states": res.distinct, "states_generated": res.generated, "depth": res.depth,
-               "verdict": "Inv holds" if res.status == "done" else res.status,
-               "seconds_to_exhaust": round(dt, 3), "distinct_per_s": round(res.distinct / dt, 1),
-               "matches_c_oracle_prefix_levels": (got[:len(gold["levels"])] == gold["levels"]) if gold else None}
-        xb = xgmi_model(res.levels, world)
-        out["xgmi_bytes_model"] = xb
-        out["xgmi_GBps_avg"] = round(xb / dt / 1e9, 2)
-        with open(args.sharded_out, "w") as f:
-            json.dump(out, f)
+    # per GPU: a 48 GB seen-set shard (6.4 G compact slots) and a 160 GB frontier ring, ~80 GB left for the
+    # rounds' buffers; the default gives the seen set half of HBM, far more than this configuration's levels
+    # fill before the ring does (DESIGN.md section 9)
+    cfg.seen_mem_bytes, cfg.frontier_mem_bytes = 48 << 30, 160 << 30
+    cfg.chunk_successors = 1 << 27  # rounds of 2^27 slots: the rounds' buffers stay within the ~80 GB left
+    c4_child(args, cfg, w, rank, world)
     dist.destroy_process_group()
 
 
@@ -236,7 +259,7 @@ def c4_child(args, cfg, w, rank, world):
     budget = float(b.item())
     out = {"workload": w["desc"], "n_gpus": world, "one_gpu_levels": C4_ONE_GPU_LEVELS}
     if budget < 30:
-        out["skipped"] = f"{budget:.0f} s left of the sharded legs' {SHARDED_TOTAL_S} s"
+        out["skipped"] = f"{budget:.0f} s of budget"
         if rank == 0:
             with open(args.sharded_out, "w") as f:
                 json.dump(out, f)
@@ -301,7 +324,7 @@ def run_child(args, workload, timeout_s, budget_s=0.0):
     if rank == 0 and os.path.exists(out):
         os.remove(out)
     cmd = [sys.executable, os.path.abspath(__file__), "--sharded-child", "--sharded-out", out,
-           "--child-workload", workload, "--child-budget", str(budget_s)]
+           "--child-budget", str(budget_s)]
     t0 = time.perf_counter()
     p = subprocess.Popen(cmd, stdout=sys.stderr, stderr=sys.stderr)
     try:
@@ -310,7 +333,7 @@ def run_child(args, workload, timeout_s, budget_s=0.0):
         p.kill()
         p.wait()
         err = {"error": f"timed out after {timeout_s:.0f} s", "wall_s": round(time.perf_counter() - t0, 1)}
-        if rank == 0 and os.path.exists(out):  # what the child reported before its limit (configs[3])
+        if rank == 0 and os.path.exists(out):  # what the child reported before its limit
             with open(out) as f:
                 err.update(json.load(f))
         return err if rank == 0 else None
@@ -322,203 +345,183 @@ def run_child(args, workload, timeout_s, budget_s=0.0):
         return json.load(f)
 
 
-def run_sharded_children(args):
-    """The two sharded legs at N > 1: Raft.cfg exhausted over the N GPUs (configs[2]), then configs[3]
-    as deep as the remaining time allows.  Every rank always starts both children; the configs[3]
-    child agrees on its budget across ranks (the minimum), so no rank is left in a collective."""
-    t0 = time.perf_counter()
-    raft = run_child(args, "raftcfg", SHARDED_TIMEOUT_S)
-    left = SHARDED_TOTAL_S - (time.perf_counter() - t0)
-    c4 = run_child(args, "c4", max(30.0, left), budget_s=min(C4_BUDGET_S, left - 60.0))
-    return raft, c4
+def progress(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-probe-peak", action="store_true")
-    ap.add_argument("--no-scale", action="store_true", help="skip the at-scale reference exhaustion (N=1) / the "
-                    "multi-GPU Raft.cfg exhaustion (N>1)")
-    ap.add_argument("--sharded-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--sharded-out", default="", help=argparse.SUPPRESS)
-    ap.add_argument("--child-workload", default="raftcfg", choices=("raftcfg", "c4"), help=argparse.SUPPRESS)
-    ap.add_argument("--child-budget", type=float, default=C4_BUDGET_S, help=argparse.SUPPRESS)
-    args = ap.parse_args()
-    if args.sharded_child:
-        sharded_child(args)
-        return
-    sharded = sharded_c4 = None
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not args.no_scale:
-        sharded, sharded_c4 = run_sharded_children(args)
-
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
+def measure(mc, steps, warmup, world, sync, label, timing_every=1, report_steps=True):
+    """W untimed warmup steps, then exactly K timed steps bracketed by a barrier + device sync on both sides;
+    the max over ranks of the timed region.  Every timing_every-th timed step carries HIP events on the
+    expansion kernels (rmc_set_timing); their per-level statistics are kept for the roofline."""
     import torch.distributed as dist
-    if world > 1:
-        dist.init_process_group("gloo")  # control plane only: barriers and the max-over-ranks time
-    torch.cuda.set_device(local)
-
-    import raftmc
-    w = WORKLOADS[args.workload]
-    cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
-                             invariants=("Inv",), check_deadlock=False, device=local,
-                             timing_phases=TIMED_PHASES)
-    parallelism = "single-gpu"
-    if world > 1:
-        # rank 0 creates the RCCL id; the control-plane group (gloo) broadcasts it
-        idt = torch.zeros(128, dtype=torch.uint8)
-        if rank == 0:
-            idt = torch.tensor(list(raftmc.comm_unique_id()), dtype=torch.uint8)
-        dist.broadcast(idt, 0)
-        cfg.rank, cfg.world_size, cfg.comm_unique_id = rank, world, bytes(idt.tolist())
-        parallelism = (f"rccl-{world}: fingerprint-owner sharding from the first level of >= 2^20 states, "
-                       f"smaller levels replicated on every GPU (all of this workload's)")
-    mc, err = None, ""
-    try:
-        mc = raftmc.ModelChecker(cfg)
-    except raftmc.RmcError as e:
-        if world == 1:
-            raise
-        err = str(e)
-    if world > 1:
-        ok = torch.tensor([0 if mc is None else 1], dtype=torch.int32)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same mode
-        if int(ok.item()) == 0:
-            print(f"rank {rank}: sharded RCCL path unavailable ({err or 'another rank failed'}); running replicas",
-                  file=sys.stderr, flush=True)
-            if mc is not None:
-                mc.close()
-            cfg.rank, cfg.world_size, cfg.comm_unique_id = 0, 1, None
-            mc = raftmc.ModelChecker(cfg)
-            parallelism = f"replicas (sharded RCCL init failed: {err or 'on another rank'})"
-    res = None
-    for _ in range(args.warmup):
+    res, first_s = None, None
+    for i in range(warmup):
         mc.reset()
+        t0 = time.perf_counter()
         res = mc.run()
+        dt = time.perf_counter() - t0
+        first_s = dt if first_s is None else first_s
+        if report_steps:
+            progress(f"{label} warmup {i + 1}/{warmup}: {dt:.3f} s ({res.distinct} distinct, {res.status})")
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    phase_ms = [0.0] * 6
-    launches = [0] * 6
-    Fs = Gs = Ns = Gself = 0
+    timed = []  # per event-timed step: its level statistics
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
-    # HIP events between kernels cost a few microseconds of queue time each on this
-    # latency-bound workload, so only every TIMING_EVERY-th timed step carries them; the
-    # dominant kernel's average launch duration comes from those steps' events.
-    for k in range(args.steps):
-        mc.set_timing(TIMED_PHASES if k % TIMING_EVERY == 0 else 0)
+    for k in range(steps):
+        on = k % timing_every == 0
+        mc.set_timing(TIMED_PHASES if on else 0)
         mc.reset()
+        ts = time.perf_counter()
         res = mc.run()
-        if k % TIMING_EVERY:
-            continue
-        for ls in res.levels:  # the event-timed steps: their launches and the bytes they moved
-            for i in range(6):
-                phase_ms[i] += ls.kernel_ms[i]
-                launches[i] += ls.kernel_launches[i]
-            Fs += ls.expanded
-            Gs += ls.generated
-            Ns += ls.new_states
-            Gself += ls.self_loops
-    torch.cuda.synchronize()
+        if on:
+            timed.append(res.levels)
+        if report_steps:
+            progress(f"{label} step {k + 1}/{steps}: {time.perf_counter() - ts:.3f} s ({res.distinct} distinct, "
+                     f"{res.status})")
+    sync()
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
+        import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    assert res is not None and res.status == "done", res
-    ms_per_step = elapsed / args.steps * 1e3
-    # replicas (RCCL unavailable) each exhaust the whole space: the job is still ONE exhaustion, so
-    # value stays its distinct states / time (never multiplied by the replica count)
-    units = res.distinct
-    value = units * args.steps / elapsed
+    if first_s is None and timed:  # no warmup: the first timed step was the cold one
+        first_s = sum(ls.seconds for ls in timed[0])
+    return res, elapsed, timed, first_s
 
-    # dominant kernel phase: the one with the most device time (HIP events on the engine's stream)
-    S, CCWB = record_bytes(res, mc.cfg)
-    slot_b = res.seen_slot_bytes or 16
+
+def split_roofline(timed, S, cfg, world=1):
+    """The headline's roofline: k_expand_items<..., false, 64>, the split chunks' expansion (DESIGN.md
+    section 4), over the event-timed steps' levels whose every chunk is split (>= SPLIT_MIN parents; a
+    level with a tail chunk below it, which the fused kernel expands, is left out).  Algorithmic bytes per
+    chunk: alg_bytes("expand_hash", split=True) with the level's successors, self-loops and new states
+    spread over its chunks by their parents; time and launches: the HIP events of those levels' expansion
+    phase on the engine's stream.  At N > 1 a rank expands 1/N of each level (block-cyclic rounds)."""
+    n, V = cfg.n_servers, cfg.n_vals
+    cp = chunk_parents(n, V, cfg.chunk_successors or (1 << 28))
+    ms, launches, alg, levels_used = 0.0, 0, 0.0, 0
+    for levels in timed:
+        for ls in levels[1:]:
+            F = ls.expanded
+            if F < SPLIT_MIN or 0 < F % cp < SPLIT_MIN or not ls.kernel_launches[PH_EXPAND]:
+                continue
+            levels_used += 1
+            ms += ls.kernel_ms[PH_EXPAND]
+            launches += ls.kernel_launches[PH_EXPAND]
+            for c0 in range(0, F, cp):
+                f = min(cp, F - c0)
+                alg += alg_bytes("expand_hash", f, ls.generated * f / F, ls.new_states * f / F, S, 4 * codec_words(n, V),
+                                 SWB=staging_bytes(cfg), split=True, CTXB=ctx_bytes(n, V),
+                                 Gself=ls.self_loops * f / F) / world
+    if not launches or ms <= 0:
+        return {"bound": "hbm", "kernel": "k_expand_items (split chunks)", "achieved": None, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": None, "traffic": None}
+    per_launch_ms = ms / launches
+    per_launch_b = alg / launches
+    achieved = per_launch_b / (per_launch_ms / 1e3) / 1e9
+    mr = 1 if n <= 3 else 2
+    roof = {"bound": "hbm", "kernel": f"k_expand_items<{n}, {V}, {mr}, false, false, 64> (split chunks)",
+            "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": None, "algorithmic_bytes_per_launch": round(per_launch_b), "avg_launch_ms": round(per_launch_ms, 5),
+            "launches": launches, "levels": levels_used, "timed_steps": len(timed), "record_bytes_avg": round(S, 2)}
+    pmc = pmc_kernel(n, V, "raftcfg", split_kernel_name(n, V), dispatches_real=None)
+    if pmc.get("traffic"):
+        # the PMC run's own split launches: traffic per launch and its ratio to their algorithmic bytes
+        roof["traffic"] = pmc["traffic"]
+        roof["traffic_source"] = pmc["source"]
+        if pmc.get("dispatches"):
+            roof["traffic_dispatches"] = pmc["dispatches"]
+    if pmc.get("valu_insts"):
+        # the expansion's other limit: VALU issue.  A wave64 VALU instruction occupies a SIMD-32 for 2 cycles
+        # (MI355X_MICROARCH.md constants table): peak = CUs x 4 SIMDs x clock / 2; the PMC run's instructions
+        # per launch over this run's average launch (the same workload's launches)
+        rate = pmc["valu_insts"] / (per_launch_ms / 1e3)
+        roof["valu"] = {"insts_per_launch": round(pmc["valu_insts"]), "achieved_insts_per_s": round(rate),
+                        "peak_insts_per_s": VALU_PEAK, "frac": round(rate / VALU_PEAK, 4), "source": pmc["source"]}
+    return roof
+
+
+def phase_roofline(timed, S, cfg, workload, depth):
+    """configs[1]'s roofline (all its levels run in the device loop): the phase with the most HIP-event time
+    -- the fused expansion k_expand_items<..., true, 16> -- its algorithmic bytes per launch over its average
+    launch duration."""
+    phase_ms, launches = [0.0] * 6, [0] * 6
+    F = G = N = Gself = 0
+    for levels in timed:
+        for ls in levels:
+            for i in range(6):
+                phase_ms[i] += ls.kernel_ms[i]
+                launches[i] += ls.kernel_launches[i]
+            F += ls.expanded
+            G += ls.generated
+            N += ls.new_states
+            Gself += ls.self_loops
     dom = max(range(4), key=lambda i: phase_ms[i])
     per_launch_ms = phase_ms[dom] / max(1, launches[dom])
-    bytes_total = alg_bytes(PHASES[dom], Fs, Gs, Ns, S, CCWB, slot_b, staging_bytes(mc.cfg), Gself=Gself)
+    bytes_total = alg_bytes(PHASES[dom], F, G, N, S, 4 * codec_words(cfg.n_servers, cfg.n_vals), 16,
+                            staging_bytes(cfg), Gself=Gself)
     achieved = bytes_total / max(1, launches[dom]) / (per_launch_ms / 1e3) / 1e9 if per_launch_ms > 0 else 0.0
-    pmc = pmc_kernel(mc, PHASES[dom], args.workload, res.depth)
+    n, V = cfg.n_servers, cfg.n_vals
+    mr = 1 if n <= 3 else 2
+    name = KERNEL_NAME.get(PHASES[dom], "").format(n=n, V=V, mr=mr)
+    # the device-driven level loop enqueues a few levels past the last one, whose launches return at once:
+    # the PMC pass's totals are spread over the launches that expanded a level
+    pmc = pmc_kernel(n, V, workload, name, dispatches_real=PMC_RUNS * depth) if name else {}
     roof = {"bound": "hbm", "kernel": PHASES[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": pmc.get("traffic"),
             "traffic_source": pmc.get("source"),
             "algorithmic_bytes_per_launch": round(bytes_total / max(1, launches[dom])),
-            "avg_launch_ms": round(per_launch_ms, 5), "launches": launches[dom],
-            "timed_steps": len(range(0, args.steps, TIMING_EVERY)),
-            "record_bytes_avg": round(S, 2), "seen_slot_bytes": slot_b,
-            "phase_ms_per_step": {PHASES[i]: round(phase_ms[i] / len(range(0, args.steps, TIMING_EVERY)), 4)
-                                  for i in range(4)}}
+            "avg_launch_ms": round(per_launch_ms, 5), "launches": launches[dom], "timed_steps": len(timed),
+            "record_bytes_avg": round(S, 2),
+            "phase_ms_per_step": {PHASES[i]: round(phase_ms[i] / max(1, len(timed)), 4) for i in range(4)}}
     if pmc.get("valu_insts") and per_launch_ms > 0:
-        # the binding limit of the expansion kernel: VALU issue.  A wave64 VALU instruction occupies a
-        # SIMD-32 for 2 cycles (MI355X_MICROARCH.md constants table): peak = CUs x 4 SIMDs x clock / 2
         rate = pmc["valu_insts"] / (per_launch_ms / 1e3)
         roof["valu"] = {"insts_per_launch": round(pmc["valu_insts"]), "achieved_insts_per_s": round(rate),
-                        "peak_insts_per_s": VALU_PEAK, "frac": round(rate / VALU_PEAK, 4),
-                        "source": pmc.get("source")}
-    # seen-set probe throughput of the run (one probe per generated successor in the expansion
-    # pass, one insert per new state in commit) against the random-probe peak of the same slot
-    # layout measured on this GPU: a table the size of the run's (2^22 slots, L2/MALL-resident)
-    # and one far beyond the caches (2^28 slots = 4 GiB, HBM-resident)
-    probes = (res.generated + res.distinct) * args.steps * (world if parallelism.startswith("replicas") else 1)
-    seen = {"probes_per_step": res.generated + res.distinct,
-            "achieved_probes_per_s": round(probes / elapsed, 1)}
-    pk_hbm = None
-    if rank == 0 and not args.no_probe_peak:
-        pk_small = raftmc.probe_peak(local, 22, 1 << 26)
-        pk_hbm = raftmc.probe_peak(local, 28, 1 << 28)
-        seen.update({"peak_probes_per_s_2^22_slots": round(pk_small, 1),
-                     "peak_probes_per_s_2^28_slots": round(pk_hbm, 1),
-                     "frac_of_hbm_probe_peak": round(probes / elapsed / pk_hbm, 5),
-                     "slot_bytes": 16})
-    line = {
-        "metric": "distinct states/sec (whole node) + wall-time to exhaust",
-        "value": round(value, 1),
-        "unit": "distinct states/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "u32",
-        "data": "synthetic: the state space of Raft.tla itself, generated from Init on the GPU each step",
-        "config": {"workload": w["desc"], "distinct_states": res.distinct, "states_generated": res.generated,
-                   "depth": res.depth, "verdict": "Inv holds" if res.status == "done" else res.status,
-                   "parallelism": parallelism},
-        "roofline": roof,
-        "seen_set": seen,
-        "survey_roofline": survey_roofline(res.levels, S, elapsed / args.steps, pk_hbm),
-    }
-    if rank == 0 and world == 1 and not args.no_scale:
-        mc.close()  # the at-scale run gets the whole device (this checker's chunk buffers are ~12 GB)
-        line["at_scale"] = dict(path="single-gpu", n_gpus=1, **at_scale(local, probes_per_s=pk_hbm))
-        if not args.no_cpu_baseline:
-            line["cpu_baseline_at_scale"] = cpu_baseline_at_scale(local)
-    if rank == 0 and sharded is not None:
-        # N > 1: the same workload (Raft.cfg exhausted) under the same key, over all N GPUs
-        line["at_scale"] = dict(path=f"sharded over {world} GPUs (RCCL)", **sharded)
-    if rank == 0 and sharded_c4 is not None:
-        line["at_scale_sharded_configs3"] = sharded_c4
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(w)
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    mc.close()
-    if world > 1:
-        dist.destroy_process_group()
+                        "peak_insts_per_s": VALU_PEAK, "frac": round(rate / VALU_PEAK, 4), "source": pmc.get("source")}
+    return roof
+
+
+def oracle_prefix_match(res, w):
+    gpath = os.path.join(ROOT, "tests", "golden", "levels_prefix.json")
+    if not os.path.exists(gpath):
+        return None, 0
+    with open(gpath) as f:
+        gold = json.load(f).get(f"n{w['n']}_v{w['V']}_e{w['E']}_r{w['R']}", {})
+    if not gold:
+        return None, 0
+    got = [ls.new_states for ls in res.levels]
+    return got[:len(gold["levels"])] == gold["levels"], len(gold["levels"])
+
+
+def configs1_leg(device, args, probes_per_s):
+    """BASELINE configs[1] on this GPU (N = 1): its own checker, 5 warmup + 20 timed exhaustions of ~1.8 ms
+    (latency-bound: every level runs in the device-driven loop), the dominant kernel's roofline, and the
+    C restatement's rate on the same workload."""
+    import raftmc
+    import torch
+    w = WORKLOADS["c2"]
+    cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
+                             invariants=("Inv",), check_deadlock=False, device=device, timing_phases=TIMED_PHASES)
+    steps = 20
+    with raftmc.ModelChecker(cfg) as mc:
+        res, elapsed, timed, _ = measure(mc, steps, 5, 1, torch.cuda.synchronize, "configs[1]", timing_every=8,
+                                         report_steps=False)
+    S, _ = record_bytes(res, cfg)
+    out = {"workload": w["desc"], "value": round(res.distinct * steps / elapsed, 1), "unit": "distinct states/s",
+           "ms_per_step": round(elapsed / steps * 1e3, 4), "steps": steps, "warmup": 5,
+           "distinct_states": res.distinct, "states_generated": res.generated, "depth": res.depth,
+           "verdict": "Inv holds" if res.status == "done" else res.status,
+           "roofline": phase_roofline(timed, S, cfg, "c2", res.depth),
+           "survey_roofline": survey_roofline(res.levels, S, elapsed / steps, probes_per_s)}
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(w)
+    return out
 
 
 def counters_at_scale(workload="raftcfg"):
@@ -540,152 +543,35 @@ def counters_at_scale(workload="raftcfg"):
     return out
 
 
-def cpu_baseline_at_scale(device, workload="raftcfg", max_states=20_000_000):
-    """The CPU restatement (oracle/raft_mt.c, every host thread this job may use) on the at-scale workload's
-    first levels -- up to the first level boundary past max_states (Raft.cfg: 24 levels, 21.6 M states, a
-    bounded 10-30 s sample) -- and the GPU over the same levels (a fresh checker, Init + one rmc_step per
-    level): same workload, same host, same levels."""
-    import raftmc
-    so = os.path.join(ROOT, "oracle", "build", "libraft_mt.so")
-    if not os.path.exists(so):
-        return None
-    w = WORKLOADS[workload]
-    lib = ctypes.CDLL(so)
-    P64 = ctypes.POINTER(ctypes.c_uint64)
-    lib.orc_mt_levels.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint64, P64, P64, ctypes.c_int, P64, P64,
-                                                       ctypes.POINTER(ctypes.c_int)]
-    threads = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
-    cap = 256
-    d, g = (ctypes.c_uint64 * cap)(), (ctypes.c_uint64 * cap)()
-    dist, gen, depth = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_int()
-    t0 = time.perf_counter()
-    v = lib.orc_mt_levels(w["n"], w["V"], w["E"], w["R"], threads, max_states, d, g, cap, ctypes.byref(dist),
-                          ctypes.byref(gen), ctypes.byref(depth))
-    dt = time.perf_counter() - t0
-    D = depth.value
-    cpu_levels = list(d[:D])
-    # the GPU's levels 1..D: Init plus the expansions of levels 1..D-1
-    cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
-                             invariants=("Inv",), check_deadlock=False, device=device)
-    with raftmc.ModelChecker(cfg) as mc:
-        mc.init()  # (buffers grow on the way: one untimed pass first)
-        for _ in range(D - 1):
-            mc.step()
-        mc.reset()
-        t0 = time.perf_counter()
-        gpu_levels = [mc.init().new_states]
-        for _ in range(D - 1):
-            gpu_levels.append(mc.step().new_states)
-        gpu_s = time.perf_counter() - t0
-    return {"value": round(dist.value / dt, 1), "unit": "distinct states/s", "cores": threads, "cpu_model": cpu_model(),
-            "kind": "port", "levels": D, "distinct_states": dist.value, "seconds": round(dt, 3),
-            "gpu_seconds_same_levels": round(gpu_s, 4),
-            "gpu_distinct_per_s_same_levels": round(dist.value / gpu_s, 1) if gpu_s > 0 else None,
-            "gpu_over_cpu_same_levels": round(dt / gpu_s, 1) if gpu_s > 0 else None,
-            "levels_match_gpu": cpu_levels == gpu_levels, "verdict_code": v,
-            "sample": f"Raft.cfg levels 1-{D} ({dist.value} distinct states) by oracle/raft_mt.c on {threads} threads "
-                      f"(C restatement of Raft.tla, exact canonical forms, level-synchronous first-wins BFS; not TLC: no "
-                      f"JVM/tla2tools.jar on the box), {dt:.1f} s; the GPU's seconds are those of the same levels of the "
-                      f"at-scale run (the small early levels are latency-bound on the GPU, so the ratio over the whole "
-                      f"exhaustion is larger)"}
+# kernel-name prefixes per phase of the fused (device-loop) levels
+KERNEL_NAME = {"expand_hash": "void rmc::k_expand_items<{n}, {V}, {mr}, false, true,",
+               "dedup": "void rmc::k_wincount<{n}, {V}, {mr}>(rmc::KParams)",
+               "materialize": "void rmc::k_commit_items<{n}, {V}, {mr}, "}
 
 
-def at_scale(device, workload="raftcfg", probes_per_s=None):
-    """configs[0]/[2] -- Raft.cfg as shipped -- exhausted on this GPU (not the headline: one run is
-    ~46 s).  The first run includes growing every buffer (the seen set's move to 8-B slots, the
-    frontier ring, the host trace); the second, after rmc_reset, is the steady state.  Its
-    first 34 levels are compared with the C oracle's (tests/golden/levels_prefix.json)."""
-    import raftmc
-    w = WORKLOADS[workload]
-    cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
-                             invariants=("Inv",), check_deadlock=False, device=device, timing_phases=TIMED_PHASES)
-    with raftmc.ModelChecker(cfg) as mc:
-        mc.set_timing(TIMED_PHASES)
-        t0 = time.perf_counter()
-        cold = mc.run()
-        dt_cold = time.perf_counter() - t0
-        mc.reset()
-        mc.set_timing(0)
-        t0 = time.perf_counter()
-        res = mc.run()
-        dt = time.perf_counter() - t0
-    ms = sum(ls.kernel_ms[PHASES.index("expand_hash")] for ls in cold.levels)
-    S, CCWB = record_bytes(cold, cfg)
-    # each expansion's bytes, chunk by chunk as the engine cuts the level (chunk_parents): a chunk of >= 2^16
-    # parents is split (k_expand<SPLIT>: no fingerprints, probe or election -- those are k_hash_probe's);
-    # a level's successors and new states are spread over its chunks in proportion to their parents
-    cp = chunk_parents(w["n"], w["V"])
-    alg = 0
-    for ls in cold.levels[1:]:  # (levels[0] is Init's)
-        F = ls.expanded
-        for c0 in range(0, F, cp):
-            f = min(cp, F - c0)
-            alg += alg_bytes("expand_hash", f, ls.generated * f / F, ls.new_states * f / F, S, CCWB,
-                             cold.seen_slot_bytes, staging_bytes(cfg), split=f >= (1 << 16),
-                             CTXB=ctx_bytes(w["n"], w["V"]), Gself=ls.self_loops * f / F)
-    gbs = alg / (ms / 1e3) / 1e9 if ms > 0 else 0.0
-    gold = {}
-    gpath = os.path.join(ROOT, "tests", "golden", "levels_prefix.json")
-    if os.path.exists(gpath):
-        with open(gpath) as f:
-            gold = json.load(f).get(f"n{w['n']}_v{w['V']}_e{w['E']}_r{w['R']}", {})
-    match = None
-    if gold:
-        got = [ls.new_states for ls in res.levels]
-        match = got[:len(gold["levels"])] == gold["levels"]
-    return {"workload": w["desc"], "distinct_states": res.distinct, "states_generated": res.generated,
-            "depth": res.depth, "verdict": "Inv holds" if res.status == "done" else res.status,
-            "seconds_to_exhaust": round(dt, 3), "distinct_per_s": round(res.distinct / dt, 1),
-            "generated_per_s": round(res.generated / dt, 1),
-            "self_loops": sum(ls.self_loops for ls in res.levels),
-            "self_loop_frac": round(sum(ls.self_loops for ls in res.levels) / max(1, res.generated), 4),
-            "first_run_seconds_incl_allocation": round(dt_cold, 3),
-            "matches_c_oracle_prefix_levels": match, "c_oracle_prefix_levels": len(gold.get("levels", [])),
-            "seen_set": f"{res.seen_slots} x {res.seen_slot_bytes} B slots",
-            "frontier_ring_bytes": res.frontier_ring_bytes, "frontier_peak_bytes": res.frontier_peak_bytes,
-            "record_bytes_avg": round(S, 2),
-            "expand_kernel_ms": round(ms, 3), "expand_alg_GBps": round(gbs, 1),
-            "expand_frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4),
-            "counters": counters_at_scale(workload),
-            "survey_roofline": survey_roofline(res.levels, S, dt, probes_per_s)}
+def split_kernel_name(n, V):
+    return f"void rmc::k_expand_items<{n}, {V}, {1 if n <= 3 else 2}, false, false, 64>"
 
 
-# kernel-name prefixes per phase: the item-parallel fused kernels (round 5) first, then round 4's
-KERNEL_NAME = {"expand_hash": ["void rmc::k_expand_items<{n}, {V}, {mr}, false, true,",
-                               "void rmc::k_expand<{n}, {V}, {mr}, 4, false>(rmc::KParams)",
-                               "void rmc::k_expand<{n}, {V}, {mr}, 4>(rmc::KParams)"],
-               "dedup": ["void rmc::k_wincount<{n}, {V}, {mr}>(rmc::KParams)"],
-               "materialize": ["void rmc::k_commit_items<{n}, {V}, {mr}, ",
-                               "void rmc::k_commit<{n}, {V}, {mr}, false>(rmc::KParams)",
-                               "void rmc::k_commit<{n}, {V}, {mr}>(rmc::KParams)"]}
-
-
-PMC_RUNS = 6  # tools/pmc.sh: bench.py --steps 5 --warmup 1 per counter pass
+PMC_RUNS = 6  # tools/pmc.sh: bench.py --workload c2 --steps 5 --warmup 1 per counter pass
 VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions per second on MI355X
 
 
-def pmc_kernel(mc, phase, workload, depth):
-    """Per launch of the dominant kernel, from the committed rocprofv3 PMC summary
-    (tools/pmc.sh + tools/pmc_summary.py): HBM bytes (FETCH_SIZE x2 correction per
-    MI355X_MICROARCH.md + WRITE_SIZE) and VALU wave-instructions (SQ_INSTS_VALU)."""
+def pmc_kernel(n, V, workload, prefix, dispatches_real=None):
+    """Per launch of a kernel, from the committed rocprofv3 PMC summary of bench.py's workload
+    (profiles/r*_pmc_<workload>.json: tools/pmc.sh + tools/pmc_summary.py): HBM bytes (FETCH_SIZE x2
+    correction per MI355X_MICROARCH.md + WRITE_SIZE) and VALU wave-instructions (SQ_INSTS_VALU).
+    dispatches_real: the launches that did work (the device loop's trailing launches return at once)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}.json")))
-    if not files or phase not in KERNEL_NAME:
+    if not files:
         return {}
-    n, V = mc.cfg.n_servers, mc.cfg.n_vals
-    mr = 1 if (mc.cfg.msg_cap or (64 if n <= 3 else 128)) <= 64 else 2
     d = json.load(open(files[-1]))
-    e = None
-    for name in KERNEL_NAME[phase]:  # kernel-name prefixes, newest first
-        pre = name.format(n=n, V=V, mr=mr)
-        e = e or next((d[k] for k in sorted(d) if k.startswith(pre) and isinstance(d[k], dict)), None)
+    e = next((d[k] for k in sorted(d) if k.startswith(prefix) and isinstance(d[k], dict)), None)
     if not e:
         return {}
-    # the device-driven level loop enqueues a few levels past the last one, whose launches
-    # return at once: spread each pass's totals over the launches that expanded a level
-    real = PMC_RUNS * depth
-    scale = e["dispatches"] / real if e["dispatches"] >= real else 1.0
-    out = {"source": os.path.relpath(files[-1], ROOT)}
+    scale = e["dispatches"] / dispatches_real if dispatches_real and e["dispatches"] >= dispatches_real else 1.0
+    out = {"source": os.path.relpath(files[-1], ROOT), "dispatches": e["dispatches"]}
     if "hbm_bytes_per_dispatch" in e:
         out["traffic"] = round(e["hbm_bytes_per_dispatch"] * scale)
     if "SQ_INSTS_VALU" in e:
@@ -725,6 +611,143 @@ def record_bytes(res, cfg):
     ns = sum(ls.new_states for ls in res.levels)
     ccwb = 4 * codec_words(cfg.n_servers, cfg.n_vals)
     return (nb / ns if ns else float(ccwb)), ccwb
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="raftcfg", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe-peak", action="store_true")
+    ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] leg (N = 1)")
+    ap.add_argument("--configs3", action="store_true", help="N > 1: first take configs[3] as deep as the node's "
+                    "HBM and a time budget allow (child processes, before the bench touches the GPU)")
+    ap.add_argument("--sharded-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--sharded-out", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--child-budget", type=float, default=C4_BUDGET_S, help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if args.sharded_child:
+        sharded_child(args)
+        return
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    sharded_c4 = None
+    if world > 1 and args.configs3:
+        sharded_c4 = run_child(args, "c4", C4_TIMEOUT_S, budget_s=C4_BUDGET_S)
+
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")  # control plane only: barriers and the max-over-ranks time
+    torch.cuda.set_device(local)
+
+    import raftmc
+    w = WORKLOADS[args.workload]
+    cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
+                             invariants=("Inv",), check_deadlock=False, device=local,
+                             timing_phases=TIMED_PHASES)
+    parallelism = "single-gpu"
+    if world > 1:
+        # rank 0 creates the RCCL id; the control-plane group (gloo) broadcasts it
+        idt = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            idt = torch.tensor(list(raftmc.comm_unique_id()), dtype=torch.uint8)
+        dist.broadcast(idt, 0)
+        cfg.rank, cfg.world_size, cfg.comm_unique_id = rank, world, bytes(idt.tolist())
+        parallelism = (f"rccl-{world}: levels of >= 2^20 states block-cyclic over the GPUs with a fingerprint-owner "
+                       f"seen set and TLC-order global-key election (RCCL exchange per round); smaller levels "
+                       f"replicated on every GPU")
+    mc, err = None, ""
+    try:
+        mc = raftmc.ModelChecker(cfg)
+    except raftmc.RmcError as e:
+        if world == 1:
+            raise
+        err = str(e)
+    if world > 1:
+        ok = torch.tensor([0 if mc is None else 1], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same mode
+        if int(ok.item()) == 0:
+            print(f"rank {rank}: sharded RCCL path unavailable ({err or 'another rank failed'}); running replicas",
+                  file=sys.stderr, flush=True)
+            if mc is not None:
+                mc.close()
+            cfg.rank, cfg.world_size, cfg.comm_unique_id = 0, 1, None
+            mc = raftmc.ModelChecker(cfg)
+            parallelism = f"replicas (sharded RCCL init failed: {err or 'on another rank'})"
+    big = args.workload != "c2"
+    res, elapsed, timed, first_s = measure(mc, args.steps, args.warmup, world, torch.cuda.synchronize,
+                                           args.workload, timing_every=1 if big else 8, report_steps=big)
+    assert res is not None and res.status == "done", res
+    ms_per_step = elapsed / args.steps * 1e3
+    # replicas (RCCL unavailable) each exhaust the whole space: the job is still ONE exhaustion, so
+    # value stays its distinct states / time (never multiplied by the replica count)
+    value = res.distinct * args.steps / elapsed
+    S, _ = record_bytes(res, mc.cfg)
+    rworld = world if parallelism.startswith("rccl") else 1
+    if big:
+        roof = split_roofline(timed, S, mc.cfg, rworld)
+        roof["counters_at_scale"] = counters_at_scale(args.workload) if args.workload == "raftcfg" else None
+    else:
+        roof = phase_roofline(timed, S, mc.cfg, args.workload, res.depth)
+    self_loops = sum(ls.self_loops for ls in res.levels)
+    match, prefix_levels = oracle_prefix_match(res, w)
+    config = {"workload": w["desc"], "distinct_states": res.distinct, "states_generated": res.generated,
+              "depth": res.depth, "verdict": "Inv holds" if res.status == "done" else res.status,
+              "parallelism": parallelism, "self_loops": self_loops,
+              "self_loop_frac": round(self_loops / max(1, res.generated), 4),
+              "seen_set": f"{res.seen_slots} x {res.seen_slot_bytes} B slots (rank 0)",
+              "frontier_ring_bytes": res.frontier_ring_bytes, "frontier_peak_bytes": res.frontier_peak_bytes,
+              "first_run_seconds_incl_allocation": round(first_s, 3) if first_s else None,
+              "matches_c_oracle_prefix_levels": match, "c_oracle_prefix_levels": prefix_levels}
+    # seen-set probe throughput of the run (one probe per fingerprinted successor, one insert per new state)
+    # against the random-probe peak of the slot layout measured on this GPU: a table far beyond the caches
+    # (2^28 16-B slots = 4 GiB, HBM-resident) and one of 2^22 slots (L2/MALL-resident)
+    probes = res.generated - self_loops + res.distinct
+    seen = {"probes_per_step": probes, "achieved_probes_per_s": round(probes * args.steps / elapsed, 1)}
+    pk_hbm = None
+    if rank == 0 and not args.no_probe_peak:
+        pk_small = raftmc.probe_peak(local, 22, 1 << 26)
+        pk_hbm = raftmc.probe_peak(local, 28, 1 << 28)
+        seen.update({"peak_probes_per_s_2^22_slots": round(pk_small, 1),
+                     "peak_probes_per_s_2^28_slots": round(pk_hbm, 1),
+                     "frac_of_hbm_probe_peak": round(probes * args.steps / elapsed / pk_hbm, 5), "slot_bytes": 16})
+    line = {
+        "metric": "distinct states/sec (whole node) + wall-time to exhaust",
+        "value": round(value, 1),
+        "unit": "distinct states/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: the state space of Raft.tla itself, generated from Init on the GPU each step",
+        "config": config,
+        "roofline": roof,
+        "seen_set": seen,
+        "survey_roofline": survey_roofline(res.levels, S, elapsed / args.steps, pk_hbm),
+    }
+    if world > 1:
+        line["xgmi_bytes_model"] = xgmi_model(res.levels, rworld)
+        line["xgmi_GBps_avg"] = round(line["xgmi_bytes_model"] / (elapsed / args.steps) / 1e9, 2)
+    mc.close()
+    if rank == 0 and world == 1 and args.workload != "c2" and not args.no_configs1:
+        line["configs1"] = configs1_leg(local, args, pk_hbm)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = (cpu_baseline_raftcfg(local) if args.workload == "raftcfg" else
+                                cpu_baseline(w) if args.workload == "c2" else None)
+    if rank == 0 and sharded_c4 is not None:
+        line["at_scale_sharded_configs3"] = sharded_c4
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -129,9 +129,9 @@ typedef struct rmc_level_stats {
     uint64_t kernel_launches[6];
     uint64_t new_bytes;       /* ABI 3: bytes of the new states' frontier records (packed core + message ids) */
     uint64_t self_loops;      /* ABI 5: generated successors equal to their parent (FollowerAcceptEntry that
-                                 changes nothing), among `generated`, where the run set them apart (single-GPU
-                                 levels -- split chunks and the item-parallel fused levels: never fingerprinted,
-                                 the parent is in the seen set); else 0 (sharded rounds) */
+                                 changes nothing), among `generated`.  Single-GPU levels set them apart (never
+                                 fingerprinted: the parent is in the seen set); sharded rounds set them apart in
+                                 split rounds and route them in smaller rounds, counting them either way */
 } rmc_level_stats;
 
 /* Final result of a run: TLC's closing lines. */
@@ -247,6 +247,12 @@ int rmc_probe_peak(int device, uint32_t table_log2, uint64_t probes, double *pro
 
 const char *rmc_last_error(void *ctx);
 void rmc_destroy(void *ctx);
+/* Frees every device allocation of the context (seen set, frontier ring, chunk buffers, streams, the
+ * communicator) and its pinned buffers, but not the host copy of the trace (~110 GB at Raft.cfg): a
+ * process about to exit returns the device at once and leaves the host memory to the kernel.  Only
+ * rmc_destroy may follow (every other call returns RMC_E_STATE).  The launcher's detached worker calls it
+ * before it reports TLC's exit code, so a GPU job started when myrun.sh returns finds the device free. */
+int rmc_release_device(void *ctx);
 
 /* ---- single-state hooks (parity tests; same kernels as rmc_step) -------------- */
 /* Successors of one state, in TLC enumeration order.  keys[i] = server<<24 |

@@ -95,3 +95,48 @@ def test_c4_leg_stops_together_on_capacity(tmp_path):
 def test_c4_leg_skipped_when_any_rank_lacks_time(tmp_path):
     r = _run(tmp_path, [120.0, 10.0])
     assert "skipped" in r and "levels_completed" not in r
+
+
+def _measure_worker(rank, world, port, out):
+    """bench.measure at N = 2 with a stand-in checker whose exhaustion takes 1 s on rank 0 and 3 s on
+    rank 1 (a simulated clock): W warmup steps untimed, exactly K timed, the max over ranks."""
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    import bench
+    clock = [0.0]
+    calls = {"run": 0, "timing": []}
+
+    class Res:
+        distinct, status, levels = 7, "done", ["levels"]
+
+    class MC:
+        def reset(self):
+            pass
+
+        def set_timing(self, m):
+            calls["timing"].append(m)
+
+        def run(self):
+            calls["run"] += 1
+            clock[0] += 1.0 + 2.0 * rank
+            return Res()
+
+    bench.time = types.SimpleNamespace(perf_counter=lambda: clock[0])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res, elapsed, timed, first_s = bench.measure(MC(), 5, 2, world, lambda: None, "t", timing_every=2,
+                                                 report_steps=False)
+    dist.destroy_process_group()
+    if rank == 0:
+        with open(out, "w") as f:
+            json.dump({"elapsed": elapsed, "timed": len(timed), "first": first_s, "runs": calls["run"],
+                       "timing": calls["timing"]}, f)
+
+
+def test_bench_measure_takes_the_slowest_rank(tmp_path):
+    out = str(tmp_path / "m.json")
+    mp.spawn(_measure_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r = json.load(open(out))
+    assert r["runs"] == 7 and r["first"] == 1.0
+    assert r["elapsed"] == pytest.approx(15.0)  # rank 1: 5 timed steps of 3 s
+    assert r["timed"] == 3 and r["timing"] == [2, 0, 2, 0, 2]

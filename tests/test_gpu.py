@@ -563,7 +563,7 @@ def test_sharded_level_stats_equal_single(name, shards):
     one, r1 = run_cfg(g, device_levels=1)
     many, rw = run_cfg(g, virtual_shards=shards, chunk_successors=3000, shard_min_states=1)
     key = lambda ls: (ls.level, ls.expanded, ls.generated, ls.new_states, ls.queue, ls.total_generated,
-                      ls.total_distinct, ls.status)
+                      ls.total_distinct, ls.status, ls.self_loops)
     assert [key(x) for x in rw.levels] == [key(x) for x in r1.levels]
     assert (rw.status, rw.distinct, rw.generated, rw.queue, rw.depth) == (r1.status, r1.distinct, r1.generated,
                                                                           r1.queue, r1.depth)
@@ -683,6 +683,41 @@ def test_sharded_resume_rejects_another_layout(tmp_path):
     with raftmc.ModelChecker(raftmc.ModelConfig(**base)) as c:
         with pytest.raises(raftmc.RmcError, match="another shard layout"):
             c.resume(path)
+
+
+def test_sharded_resume_adopts_a_smaller_stored_chunk(tmp_path):
+    """A sharded checkpoint written with a smaller chunk size (chunk_successors) than the resuming context's
+    is adopted -- the block-cyclic layout needs the writer's size and the larger buffers hold it -- and the
+    run finishes with the golden counts; a larger stored chunk is refused, and the refusing context still
+    runs from Init with its own chunk size (the adoption is undone when a resume fails)."""
+    g = LEVELS["n3_v1_e2_r3"]
+    small, large = str(tmp_path / "small.ckpt"), str(tmp_path / "large.ckpt")
+    base = dict(n_servers=3, n_vals=1, max_election=2, max_restart=3, shard_min_states=1, virtual_shards=2)
+    for path, cs in ((small, 3000), (large, 12000)):
+        with raftmc.ModelChecker(raftmc.ModelConfig(**base, chunk_successors=cs)) as a:
+            a.init()
+            for _ in range(6):
+                a.step()
+            a.checkpoint(path)
+    with raftmc.ModelChecker(raftmc.ModelConfig(**base, chunk_successors=6000)) as b:
+        b.resume(small)
+        res = b.run()
+        assert (res.status, res.distinct, res.generated, res.depth) == ("done", g["distinct"], g["generated"],
+                                                                        g["depth"])
+        assert [ls.new_states for ls in res.levels if ls.new_states] == g["levels"][7:]
+    with raftmc.ModelChecker(raftmc.ModelConfig(**base, chunk_successors=6000)) as c:
+        with pytest.raises(raftmc.RmcError, match="another shard layout"):
+            c.resume(large)
+        check_levels(g, c.run())
+    # adopted, then refused further on (a corrupt data section): the context keeps its own chunk size
+    data = bytearray(open(small, "rb").read())
+    data[-20] ^= 0xFF
+    bad = str(tmp_path / "bad.ckpt")
+    open(bad, "wb").write(bytes(data))
+    with raftmc.ModelChecker(raftmc.ModelConfig(**base, chunk_successors=6000)) as d:
+        with pytest.raises(raftmc.RmcError):
+            d.resume(bad)
+        check_levels(g, d.run())
 
 
 def test_resume_rejects_another_configuration(tmp_path):
@@ -937,18 +972,34 @@ def _oracle_self_loops(name):
     return want
 
 
-@pytest.mark.parametrize("mode", ["device_loop", "host_fused", "split"])
+SHARDED_SELF_MODES = {
+    "virtual2": dict(virtual_shards=2, chunk_successors=3000, shard_min_states=1),
+    "virtual3": dict(virtual_shards=3, chunk_successors=3000, shard_min_states=1),
+    "rccl1": dict(world_size=1, rank=0, chunk_successors=3000, shard_min_states=1),
+}
+
+
+@pytest.mark.parametrize("mode", ["device_loop", "host_fused", "split", "virtual2", "virtual3", "rccl1",
+                                  "virtual2_split", "rccl1_split"])
 @pytest.mark.parametrize("name", SELF_LOOP_CASES)
 def test_self_loops_per_level_match_oracle(name, mode, monkeypatch):
     """rmc_level_stats.self_loops (ABI 5): per expanded level, the successors equal to their parent
     (FollowerAcceptEntry changing nothing, tla:275-300) -- counted by the item-parallel fused expansion
-    (device loop and host-driven chunks) and by a split chunk's winner count -- equal the oracle's count
-    of successors identical to their parent (oracle/raft_ref.py successors, exact state equality)."""
+    (device loop and host-driven chunks), by a split chunk's winner count, and on the sharded path (2 / 3
+    virtual shards, a one-rank RCCL communicator; rounds below the split size count them in the routed
+    expansion, split rounds in the winner count) -- equal the oracle's count of successors identical to
+    their parent (oracle/raft_ref.py successors, exact state equality)."""
     g = LEVELS[name]
     want = _oracle_self_loops(name)
-    if mode == "split":
+    if mode.endswith("split"):
         monkeypatch.setenv("RMC_SPLIT_MIN", "1")
-    mc, res = run_cfg(g, **({} if mode == "device_loop" else {"device_levels": 1}))
+    base = mode[:-len("_split")] if mode.endswith("_split") else mode
+    kw = dict(SHARDED_SELF_MODES.get(base, {}))
+    if base == "rccl1":
+        kw["comm_unique_id"] = raftmc.comm_unique_id()
+    if base in ("host_fused", "split"):
+        kw["device_levels"] = 1
+    mc, res = run_cfg(g, **kw)
     check_levels(g, res)
     got = [ls.self_loops for ls in res.levels[1:]]
     assert got == want[:len(got)] and sum(got) == sum(want), (got, want)

@@ -57,7 +57,20 @@ def test_library_exports_every_declared_symbol():
     assert len(decl) >= 14
     for name in decl:
         assert hasattr(lib, name), name
-    assert lib.rmc_abi_version() == 5
+    assert lib.rmc_abi_version() == raftmc.ABI_VERSION == 5
+
+
+def test_load_library_refuses_another_abi(tmp_path, monkeypatch):
+    """A librmc.so of another ABI is refused, not decoded with the wrong struct strides (round 5's r05i
+    failure: an ABI-4 race-probe build read through the ABI-5 rmc_level_stats)."""
+    src = tmp_path / "old.c"
+    src.write_text("int rmc_abi_version(void) { return 4; }\n")
+    so = tmp_path / "librmc_old.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)], check=True)
+    monkeypatch.setattr(raftmc, "_lib", None)
+    with pytest.raises(raftmc.RmcError, match="ABI 4"):
+        raftmc.load_library(str(so))
+    assert raftmc._lib is None
 
 
 def test_parse_shipped_config_equivalent():
@@ -241,10 +254,11 @@ def test_bench_xgmi_model():
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    levels = [L(expanded=10, generated=50, new_bytes=400, new_states=10),
-              L(expanded=2 ** 20, generated=100, new_bytes=800, new_states=20),
-              L(expanded=100, generated=10, new_bytes=0, new_states=0)]
+    levels = [L(expanded=10, generated=50, new_bytes=400, new_states=10, self_loops=5),
+              L(expanded=2 ** 20, generated=130, new_bytes=800, new_states=20, self_loops=30),
+              L(expanded=100, generated=10, new_bytes=0, new_states=0, self_loops=0)]
     assert bench.xgmi_model(levels, 1) == 0
+    # (self-loops of a split round are set apart, never routed)
     per = 100 * 28 + 800 + 16 * 20 + 10 * 28
     assert bench.xgmi_model(levels, 2) == per // 2
     assert bench.xgmi_model(levels, 8) == int(per * 7 / 8)
@@ -270,6 +284,43 @@ def test_bench_split_bytes_account_for_the_probe_pass():
     split = bench.alg_bytes("expand_hash", F, G, N, S, 16, 8, 32, split=True, CTXB=ctxb) + \
         bench.alg_bytes("probe", F, G, N, S, 16, 8, 32, CTXB=ctxb)
     assert split == fused + F * (4 + 2 * ctxb) + G * 32
+
+
+def test_bench_split_roofline_levels_and_bytes():
+    """The headline roofline counts the levels whose every chunk is split (>= 2^16 parents; a level whose tail
+    chunk is smaller runs that chunk on the fused kernel and is left out), their chunks' algorithmic bytes
+    (alg_bytes split=True with the level's successors spread by parents) over their HIP-event expansion time."""
+    from types import SimpleNamespace as L
+    bench = _bench()
+    cfg = L(n_servers=3, n_vals=2, chunk_successors=0)
+    cp = bench.chunk_parents(3, 2)
+    assert cp == 3050402
+
+    def lv(F, G, N, slf, ms, k):
+        ph = [0.0] * 6
+        ph[bench.PH_EXPAND] = ms
+        la = [0] * 6
+        la[bench.PH_EXPAND] = k
+        return L(expanded=F, generated=G, new_states=N, self_loops=slf, kernel_ms=ph, kernel_launches=la)
+    levels = [lv(1, 3, 1, 0, 0.0, 1),                    # Init's level (skipped)
+              lv(1000, 5000, 2000, 100, 0.05, 1),        # fused: below the split size
+              lv(2 * cp, 10 * cp, 3 * cp, cp, 80.0, 2),  # two whole split chunks
+              lv(cp + 1000, 5 * cp, cp, 0, 50.0, 2),     # a fused tail chunk: left out
+              lv(cp + 70000, 5 * cp, cp, 0, 60.0, 2)]    # a split tail chunk
+    r = bench.split_roofline([levels], 69.5, cfg)
+    assert r["launches"] == 4 and r["levels"] == 2
+    want = 0.0
+    for F, G, N, slf in ((2 * cp, 10 * cp, 3 * cp, cp), (cp + 70000, 5 * cp, cp, 0)):
+        for c0 in range(0, F, cp):
+            f = min(cp, F - c0)
+            want += bench.alg_bytes("expand_hash", f, G * f / F, N * f / F, 69.5, 16, SWB=32, split=True, CTXB=112,
+                                    Gself=slf * f / F)
+    assert r["algorithmic_bytes_per_launch"] == round(want / 4)
+    assert abs(r["achieved"] - want / 0.140 / 1e9) < 0.01
+    assert r["frac"] == round(r["achieved"] / bench.HBM_PEAK_GBS, 5)
+    # at N > 1 a rank expands 1/N of every level
+    r2 = bench.split_roofline([levels], 69.5, cfg, world=2)
+    assert abs(r2["algorithmic_bytes_per_launch"] - round(want / 8)) <= 1
 
 
 def test_bench_counters_at_scale_read_from_profiles():

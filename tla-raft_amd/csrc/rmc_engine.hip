@@ -516,6 +516,7 @@ struct rmc_ctx {
 
     // progress
     bool inited = false, finished = false;
+    bool device_released = false;  // rmc_release_device: only rmc_destroy may follow
     int status = RMC_OK;
     int depth = 0;
     uint64_t total_generated = 0, total_distinct = 0, queue_at_end = 0;
@@ -1012,7 +1013,7 @@ struct rmc_ctx {
         s.pslot = dmalloc<uint16_t>(s.trace_cap);
     }
 
-    void free_shard(Shard &s) {
+    void free_shard(Shard &s, bool keep_host_trace = false) {
         dfree(s.R); dfree(s.cur_off); dfree(s.nxt_off); dfree(s.T); dfree(s.Tc); dfree(s.par); dfree(s.pslot);
         dfree(s.cnt);
         dfree(s.lslot); dfree(s.wpos); dfree(s.fp); dfree(s.E); dfree(s.tmp);
@@ -1029,18 +1030,23 @@ struct rmc_ctx {
         if (s.hloop) (void)hipHostFree(s.hloop);
         if (s.hlrec) (void)hipHostFree(s.hlrec);
         s.hsum = nullptr; s.hctl = nullptr; s.hloop = nullptr; s.dloop = nullptr; s.hlrec = nullptr;
-        s.hpar.release();
-        s.hslot.release();
+        if (!keep_host_trace) {
+            s.hpar.release();
+            s.hslot.release();
+        }
         if (s.tev) (void)hipEventDestroy(s.tev);
         s.tev = nullptr;
     }
 
-    void release() {
+    // Every device allocation, stream, event and communicator (and the pinned buffers); with
+    // keep_host_trace the shards' host trace blocks stay (rmc_release_device: the process exits next and
+    // the kernel returns them).  Idempotent: rmc_destroy after rmc_release_device frees the rest.
+    void release(bool keep_host_trace = false) {
         if (stream) (void)hipStreamSynchronize(stream);
         if (cstream) (void)hipStreamSynchronize(cstream);
         stager.reset();  // (its thread finishes the pieces already copied: before the blocks go)
-        for (Shard &s : sh) free_shard(s);
-        sh.clear();
+        for (Shard &s : sh) free_shard(s, keep_host_trace);
+        if (!keep_host_trace) sh.clear();
         dfree(d_info); dfree(d_nat2id); dfree(d_gmsg); dfree(d_seeds);
         dfree(d_one); dfree(d_init_rec); dfree(d_init_fp); dfree(d_out); dfree(d_keys); dfree(d_cnt1); dfree(d_fp1); dfree(d_inv); dfree(d_err1);
         dfree(d_flags1); dfree(d_red);
@@ -1856,6 +1862,9 @@ struct rmc_ctx {
         if (f & 4u) return "race probe: the commit's arrival counters were not all re-armed when the level finished";
         return "internal: unknown flag " + std::to_string(f);
     }
+    // the return code of a chunk's flags: a state past msg_cap (bit 0) is a capacity failure, anything
+    // else an internal invariant of the engine that failed (RMC_E_STATE)
+    static int flag_code(unsigned long long f) { return (f & 1u) ? RMC_E_CAPACITY : RMC_E_STATE; }
 
     static int first_error(const unsigned long long *e, unsigned long long *best) {
         int kind = -1;
@@ -1925,24 +1934,29 @@ struct rmc_ctx {
             const bool split = split_min && np_ >= split_min;
             // a split chunk's winners go into the seen set in its commit (k_commit_items reads the
             // election words itself: no k_insert_winners pass) when the items commit takes its slots
-            const bool fold = split && nzlist && fold_insert && ks.maxsucc <= 256;
+            const bool fold = split && ks.maxsucc <= 256;
             auto params = [&] {
                 KParams Q = chunk_params(s);
                 Q.p_begin = p0; Q.p_end = p1; Q.next_base = s.nxt_n; Q.next_wbase = s.nxt_words;
                 Q.gid_next_base = gid_nxt; Q.gid_parent_base = gid_cur;
                 Q.Lmask = Lcap - 1;
                 Q.epoch = s.epoch;
-                Q.split = split ? (fold ? 1 : (split_insert ? split_flags : 1)) : 0;
-                Q.plist = split && nzlist ? s.plist : nullptr;
+                // (a chunk whose 256-lane commit cannot take a parent's slots -- the BecomeFollower variant at
+                // n >= 4 -- inserts its winners in a pass of its own, k_insert_winners, and leaves the verdicts
+                // in lslot for k_commit_split)
+                Q.split = split ? (fold ? 1 : 7) : 0;
+                Q.plist = split ? s.plist : nullptr;
                 // (a split chunk's self-loops are staged after the successors to fingerprint)
-                Q.hcnt = split && nzlist && (fold || (split_insert && split_flags == 7)) ? s.hcnt : nullptr;
+                Q.hcnt = split ? s.hcnt : nullptr;
                 s.chunk_sep = Q.hcnt != nullptr;
                 return Q;
             };
             // expand + fingerprint + seen-set probe + staging, one evaluation per parent (a split
             // chunk: expand + staging + hash context, then fingerprint + probe + election a lane per successor)
-            // (the chunk's self-loops: counted by the fused expansion or the split chunk's winner count)
-            HIPCHK(hipMemsetAsync(s.sum + SUM_SELF, 0, 8, stream));
+            // (the chunk's self-loops: counted by the fused expansion or the split chunk's winner count; the
+            // fused expansion's stripes are cleared with the sum, in case an earlier chunk stopped between its
+            // expansion and its commit)
+            HIPCHK(hipMemsetAsync(s.sum + SUM_SELF, 0, (SUM_SELF_STRIPE + SELF_STRIDE * SELF_STRIPES - SUM_SELF) * 8, stream));
             timed(PH_HASH, [&] {
                 if (split) ks.split(params(), stream);
                 else ks.fused(params(), stream);
@@ -1950,7 +1964,7 @@ struct rmc_ctx {
             if (split) timed(PH_OTHER, [&] { ks.hash_probe(params(), np_, stream); });
             timed(PH_DEDUP, [&] {
                 ks.wincount(params(), np_, stream);
-                if (split && nzlist) launch_nzlist(params(), np_, stream);
+                if (split) launch_nzlist(params(), np_, stream);
             });
             if (!small) {
                 HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
@@ -1964,10 +1978,10 @@ struct rmc_ctx {
             }
             trace_fence(s);
             // (timed with the winner count: PH_OTHER stays the probe pass alone)
-            if (split && split_insert && !fold) timed(PH_DEDUP, [&] { ks.insert(params(), np_, stream); });
+            if (split && !fold) timed(PH_DEDUP, [&] { ks.insert(params(), np_, stream); });
             // + chunk summary; a split chunk's winners a lane per successor slot of its parents with winners
             timed(PH_MAT, [&] {
-                if (split && nzlist && (fold || (split_insert && split_flags == 7))) ks.commit_split(params(), np_, stream);
+                if (split) ks.commit_split(params(), np_, stream);
                 else ks.commit(params(), stream);
             });
             HIPCHK(hipMemcpyAsync(s.hsum, s.sum, (SUM_SELF + 1) * 8, hipMemcpyDeviceToHost, stream));
@@ -1976,7 +1990,7 @@ struct rmc_ctx {
             collect_times(st);
             const uint64_t G = s.hsum[0], Wn = s.hsum[1], Ww = s.hsum[SUM_WORDS];
             level_self += s.hsum[SUM_SELF];
-            if (s.hsum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, flag_msg(s.hsum[2 + ERR_NSLOTS]));
+            if (s.hsum[2 + ERR_NSLOTS]) throw Fail(flag_code(s.hsum[2 + ERR_NSLOTS]), flag_msg(s.hsum[2 + ERR_NSLOTS]));
             flush_trace(s, gid_nxt + s.nxt_n + Wn);
             level_gen += G;
             s.T_count += Wn;
@@ -2032,16 +2046,6 @@ struct rmc_ctx {
     // parents per host-driven chunk from which the seen-set probe and election run as their own
     // pass (k_probe; 0 = always fused into the expansion)
     const uint64_t split_min = (uint64_t)env_int("RMC_SPLIT_MIN", 1 << 16, 0, 1 << 30);
-    // ... and their winners go into the seen set in a pass of their own too (k_insert_winners)
-    const bool split_insert = env_int("RMC_SPLIT_INSERT", 1, 0, 1) != 0;
-    // ... and their commit visits only the parents with winners (k_nzlist)
-    const bool nzlist = env_int("RMC_NZLIST", 1, 0, 1) != 0;
-    // KParams.split of such chunks (measurement knob): 7 = verdicts in lslot for the commit, 3 = the
-    // commit reads the election words itself
-    const int split_flags = env_int("RMC_SPLIT_FLAGS", 7, 3, 7) == 3 ? 3 : 7;
-    // split chunks whose commit is k_commit_items: the commit tests the election words and inserts the
-    // winners itself (RMC_FOLD_INSERT=0: the k_insert_winners pass and verdicts, as round 4)
-    const bool fold_insert = env_int("RMC_FOLD_INSERT", 1, 0, 1) != 0;
     const int dl_group = env_int("RMC_DL_GROUP", 2, 1, 64);
     const int dl_ahead = env_int("RMC_DL_AHEAD", 2, 1, 64);
     const int dl_query_us = env_int("RMC_DL_QUERY_US", 2000, 0, 1 << 30);
@@ -2247,7 +2251,7 @@ struct rmc_ctx {
             // the level the loop stopped in is intact: report its error as the host path does
             rmc_level_stats *st = &out[D];
             st->seconds = el / nst;
-            if (s.hsum[2 + ERR_NSLOTS]) throw Fail(RMC_E_CAPACITY, flag_msg(s.hsum[2 + ERR_NSLOTS]));
+            if (s.hsum[2 + ERR_NSLOTS]) throw Fail(flag_code(s.hsum[2 + ERR_NSLOTS]), flag_msg(s.hsum[2 + ERR_NSLOTS]));
             const int L = (int)s.level_start.size();
             st->level = L;
             st->expanded = s.cur_n;
@@ -2364,7 +2368,7 @@ struct rmc_ctx {
     // TLC order (the fused winner count + commit), and the winners go to the shards that own their
     // global next-level indices, appended in source order -- the level's order.  Levels, counters
     // at an error and traces are those of W = 1.
-    bool round_sep(const Shard &s) const { return split_min && s.np >= split_min && env_int("RMC_NZLIST", 1, 0, 1); }
+    bool round_sep(const Shard &s) const { return split_min && s.np >= split_min; }
     KParams round_params(const Shard &s, uint64_t gbase) const {
         KParams Q = chunk_params(s);
         Q.p_begin = s.p0;
@@ -2429,8 +2433,9 @@ struct rmc_ctx {
         }
     }
 
-    // per-shard round row: generated, winners, words, inserted, error kind + 1, error key, -failure code
-    static constexpr int TAB = 7;
+    // per-shard round row: generated, winners, words, inserted, error kind + 1, error key, -failure code,
+    // self-loops
+    static constexpr int TAB = 8;
 
     int step_sharded(rmc_level_stats *st) {
         auto t0 = std::chrono::steady_clock::now();
@@ -2452,7 +2457,7 @@ struct rmc_ctx {
         st->expanded = Fg;
         const uint64_t gbase = glevel[L - 1], rounds = (Fg + B * W - 1) / (B * W);
         const size_t NL = sh.size();
-        uint64_t level_gen = 0, level_new = 0, level_words = 0;
+        uint64_t level_gen = 0, level_new = 0, level_words = 0, level_self = 0;
         // A shard that runs out of seen-set or ring room, or meets a state past msg_cap, must not
         // leave the others waiting in a collective: it records the failure, skips its own kernels
         // and keeps exchanging; the round's table (and a last check at the round's end) carries the
@@ -2654,13 +2659,15 @@ struct rmc_ctx {
             std::vector<uint64_t> ins(NL, 0), wnum(NL, 0), wwords(NL, 0);
             for (size_t li = 0; li < NL; li++) {
                 Shard &s = sh[li];
-                HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 10 * 8, hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipMemcpyAsync(s.hsum, s.sum, (SUM_SELF + 1) * 8, hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
                 ins[li] = s.hsum[9];
                 if (s.np && !fail[li]) {
                     tab[TAB * s.id + 0] = s.hsum[0];
                     wnum[li] = s.hsum[1];
                     wwords[li] = s.hsum[SUM_WORDS];
+                    // self-loops: a split round's set apart (k_wincount), a fused round's counted by the expansion
+                    tab[TAB * s.id + 7] = s.hsum[SUM_SELF];
                 }
             }
             collect_times(st);
@@ -2687,7 +2694,7 @@ struct rmc_ctx {
                 HIPCHK(hipStreamSynchronize(stream));
                 HIPCHK(hipGetLastError());
                 if (s.hsum[2 + ERR_NSLOTS] && !fail[li]) {
-                    fail[li] = RMC_E_CAPACITY;
+                    fail[li] = flag_code(s.hsum[2 + ERR_NSLOTS]);
                     fail_msg = flag_msg(s.hsum[2 + ERR_NSLOTS]);
                 }
                 uint64_t *row = &tab[TAB * s.id];
@@ -2903,6 +2910,7 @@ struct rmc_ctx {
                 level_gen += tab[TAB * t + 0];
                 level_new += tab[TAB * t + 1];
                 level_words += tab[TAB * t + 2];
+                level_self += tab[TAB * t + 7];
             }
             // (no wait here: the next round's first read-back orders everything before it, and its
             // phase times are collected after that)
@@ -2914,6 +2922,7 @@ struct rmc_ctx {
         st->generated = level_gen;
         st->new_states = level_new;
         st->new_bytes = level_words * 4;
+        st->self_loops = level_self;
         for (Shard &s : sh) {
             const uint64_t gid_nxt = s.level_start[L - 1] + s.cur_n;
             s.peak_words = std::max(s.peak_words, s.nxt_words);  // (the level's rounds counted the rest)
@@ -3230,8 +3239,17 @@ struct rmc_ctx {
             h.spec_variant != want.spec_variant || h.no_symmetry != want.no_symmetry || h.msg_cap != want.msg_cap)
             fail(" is not a checkpoint of this configuration");
         if (h.scheme != want.scheme) fail(" was written with another fingerprint scheme");
-        // a smaller stored chunk size is adopted (the buffers hold it): the chunk follows free memory at
-        // create when budgets are explicit, so a resume on a device with less headroom must not fail
+        // A sharded checkpoint written with a SMALLER chunk size than this context's is adopted (the chunk
+        // buffers hold it; the block-cyclic layout needs the writer's size): the chunk follows free memory at
+        // create when budgets are explicit, so a context created with more headroom than the writer had
+        // resumes.  A larger stored chunk would need larger buffers than this context sized: refused below.
+        // The adoption is undone if the resume fails (cp_guard).
+        struct CpGuard {
+            uint64_t &cp;
+            const uint64_t before;
+            bool keep;
+            ~CpGuard() { if (!keep) cp = before; }
+        } cp_guard{chunk_parents, chunk_parents, false};
         if (multi && h.chunk_parents && h.chunk_parents < want.chunk_parents)
             want_chunk_parents_adopt = h.chunk_parents;
         else
@@ -3370,6 +3388,7 @@ struct rmc_ctx {
         inited = true;
         finished = sh[0].cur_n == 0 && (replicated || !multi);
         if (finished) { status = RMC_DONE; queue_at_end = 0; }
+        cp_guard.keep = true;
     }
 
     // Forget every explored state but keep all device buffers (repeat runs, benchmarks).
@@ -3436,6 +3455,10 @@ struct rmc_ctx {
 template <class F>
 static int guarded(rmc_ctx *c, F &&f) {
     if (!c) return RMC_E_ARG;
+    if (c->device_released) {
+        c->err = "the context's device memory was released (rmc_release_device): only rmc_destroy may follow";
+        return RMC_E_STATE;
+    }
     try {
         return f();
     } catch (const Fail &e) {
@@ -3639,6 +3662,14 @@ void rmc_destroy(void *ctx) {
     if (!c) return;
     c->release();
     delete c;
+}
+
+int rmc_release_device(void *ctx) {
+    rmc_ctx *c = (rmc_ctx *)ctx;
+    if (!c) return RMC_E_ARG;
+    c->release(true);
+    c->device_released = true;
+    return RMC_OK;
 }
 
 int rmc_successors(void *ctx, const int32_t *unpacked, int32_t *out, size_t stride, uint32_t cap, uint32_t *keys,

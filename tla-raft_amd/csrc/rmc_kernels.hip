@@ -24,7 +24,6 @@
 //   FUSED        single-GPU level: expand + fingerprint + seen-set probe + election + staging
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
 
 #include "rmc_kernels.h"
 
@@ -65,19 +64,13 @@ extern "C" int rmc_debug_phases(unsigned long long *out, int reset) {
 #ifndef RMC_WIDE_WAVES
 #define RMC_WIDE_WAVES 2
 #endif
-#ifndef RMC_FUSED_SKIPSELF  // the fused expansion sets self-loops apart (0: hashes and probes them, round 4)
-#define RMC_FUSED_SKIPSELF 1
-#endif
-#ifndef RMC_SPLIT_WAVES  // the split expansion (no fingerprints): waves per SIMD its registers are cut for
-#define RMC_SPLIT_WAVES 6
-#endif
 
 namespace rmc {
 
-// SINGLE: every successor of one state (parity hook); FUSED: expand + fingerprint + seen-set probe +
-// election + staging (device loop, small chunks, sharded rounds); SPLIT: expand + staging + the
-// parent's hash context only -- k_hash_probe fingerprints, probes and elects a lane per successor
-enum Mode { M_SINGLE = 3, M_FUSED = 4, M_SPLIT = 5 };
+// SINGLE: every successor of one state (parity hook); FUSED: expand + fingerprint + staging, the
+// fingerprints routed to their owners (sharded rounds below the split size).  Single-GPU levels and
+// split chunks use the item-parallel k_expand_items.
+enum Mode { M_SINGLE = 3, M_FUSED = 4 };
 
 template <int N>
 __device__ __forceinline__ uint32_t sel(const uint32_t *a, int i) {
@@ -1428,8 +1421,7 @@ __device__ __forceinline__ uint32_t probe_elect(const KParams &P, const ulonglon
 
 template <int N, int MR, int MODE, bool BFV>
 constexpr int expand_waves() {
-    return MODE == M_SPLIT ? ((MR == 1 && !BFV) ? RMC_SPLIT_WAVES : RMC_WIDE_WAVES)
-                           : ((N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((BFV && N >= 4) ? 1 : RMC_WIDE_WAVES));
+    return (N <= 3 && MR == 1 && !BFV) ? RMC_N3_WAVES : ((BFV && N >= 4) ? 1 : RMC_WIDE_WAVES);
 }
 
 // BFV: the BecomeFollower variant (tla:420) -- MR more candidates (one per message lane) and MR * 64
@@ -1438,30 +1430,28 @@ template <int N, int V, int MR, int MODE, bool BFV = false>
 __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expand(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
-    constexpr bool HASH = MODE != M_SPLIT;              // fingerprints in this kernel
     constexpr int MX = S::MAXS + (BFV ? S::MCAP : 0);   // successor slots per parent
     constexpr int NC = MR + 1 + (BFV ? MR : 0);         // candidates per lane: messages, slot, BecomeFollower
-    constexpr int HX = HASH ? MX : 1;                   // per-successor hash inputs, by TLC rank
-    constexpr int HB = !HASH ? 1 : (N <= 3 ? 32 : 64);  // successors hashed per batch
-    constexpr int FH = HASH ? 64 / HB : 1;              // lanes per batch successor: one per half when 2
+    constexpr int HX = MX;                              // per-successor hash inputs, by TLC rank
+    constexpr int HB = N <= 3 ? 32 : 64;                // successors hashed per batch
+    constexpr int FH = 64 / HB;                         // lanes per batch successor: one per half when 2
     __shared__ uint64_t M0[N * N], M1[N * N];           // the parent's message-hash sums per (src, dst)
     __shared__ uint32_t pcore[Lo::NW + N];
-    __shared__ uint64_t sK[2][HASH ? N * N : 1];        // position constants K_f[a][b]
-    __shared__ uint64_t pC[2][HASH ? N * N : 1];        // the parent's content matrix C_f[t][j]
-    __shared__ uint64_t psig[HASH ? N : 1];             // ... and its servers' signatures
+    __shared__ uint64_t sK[2][N * N];        // position constants K_f[a][b]
+    __shared__ uint64_t pC[2][N * N];        // the parent's content matrix C_f[t][j]
+    __shared__ uint64_t psig[N];             // ... and its servers' signatures
     // every successor's row inputs at its TLC rank: own word; matchIndex row | votedFor << 20;
     // nextIndex row; where its added messages' info words are (sAinf); acting server; |added|
     __shared__ uint64_t sUg[HX];
     __shared__ uint32_t sW1[HX], sW2[HX];
     __shared__ uint16_t sCa[HX];
     __shared__ uint8_t sS[HX], sNa[HX];
-    __shared__ uint16_t sRq[HX];                        // fused level: the TLC rank of each successor hashed
     // per batch successor: its acting row's contents, tie ranks, first task, running minimum;
     // per task lane: its partial minimum and successor
-    __shared__ uint64_t sC[2][HASH ? HB * N : 1];
-    __shared__ uint32_t sRk[HB], sKoff[HB], sTl[HASH ? 64 : 1];
-    __shared__ ulonglong2 sBest[HB], sPart[HASH ? 64 : 1];
-    __shared__ uint32_t sAinf[HASH ? (MR + 1) * 64 * S::NADD : 1];  // info words of the messages each candidate adds
+    __shared__ uint64_t sC[2][HB * N];
+    __shared__ uint32_t sRk[HB], sKoff[HB], sTl[64];
+    __shared__ ulonglong2 sBest[HB], sPart[64];
+    __shared__ uint32_t sAinf[(MR + 1) * 64 * S::NADD];  // info words of the messages each candidate adds
     extern __shared__ uint32_t sBM[];                    // bitmap of the parent's message ids (P.t.bmw words)
     if (MODE == M_FUSED && !level_args(P)) return;
     // device loop: the levels committed so far go to the host as this level starts (the write to
@@ -1471,7 +1461,7 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
     // device-loop grids are sized on a bound of the level: blocks past it leave before the LDS setup
     if (MODE == M_FUSED && P.p_begin + blockIdx.x >= P.p_end) return;
     const int lane = threadIdx.x;
-    if (HASH && lane < 2 * N * N) {
+    if (lane < 2 * N * N) {
         const int f = lane / (N * N), a = (lane / N) % N, b = lane % N;
         sK[f][a * N + b] = P.t.seeds[f * SEEDS_PER_F + a * MAXN + b];
     }
@@ -1484,6 +1474,7 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
     // expansion is at its register limit already).
     uint64_t p = P.p_begin + blockIdx.x, nstart = 0, nnstart = 0;
     uint32_t nrw0 = 0, nrw1 = 0;
+    uint32_t route_self = 0;  // sharded round: the wave's self-loops (sum[SUM_SELF], one atomic per wave)
     constexpr bool PREM = MR == 1;
     MsgPre<MR> pm;
     if (p < P.p_end) {
@@ -1498,7 +1489,6 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
         nstart = nnstart;
         if (p + 2ull * gridDim.x < P.p_end) nnstart = rec_start<S::RECW_MAX>(P, p + 2ull * gridDim.x);
         Wave<N, V, MR> W;
-        const uint32_t rec0 = nrw0;  // this parent's record words (lane k: word k; the split context keeps the core)
         if constexpr (PREM) {
             load_parent_pre<N, V, MR>(P, start, nrw0, lane, W, M0, M1, pcore, pm);
             if (more) fetch_record<MR, S::RECW_MAX>(P, nstart, lane, nrw0, nrw1);
@@ -1527,8 +1517,8 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
 #pragma unroll
         for (int r = 0; r < MR; r++)
             eval_msg<N, V, MR, BFV>(P, W, r, ln, cand[r], cand[BFV ? MR + 1 + r : r], akey,
-                                    HASH ? &sAinf[(r * 64 + ln) * S::NADD] : nullptr, mid[r]);
-        eval_slot<N, V, MR>(P, W, ln, cand[MR], HASH ? &sAinf[(MR * 64 + ln) * S::NADD] : nullptr, sid);
+                                    &sAinf[(r * 64 + ln) * S::NADD], mid[r]);
+        eval_slot<N, V, MR>(P, W, ln, cand[MR], &sAinf[(MR * 64 + ln) * S::NADD], sid);
         if constexpr (PREM) {
             if (more) fetch_msgs<N, V, MR>(P, nrw0, nrw1, lane, pm);
         } else {
@@ -1555,32 +1545,11 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
                 for (int r = 0; r < NC; r++) rank[r] += kt < cand[r].key ? 1u : 0u;
             }
         }
-        // fused level: a self-loop (the parent itself, FollowerAcceptEntry changing nothing -- ~40 % of
-        // configs[1]'s successors) is in the seen set already: it takes its slot with LS_SEEN and no
-        // fingerprint, probe or election; the others are hashed in TLC order at hrank (sharded rounds
-        // route every successor's fingerprint: none set apart)
-        constexpr bool SKIPSELF = MODE == M_FUSED && RMC_FUSED_SKIPSELF;
-        uint32_t hrank[NC], htotal = total;
-        uint64_t sm[NC];
+        // a sharded round routes every successor's fingerprint to its owner, self-loops (the parent itself,
+        // FollowerAcceptEntry changing nothing) too; they are counted for the level statistics only
+        if (MODE == M_FUSED) {
 #pragma unroll
-        for (int r = 0; r < NC; r++) {
-            hrank[r] = rank[r];
-            sm[r] = 0;
-        }
-        if (SKIPSELF && !P.route) {
-#pragma unroll
-            for (int r = 0; r < NC; r++) {
-                sm[r] = __ballot(cand[r].key != KEY_NONE && cand[r].self);
-                htotal -= (uint32_t)__popcll(sm[r]);
-            }
-#pragma unroll
-            for (int q = 0; q < NC; q++) {
-                for (uint64_t m = sm[q]; m; m &= m - 1) {
-                    const uint32_t kt = rdlane(cand[q].key, __ffsll((unsigned long long)m) - 1);
-#pragma unroll
-                    for (int r = 0; r < NC; r++) hrank[r] -= kt < cand[r].key ? 1u : 0u;
-                }
-            }
+            for (int r = 0; r < NC; r++) route_self += (uint32_t)__popcll(__ballot(cand[r].key != KEY_NONE && cand[r].self));
         }
         const uint64_t pl = p - P.p_begin;  // chunk-local parent index
         uint64_t am = 0;
@@ -1601,7 +1570,6 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
         }
         if (MODE != M_SINGLE && lane == 0) {
             P.cnt[pl] = total;
-            if (MODE == M_SPLIT && P.hcnt) P.hcnt[pl] = total;  // (no self-loops set apart here)
             P.pnm[pl] = W.nm;
             if (total == 0 && !am && P.check_deadlock) atomicMin(&P.err[ERR_DEADLOCK], ((unsigned long long)p << 16) << 8);
         }
@@ -1613,35 +1581,10 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
             for (int r = 0; r < NC; r++) {
                 if (cand[r].key == KEY_NONE) continue;
                 const uint64_t q = pl * (uint64_t)MX + rank[r];
-                if (SKIPSELF && ((sm[r] >> lane) & 1u)) {  // a self-loop: decided here, never committed
-                    P.lslot[q] = LS_SEEN;
-                    continue;
-                }
                 stage_succ<N, V, MR>(cand[r], W.nm, P.score + q * (uint64_t)S::SW4);
             }
         }
         PHASE(3);
-        if constexpr (MODE == M_SPLIT) {
-            // the parent's hash context for k_hash_probe: record words 0 .. CCW - 1 are in lanes
-            // 0 .. CCW - 1 (rec0), the message-hash sums in LDS
-            constexpr int CTXW = ctx_words<N, V>(), CC = ((S::CCW + 3) / 4) * 4;
-            uint32_t *cx = P.hctx + pl * (uint64_t)CTXW;
-            for (int k = lane; k < CTXW; k += 64) {
-                uint32_t v = 0u;
-                if (k < CC) {
-                    v = k < S::CCW ? rec0 : 0u;
-                } else {
-                    const int pi = (k - CC) >> 2, part = k & 3;
-                    const int t = pi / (N - 1), jj = pi % (N - 1), j = jj < t ? jj : jj + 1;
-                    const uint64_t m = part < 2 ? M0[t * N + j] : M1[t * N + j];
-                    v = (part & 1) ? (uint32_t)(m >> 32) : (uint32_t)m;
-                }
-                cx[k] = v;
-            }
-            __syncthreads();  // M0 / M1 are cleared for the next parent
-            PHASE(4);
-            continue;
-        }
         // ---- fingerprints (rmc_spec.h): content matrix, signature coset, minimum -----------------
         // (a) the parent's content matrix, a lane per (half, row, column)
         if (lane < 2 * N * N) {
@@ -1649,13 +1592,12 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
             pC[f][t * N + j] = content<N>(f, (uint32_t)t, (uint32_t)j, W.c, pcore[Lo::W_LOG + t], pcore[Lo::W_MI + t],
                                           pcore[Lo::W_NI + t], f ? M1[t * N + j] : M0[t * N + j]);
         }
-        // (b) every enabled successor's row inputs at its TLC rank (self-loops apart: hrank)
+        // (b) every enabled successor's row inputs at its TLC rank
 #pragma unroll
         for (int r = 0; r < NC; r++) {
-            if (cand[r].key == KEY_NONE || ((sm[r] >> lane) & 1u)) continue;
+            if (cand[r].key == KEY_NONE) continue;
             const Succ<N, V, MR> &o = cand[r];
-            const uint32_t g = hrank[r];
-            sRq[g] = (uint16_t)rank[r];
+            const uint32_t g = rank[r];
             const uint32_t vfs = nib(o.c[Lo::W_VF], o.s);
             sUg[g] = own_word<N>(o.c[Lo::W_VF], o.c[Lo::W_CT], o.c[Lo::W_ROLE], o.c[Lo::W_CI], o.c[Lo::W_LL], o.lw,
                                  o.mirow, o.nirow, o.s);
@@ -1677,18 +1619,14 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
         auto emit = [&](uint32_t lo, ulonglong2 best) {
             const ulonglong2 f = make_ulonglong2(best.x | 1ull, best.y);
             if (MODE == M_FUSED) {
-                // the seen set is read-only in this launch (commit inserts)
-                const uint64_t q = pl * (uint64_t)MX + sRq[lo];
-                P.fp[q] = f;
-                if (P.route) return;  // sharded round: the fingerprint's owner probes and elects
-                P.lslot[q] = probe_elect<MX>(P, f, q, ((uint32_t)sNa[lo] + (W.nm & 1u) + 1u) >> 1);
+                P.fp[pl * (uint64_t)MX + lo] = f;  // sharded round: the fingerprint's owner probes and elects
             } else {
                 P.fp[lo] = f;
             }
         };
         // (c) per batch of HB successors (by TLC rank)
-        for (uint32_t b0 = 0; b0 < htotal; b0 += (uint32_t)HB) {
-            const uint32_t nb = htotal - b0 < (uint32_t)HB ? htotal - b0 : (uint32_t)HB;
+        for (uint32_t b0 = 0; b0 < total; b0 += (uint32_t)HB) {
+            const uint32_t nb = total - b0 < (uint32_t)HB ? total - b0 : (uint32_t)HB;
             {  // (c1) the acting row's contents: lane (half, successor) when FH == 2, else both halves
                 const uint32_t l = (uint32_t)lane % HB, g = b0 + l;
                 if (l < nb) {
@@ -1811,6 +1749,7 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
         }
         if (lane == 0) *P.out_count = total;
     }
+    if (MODE == M_FUSED && P.route && lane == 0 && route_self) atomicAdd(&P.sum[SUM_SELF], (unsigned long long)route_self);
     PHASE_FLUSH;
 }
 
@@ -3617,34 +3556,6 @@ __global__ __launch_bounds__(256) void k_local_flags(KParams P, Seen seen, const
     block_count_add(mine, inserted);
 }
 
-// split chunks: the item-parallel expansion (k_expand_items; RMC_SPLIT_ITEMS=0: the wave-per-parent one)
-static bool split_items() {
-    static const bool on = [] {
-        const char *v = std::getenv("RMC_SPLIT_ITEMS");
-        return !(v && v[0] == '0');
-    }();
-    return on;
-}
-
-// fused levels (device loop, chunks below the split size): the item-parallel expansion with the
-// fingerprints and election in the same launch (RMC_FUSED_ITEMS=0: k_expand<M_FUSED>, round 4's)
-static bool fused_items() {
-    static const bool on = [] {
-        const char *v = std::getenv("RMC_FUSED_ITEMS");
-        return !(v && v[0] == '0');
-    }();
-    return on;
-}
-
-// ... and their commit: k_commit_items<FUSE> (RMC_FUSED_COMMIT=0: k_commit, a wave per parent)
-static bool fused_commit() {
-    static const bool on = [] {
-        const char *v = std::getenv("RMC_FUSED_COMMIT");
-        return fused_items() && !(v && v[0] == '0');
-    }();
-    return on;
-}
-
 static inline unsigned grid_for(uint64_t n) {
     const uint64_t cap = 256ull * RMC_GRID_PER_CU;  // one-wave blocks per CU (default 32) on 256 CUs
     return (unsigned)(n < cap ? (n ? n : 1) : cap);
@@ -3658,24 +3569,20 @@ struct Launch {
         hipLaunchKernelGGL((k_expand<N, V, MR, M_SINGLE, BFV>), dim3(1), dim3(64), bm_bytes(P), s, P);
     }
     static void fused(const KParams &P, hipStream_t s) {
-        if (fused_items() && !P.route) {  // a block per 64 parents, fingerprints and election in the same launch
+        if (!P.route) {  // a block per XF_PARENTS parents, fingerprints and election in the same launch
             const uint64_t nbat = (P.p_end - P.p_begin + XF_PARENTS - 1) / XF_PARENTS;
             hipLaunchKernelGGL((k_expand_items<N, V, MR, BFV, true, XF_PARENTS>), dim3((unsigned)(nbat < 8192 ? (nbat ? nbat : 1) : 8192)),
                                dim3(XB_THREADS), 0, s, P);
             return;
         }
+        // a sharded round below the split size: a wave per parent, fingerprints routed to their owners
         hipLaunchKernelGGL((k_expand<N, V, MR, M_FUSED, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64),
                            bm_bytes(P), s, P);
     }
     static void split(const KParams &P, hipStream_t s) {
-        if (split_items()) {
-            const uint64_t nbat = (P.p_end - P.p_begin + XB_PARENTS - 1) / XB_PARENTS;
-            hipLaunchKernelGGL((k_expand_items<N, V, MR, BFV, false, XB_PARENTS>), dim3((unsigned)(nbat < 2048 ? (nbat ? nbat : 1) : 2048)),
-                               dim3(XB_THREADS), 0, s, P);
-            return;
-        }
-        hipLaunchKernelGGL((k_expand<N, V, MR, M_SPLIT, BFV>), dim3(grid_for(P.p_end - P.p_begin)), dim3(64),
-                           bm_bytes(P), s, P);
+        const uint64_t nbat = (P.p_end - P.p_begin + XB_PARENTS - 1) / XB_PARENTS;
+        hipLaunchKernelGGL((k_expand_items<N, V, MR, BFV, false, XB_PARENTS>), dim3((unsigned)(nbat < 2048 ? (nbat ? nbat : 1) : 2048)),
+                           dim3(XB_THREADS), 0, s, P);
     }
     static void hash_probe(const KParams &P, uint64_t np, hipStream_t s) {
         const uint64_t blocks = (np + 255) / 256;  // four one-group waves per block
@@ -3693,7 +3600,7 @@ struct Launch {
     }
     static void commit(const KParams &P, hipStream_t s) {
         if constexpr (MX <= XB_THREADS) {
-            if (fused_commit() && !P.route && !P.split && !P.plist) {  // a block per 16 parents, records in LDS
+            if (!P.route && !P.split && !P.plist) {  // a block per 16 parents, records in LDS
                 const uint64_t nbat = (P.p_end - P.p_begin + XC_PARENTS - 1) / XC_PARENTS;
                 hipLaunchKernelGGL((k_commit_items<N, V, MR, MX, true, XC_PARENTS>),
                                    dim3((unsigned)(nbat < 8192 ? (nbat ? nbat : 1) : 8192)), dim3(XB_THREADS), 0, s, P);

@@ -342,8 +342,8 @@ int run_ranks(int N, bool onerank, const rmc_config &base, const std::function<i
 // kernel's teardown of the worker (~110 GB of host trace and the device memory after a Raft.cfg
 // exhaustion: ~4 s) then runs after this process has returned TLC's exit code,
 // so the shell returns as the "Finished" line prints.
-// The worker then frees the device memory itself (hipFree: milliseconds) before
-// the host trace, so a GPU job started right after the shell returns finds the device free.
+// The worker frees the device memory itself (rmc_release_device) before it reports, so a GPU job started
+// right after the shell returns finds the device free; only the host trace's teardown overlaps it.
 int g_report_fd = -1;
 
 void report(int code) {  // (a no-op in the one-process mode)
@@ -634,9 +634,11 @@ int main(int argc, char **argv) {
     std::fflush(stderr);
     const char *fe = std::getenv("RMC_FAST_EXIT");
     if (!(fe && std::string(fe) == "0")) {
-        if (g_report_fd >= 0) {  // detached worker: the caller has its code; device memory goes first
+        if (g_report_fd >= 0) {  // detached worker: the device goes back before the caller has its code
+            phase_time("release device");
+            rmc_release_device(ctx);
+            phase_time("device released");
             report(exit_code);
-            rmc_destroy(ctx);
         }
         std::_Exit(exit_code);
     }

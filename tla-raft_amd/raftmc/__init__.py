@@ -36,6 +36,9 @@ ACTIONS = ("BecomeCandidate", "UpdateTerm", "ResponseVote", "BecomeLeader", "Cli
            "FollowerAppendEntry", "BecomeFollower")  # 11: never enabled (tla:425 variant); 12: tla:420 variant
 SPEC_RAFT, SPEC_SEEDED, SPEC_BECOME_FOLLOWER = 0, 1, 2
 SPEC_SPLIT_BRAIN, SPEC_COMMIT_PAST_LOG = 3, 4  # test variants: Assert / evaluation error reachable in a BFS
+# include/rmc.h RMC_ABI_VERSION: the struct layouts below (_Config, _LevelStats, _Result) follow this ABI; a
+# library of another ABI would be decoded with the wrong strides, so load_library refuses it
+ABI_VERSION = 5
 
 
 class RmcError(RuntimeError):
@@ -102,6 +105,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     vp, i32, u32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
     P = ctypes.POINTER
     lib.rmc_abi_version.restype = ctypes.c_int
+    abi = lib.rmc_abi_version()
+    if abi != ABI_VERSION:
+        raise RmcError(f"{path} has ABI {abi}, this binding decodes ABI {ABI_VERSION}: rebuild it "
+                       f"(make -C tla-raft_amd)")
     lib.rmc_parse_config.argtypes = [ctypes.c_char_p, ctypes.c_char_p, P(_Config), ctypes.c_char_p, ctypes.c_size_t]
     lib.rmc_create.argtypes = [P(_Config), P(vp)]
     lib.rmc_init.argtypes = [vp, P(_LevelStats)]

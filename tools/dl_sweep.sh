@@ -12,7 +12,7 @@ for v in "$@"; do
   D=${D:-build}
   echo "== G=$G A=$A Q=$Q lib=$D ($(date +%T))"
   RMC_LIBRARY="$R/tla-raft_amd/$D/librmc.so" RMC_DL_GROUP=$G RMC_DL_AHEAD=$A RMC_DL_QUERY_US=$Q timeout -k 10 120 python -u bench.py --steps 40 --warmup 5 \
-    --no-cpu-baseline --no-probe-peak --no-scale > "gpurun_out/dl_sweep/$G-$A-$Q-$D.json" 2> "gpurun_out/dl_sweep/$G-$A-$Q-$D.err" \
+    --no-cpu-baseline --no-probe-peak --workload c2 > "gpurun_out/dl_sweep/$G-$A-$Q-$D.json" 2> "gpurun_out/dl_sweep/$G-$A-$Q-$D.err" \
     || { tail -5 "gpurun_out/dl_sweep/$G-$A-$Q-$D.err"; exit 1; }
   python -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['ms_per_step'], d['value'])" "gpurun_out/dl_sweep/$G-$A-$Q-$D.json"
 done

@@ -24,7 +24,7 @@ for v in "$@"; do
   grep RESULT gpurun_out/ab/$name.log
   if [ -n "$BENCHC2" ]; then  # the headline line (configs[1]) with the same variant
     ( IFS=','; for e in $envs; do [ -n "$e" ] && export "$e"; done; unset IFS
-      exec timeout -k 10 120 python -u bench.py --no-scale --no-cpu-baseline --no-probe-peak ) > gpurun_out/ab/$name.bench.json 2> gpurun_out/ab/$name.bench.err || { tail -5 gpurun_out/ab/$name.bench.err; exit 1; }
+      exec timeout -k 10 120 python -u bench.py --workload c2 --no-cpu-baseline --no-probe-peak ) > gpurun_out/ab/$name.bench.json 2> gpurun_out/ab/$name.bench.err || { tail -5 gpurun_out/ab/$name.bench.err; exit 1; }
     python -c "import json,sys; d=json.load(open(sys.argv[1])); print('bench', d['value'], d['ms_per_step'])" gpurun_out/ab/$name.bench.json
   fi
 done

@@ -8,6 +8,6 @@ mkdir -p gpurun_out/c2ab
 for v in "$@"; do
   name=${v%%=*}; envs=${v#*=}
   ( IFS=','; for e in $envs; do [ -n "$e" ] && export "$e"; done; unset IFS
-    exec timeout -k 10 120 python -u bench.py --no-scale --no-cpu-baseline --no-probe-peak ) > gpurun_out/c2ab/$name.json 2> gpurun_out/c2ab/$name.err || { tail -5 gpurun_out/c2ab/$name.err; exit 1; }
+    exec timeout -k 10 120 python -u bench.py --workload c2 --no-cpu-baseline --no-probe-peak ) > gpurun_out/c2ab/$name.json 2> gpurun_out/c2ab/$name.err || { tail -5 gpurun_out/c2ab/$name.err; exit 1; }
   python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['value'], d['ms_per_step'])" gpurun_out/c2ab/$name.json "$name [$envs]"
 done
