@@ -3220,8 +3220,20 @@ struct rmc_ctx {
             throw Fail(RMC_E_ARG, std::string("checkpoint: cannot rename to ") + path);
     }
 
+    // A resume that fails part way (a corrupt data section, a short file, an allocation) may have loaded
+    // part of the checkpoint into the seen set and rings: the context is reset, so it starts from Init
+    // (or takes another resume) as if the failed call had not been made.
     void resume(const char *path_arg) {
         if (inited) throw Fail(RMC_E_STATE, "resume: needs a context not yet initialised (rmc_create or rmc_reset)");
+        try {
+            resume_body(path_arg);
+        } catch (...) {
+            reset();
+            throw;
+        }
+    }
+
+    void resume_body(const char *path_arg) {
         HIPCHK(hipStreamSynchronize(stream));  // rmc_reset's clears are stream-ordered, the loads below are not
         const std::string path = ckpt_path(path_arg);
         FILE *f = std::fopen(path.c_str(), "rb");

@@ -81,6 +81,8 @@ constexpr int SUM_WORDS = 7;     // chunk summary slot of the new states' record
 constexpr int SUM_NZ = 16;       // ... and of the parents with winners (KParams::plist)
 constexpr int SUM_SELF = 17;     // ... and the self-loops set apart (KParams::hcnt, or a host-driven fused chunk's;
                                  // zeroed by the host per chunk)
+constexpr int SUM_HFP = 18;      // ... and a split chunk's successors to fingerprint (its expansion counts them; the
+                                 // election of k_hash_probe takes a table of twice as many slots; zeroed with SUM_SELF)
 // the fused expansion's self-loop counters: SELF_STRIPES words a 128-B line apart (block b adds to stripe
 // b % SELF_STRIPES), folded by finish_level (k_set_ctl zeroes them for the device loop; 0 between levels)
 constexpr int SUM_SELF_STRIPE = 32, SELF_STRIDE = 16, SELF_STRIPES = 8;  // sum[32 .. 144]

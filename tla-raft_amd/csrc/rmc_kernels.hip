@@ -1412,11 +1412,12 @@ __device__ __forceinline__ ulonglong2 staged_fp(const KParams &P, const uint32_t
 // The fused election of a new fingerprint (the seen set is read-only in the launch): its slot q's
 // verdict LS_SEEN, or the election slot it bid in.  e: the record words a winner adds (elect_key)
 template <int MX>
-__device__ __forceinline__ uint32_t probe_elect(const KParams &P, const ulonglong2 f, uint64_t q, uint32_t e) {
+__device__ __forceinline__ uint32_t probe_elect(const KParams &P, const ulonglong2 f, uint64_t q, uint32_t e,
+                                                uint64_t Lmask) {
     // the election slot's first word goes out with the seen-set probe: one round trip fewer
-    const uint64_t g = l_index(f, P.Lmask);
+    const uint64_t g = l_index(f, Lmask);
     const unsigned long long v0 = __hip_atomic_load(&P.ET[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return seen_contains(P.seen, f) ? LS_SEEN : elect_slot<MX>(P.ET, P.wacc, P.Lmask, P.epoch, f, q, e, g, v0);
+    return seen_contains(P.seen, f) ? LS_SEEN : elect_slot<MX>(P.ET, P.wacc, Lmask, P.epoch, f, q, e, g, v0);
 }
 
 template <int N, int MR, int MODE, bool BFV>
@@ -2148,8 +2149,12 @@ __global__ __launch_bounds__(XB_THREADS, FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) :
     uint16_t *sKey = sQ + IC_N * NT;                    // [NT * NCI] the round's enabled keys, per parent at its items' offset
     __shared__ uint32_t sSpan;
     __shared__ uint32_t sSelfN;                    // fused level: the block's self-loops (finish_level adds them up)
+    __shared__ uint32_t sHfp;                      // split chunk: the block's successors to fingerprint (SUM_HFP)
     const int tid = threadIdx.x;
-    if (tid == 0) sSelfN = 0u;
+    if (tid == 0) {
+        sSelfN = 0u;
+        sHfp = 0u;
+    }
     if constexpr (FUSE) {
         // device loop: the level from the control block, the levels committed so far to the host as
         // this one starts (as k_expand<M_FUSED>); grids are sized on a bound of the level
@@ -2377,7 +2382,7 @@ __global__ __launch_bounds__(XB_THREADS, FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) :
                             [&](int a, uint32_t) { return x.ainf[a]; }, st4[0], st4[1],
                             S::SW4 > 2 ? st4[S::SW4 > 2 ? 2 : 0] : make_uint4(0u, 0u, 0u, 0u), sK);
                         P.fp[q] = f;
-                        P.lslot[q] = probe_elect<MX>(P, f, q, (x.nadd + (nmj & 1u) + 1u) >> 1);
+                        P.lslot[q] = probe_elect<MX>(P, f, q, (x.nadd + (nmj & 1u) + 1u) >> 1, P.Lmask);
                     } else {
                         row_stage<S::NADD>(x, nmj, S::SW4, P.score + q * (uint64_t)S::SW4);
                     }
@@ -2391,6 +2396,7 @@ __global__ __launch_bounds__(XB_THREADS, FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) :
                 const uint32_t total = sCnt[jj] + sSelf[jj], ak = sAk[jj];
                 P.cnt[pl] = total;
                 if (P.hcnt) P.hcnt[pl] = sCnt[jj];
+                if (!FUSE && sCnt[jj]) atomicAdd(&sHfp, sCnt[jj]);
                 P.pnm[pl] = (sCore[jj * NWP + Lo::W_MISC] >> 16) & 0xFFu;
                 if (ak != KEY_NONE) atomicMin(&P.err[ERR_ASSERT], (((unsigned long long)p << 16) | ak) << 8);
                 else if (total == 0 && P.check_deadlock)
@@ -2402,10 +2408,12 @@ __global__ __launch_bounds__(XB_THREADS, FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) :
             a = b;
         }
     }
+    __syncthreads();
     if constexpr (FUSE) {
-        __syncthreads();
         if (tid == 0 && sSelfN)
             atomicAdd(&P.sum[SUM_SELF_STRIPE + SELF_STRIDE * (blockIdx.x % SELF_STRIPES)], (unsigned long long)sSelfN);
+    } else {
+        if (tid == 0 && sHfp) atomicAdd(&P.sum[SUM_HFP], (unsigned long long)sHfp);
     }
     PHASE_FLUSH;
 }
@@ -2512,6 +2520,16 @@ __global__ __launch_bounds__(256) void k_hash_probe(KParams P) {
         sK[f][a * N + b] = P.t.seeds[f * SEEDS_PER_F + a * MAXN + b];
     }
     if (threadIdx.x < 64) sOwn[threadIdx.x] = 0u;
+    // The election table of the chunk: twice its successors to fingerprint (counted by the expansion), not
+    // the host's bound of MAXS per parent -- ~35x fewer slots at Raft.cfg's depth, so the elections' random
+    // lines stay in the caches far more often (every slot of the table is free for this chunk's tag, so any
+    // prefix of it serves)
+    uint64_t Lmask = P.Lmask;
+    if (!P.route) {
+        const unsigned long long nf = __hip_atomic_load(&P.sum[SUM_HFP], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t want = nf < 512ull ? 1024ull : 1ull << (64 - __clzll((long long)(2 * nf - 1)));
+        Lmask = want - 1 < Lmask ? want - 1 : Lmask;
+    }
     __syncthreads();
     each_successor<MX>(P, [&](uint64_t pl, uint32_t r) {
         const uint64_t q = pl * (uint64_t)MX + r;
@@ -2549,7 +2567,7 @@ __global__ __launch_bounds__(256) void k_hash_probe(KParams P) {
             return;
         }
         const uint32_t nm = (pc[Lo::W_MISC] >> 16) & 0xFFu;
-        P.lslot[q] = probe_elect<MX>(P, f, q, (nadd + (nm & 1u) + 1u) >> 1);
+        P.lslot[q] = probe_elect<MX>(P, f, q, (nadd + (nm & 1u) + 1u) >> 1, Lmask);
     });
     if (P.route && P.ocnt) {
         __syncthreads();
