@@ -853,8 +853,8 @@ struct rmc_ctx {
         HIPCHK(hipMemcpy(d_seeds, seeds.data(), seeds.size() * 8, hipMemcpyHostToDevice));
         // fingerprint scheme identity (checkpoints): seeds, message hashes, record codec, slot hash
         // (4: signature-coset minimum for n >= 4; 5: positional slot keys; 6: codec of (N, V); 7: content
-        // matrix x position constants, signature coset for every n)
-        scheme_hash = 0x5eed5c4e3e000007ull;
+        // matrix x position constants, signature coset for every n; 8: the compact seen set in 64-B buckets)
+        scheme_hash = 0x5eed5c4e3e000008ull;
         auto mixin = [&](uint64_t v) { scheme_hash = mix64(scheme_hash ^ (v + 0x9e3779b97f4a7c15ull)); };
         for (uint64_t s : seeds) mixin(s);
         for (const ulonglong2 &g : U.gmsg) { mixin(g.x); mixin(g.y); }
@@ -3313,7 +3313,7 @@ struct rmc_ctx {
             uint64_t chk = 0;
             ok = std::fread(&c, sizeof c, 1, f) == 1 && std::fread(&chk, 8, 1, f) == 1;
             if (!ok || chk != fnv(c, sizeof c) || c.id != s.id || c.n_levels == 0 || c.n_levels > 100000 ||
-                (!c.compact && (c.T_cap & (c.T_cap - 1)) != 0) || c.T_cap == 0 || c.T_count >= c.T_cap ||
+                (!c.compact && (c.T_cap & (c.T_cap - 1)) != 0) || (c.compact && c.T_cap % 8) || c.T_cap == 0 || c.T_count >= c.T_cap ||
                 c.T_count > h.total_distinct || (!multi && c.T_count > c.trace_n) || c.cur_words > c.cur_n * (uint64_t)RECW || c.cur_words < c.cur_n * (uint64_t)ks.CCW)
                 fail(" has an inconsistent shard header");
             std::vector<uint64_t> &ls = lss[i];

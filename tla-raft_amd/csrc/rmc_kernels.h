@@ -29,10 +29,10 @@ struct ESlot {
 
 // Seen set (TLC's FPSet): open addressing over 128-bit fingerprints {x | 1, y}.
 //   full:    16-B slots {x, y} (T != nullptr), grown x4 by rehash while small;
-//   compact:  8-B slots holding x only (Tc != nullptr): the slot's probe run, which starts at the
-//             home index derived from y, carries the rest of the identity.  Used once the run is
-//             large (rmc_config.compact_log2); sized once from the memory budget (any slot count:
-//             the home slot is the high half of hash * cap), never grown.
+//   compact:  8-B slots holding x only (Tc != nullptr), eight to a 64-B bucket: the bucket probe run,
+//             which starts at the home bucket derived from y, carries the rest of the identity.  Used
+//             once the run is large (rmc_config.compact_log2); sized once from the memory budget (any
+//             multiple of 64 slots: the home bucket is the high half of hash * buckets), never grown.
 struct Seen {
     ulonglong2 *T;
     unsigned long long *Tc;

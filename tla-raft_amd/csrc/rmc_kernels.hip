@@ -1175,23 +1175,44 @@ __device__ __forceinline__ uint64_t t_index(const ulonglong2 f, uint64_t mask) {
     return (f.y ^ (f.y >> 29) ^ (f.x >> 23)) & mask;
 }
 
-// Home slot of the compact table: multiply-shift of a remixed word (any cap).  The remix matters:
-// y is a minimum over Permutations(Servers), so its high bits are far from uniform (the smallest of
-// 6 -- or 120 -- hashes), and multiply-shift reads the high bits.
-__device__ __forceinline__ uint64_t t_home_c(const ulonglong2 f, uint64_t cap) {
+// The compact table is bucketed: TB = 8 slots of 8 B per 64-B bucket, a fingerprint x in the first bucket
+// from its home (linear over buckets) that had a free slot when it was inserted -- a probe reads one
+// bucket in one round trip (four 16-B loads issued together) where single-slot linear probing took a
+// dependent load per slot of the run.  Slots are only ever filled, so a bucket with a free slot ends a
+// probe: a fingerprint inserted earlier would have found that slot (or one before it) free.
+constexpr uint64_t TB = 8;
+// Home bucket: multiply-shift of a remixed word (any bucket count).  The remix matters: y is a minimum
+// over Permutations(Servers), so its high bits are far from uniform (the smallest of 6 -- or 120 --
+// hashes), and multiply-shift reads the high bits.
+__device__ __forceinline__ uint64_t t_home_c(const ulonglong2 f, uint64_t nbk) {
     uint64_t z = (f.y ^ (f.x >> 17)) * 0x9e3779b97f4a7c15ull;
     z ^= z >> 29;
-    return __umul64hi(z, cap);
+    return __umul64hi(z, nbk);
+}
+
+// the eight slots of bucket b, loaded together
+__device__ __forceinline__ void bucket_load(const unsigned long long *Tc, uint64_t b, unsigned long long e[TB]) {
+    const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(Tc + b * TB);
+    const ulonglong2 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+    e[0] = a0.x; e[1] = a0.y; e[2] = a1.x; e[3] = a1.y; e[4] = a2.x; e[5] = a2.y; e[6] = a3.x; e[7] = a3.y;
 }
 
 __device__ __forceinline__ bool seen_contains(const Seen &S, ulonglong2 f) {
     if (S.Tc) {
-        uint64_t h = t_home_c(f, S.cap);
+        const uint64_t nbk = S.cap / TB;
+        uint64_t b = t_home_c(f, nbk);
         for (;;) {
-            const unsigned long long e = S.Tc[h];
-            if (e == 0ull) return false;
-            if (e == f.x) return true;
-            h = (h + 1 == S.cap) ? 0 : h + 1;
+            unsigned long long e[TB];
+            bucket_load(S.Tc, b, e);
+            bool hit = false, free_ = false;
+#pragma unroll
+            for (uint64_t k = 0; k < TB; k++) {
+                hit |= e[k] == f.x;
+                free_ |= e[k] == 0ull;
+            }
+            if (hit) return true;
+            if (free_) return false;
+            b = (b + 1 == nbk) ? 0 : b + 1;
         }
     }
     uint64_t h = t_index(f, S.mask);
@@ -1209,10 +1230,15 @@ __device__ __forceinline__ bool seen_contains(const Seen &S, ulonglong2 f) {
 // keys inserted are never already present (winners are new, rehash moves distinct keys)
 __device__ __forceinline__ void seen_insert(const Seen &S, ulonglong2 f) {
     if (S.Tc) {
-        uint64_t h = t_home_c(f, S.cap);
+        const uint64_t nbk = S.cap / TB;
+        uint64_t b = t_home_c(f, nbk);
         for (;;) {
-            if (atomicCAS(&S.Tc[h], 0ull, (unsigned long long)f.x) == 0ull) return;
-            h = (h + 1 == S.cap) ? 0 : h + 1;
+            unsigned long long e[TB];
+            bucket_load(S.Tc, b, e);
+            // the bucket's free slots in order; a slot another insert took first fails its CAS
+            for (uint64_t k = 0; k < TB; k++)
+                if (e[k] == 0ull && atomicCAS(&S.Tc[b * TB + k], 0ull, (unsigned long long)f.x) == 0ull) return;
+            b = (b + 1 == nbk) ? 0 : b + 1;
         }
     }
     uint64_t h = t_index(f, S.mask);
@@ -1795,6 +1821,13 @@ constexpr int XC_PARENTS = RMC_FUSED_CPB;
                            // n >= 4 would spill)
 #endif
 constexpr int XB_THREADS = 256;  // threads per block = items per evaluation round at most
+#ifndef RMC_ITEMS_NT  // ... of the split expansion where a parent's items fit that many (else 256)
+#define RMC_ITEMS_NT 256
+#endif
+template <int N, int V, int MR, bool FUSE>
+constexpr int items_threads() {
+    return (!FUSE && Spec<N, V, MR>::MCAP + N * Spec<N, V, MR>::SLOTS_PER_SERVER <= RMC_ITEMS_NT) ? RMC_ITEMS_NT : XB_THREADS;
+}
 
 // votedFor, currentTerm, role, commitIndex, Len(logs) of server s and s itself: staging word 0
 __device__ __forceinline__ uint32_t row_w0(uint32_t vf, uint32_t ct, uint32_t role, uint32_t ci, uint32_t ll,
@@ -2114,10 +2147,10 @@ __device__ __forceinline__ uint32_t slot_class(uint32_t t) {
 }
 
 template <int N, int V, int MR, bool BFV, bool FUSE, int PB>
-__global__ __launch_bounds__(XB_THREADS, FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) : RMC_ITEMS_WAVES) void k_expand_items(KParams P) {
+__global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) : RMC_ITEMS_WAVES) void k_expand_items(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
-    constexpr int NT = XB_THREADS;
+    constexpr int NT = items_threads<N, V, MR, FUSE>();
     static_assert(PB >= 2 && PB <= 64 && (PB & (PB - 1)) == 0, "parents per batch: a power of two, a lane of wave 0 each");
     constexpr int CCW = S::CCW, RECW = S::RECW_MAX, NW = Lo::NW, NWP = (NW + 3) / 4 * 4;
     constexpr int MX = S::MAXS + (BFV ? S::MCAP : 0);
@@ -2315,6 +2348,7 @@ __global__ __launch_bounds__(XB_THREADS, FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) :
                 }
             }
             __syncthreads();
+            PHASE(7);
             RowSucc<S::NADD> o, ob;
             o.key = KEY_NONE;
             ob.key = KEY_NONE;
@@ -2508,8 +2542,11 @@ __device__ __forceinline__ uint32_t owner_bid(ESlot *OT, uint64_t mask, uint32_t
 // and elected with the fused pass's protocol (elect_slot) -- 64 independent chains per wave instead
 // of the ~5 of one parent, and the hash at full lane occupancy.  A sharded round (P.route) only
 // needs the fingerprints: its owners probe and elect.
+#ifndef RMC_PROBE_WAVES  // waves per SIMD the probe pass's registers are cut for (0: the compiler's choice)
+#define RMC_PROBE_WAVES 0
+#endif
 template <int N, int V, int MR, int MX>
-__global__ __launch_bounds__(256) void k_hash_probe(KParams P) {
+__global__ __launch_bounds__(256, RMC_PROBE_WAVES) void k_hash_probe(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
     constexpr int CTXW = ctx_words<N, V>(), CC4 = (S::CCW + 3) / 4;
@@ -3600,7 +3637,7 @@ struct Launch {
     static void split(const KParams &P, hipStream_t s) {
         const uint64_t nbat = (P.p_end - P.p_begin + XB_PARENTS - 1) / XB_PARENTS;
         hipLaunchKernelGGL((k_expand_items<N, V, MR, BFV, false, XB_PARENTS>), dim3((unsigned)(nbat < 2048 ? (nbat ? nbat : 1) : 2048)),
-                           dim3(XB_THREADS), 0, s, P);
+                           dim3(items_threads<N, V, MR, false>()), 0, s, P);
     }
     static void hash_probe(const KParams &P, uint64_t np, hipStream_t s) {
         const uint64_t blocks = (np + 255) / 256;  // four one-group waves per block

@@ -40,8 +40,8 @@ a = ap.parse_args()
 if a.items:
     NAMES[:8] = ["items: record offsets + copy into LDS", "items: decode cores, message scan",
                  "items: message pass (hash sums, votes, classes)", "items: hash context write, item scan",
-                 "items: class lists + evaluate (action, key list)", "items: ranks + staging",
-                 "items: per-parent counts, error keys, round sync", "-"]
+                 "items: evaluate (action, key list)", "items: ranks + staging",
+                 "items: per-parent counts, error keys, round sync", "items: class lists (+ round start)"]
 cfg = raftmc.ModelConfig(n_servers=a.n, n_vals=a.V, max_election=a.E, max_restart=a.R, device_levels=a.device_levels)
 mc = raftmc.ModelChecker(cfg)
 lib = raftmc.load_library()
