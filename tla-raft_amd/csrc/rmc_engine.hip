@@ -405,6 +405,8 @@ struct Shard {
     uint32_t *cnt = nullptr, *lslot = nullptr, *wpos = nullptr;
     uint32_t *hcnt = nullptr;   // split chunks: successors per parent to fingerprint (KParams::hcnt)
     bool chunk_sep = false;     // the chunk being processed set self-loops apart (hcnt valid)
+    bool chunk_dense = false;   // ... and laid its successor slots out densely (hoff valid)
+    uint32_t *hoff = nullptr;   // split chunk: each parent's first successor slot (KParams::hoff)
     ulonglong2 *fp = nullptr;
     ESlot *E = nullptr;         // election table: tagged fingerprint + election word per slot (32 B)
     uint32_t epoch = 0;
@@ -432,6 +434,8 @@ struct Shard {
     ESlot *OT = nullptr;
     uint64_t ot_cap = 0;
     uint32_t ot_round = 0;  // rounds on the owner table since it was last cleared (its tag, k_owner_elect)
+    ESlot *rt_table = nullptr;  // the table the round's bids went to (E or OT) and its round: a split round's
+    uint32_t rt_round = 0;      // commit decides the shard's own candidates there
     // split rounds: the fused election table (E, unused once the run is sharded) is the owner
     // table, so k_hash_probe bids the shard's own successors as it fingerprints them; rounds on it
     // since its last clear (0: not yet cleared for this use), and whether this round's own bids went in
@@ -967,6 +971,7 @@ struct rmc_ctx {
         s.wacc = dmalloc<uint32_t>(chunk_parents + 1);
         s.pnm = dmalloc<uint32_t>(chunk_parents + 1);
         s.hcnt = dmalloc<uint32_t>(chunk_parents + 1);
+        s.hoff = dmalloc<uint32_t>(chunk_parents + 1);
         s.wposw = dmalloc<uint32_t>(chunk_parents + 1);
         s.ctick = dmalloc<uint32_t>(33 * 32);
         HIPCHK(hipMemsetAsync(s.ctick, 0, 33 * 32 * 4, stream));
@@ -990,7 +995,6 @@ struct rmc_ctx {
         if (multi) {
             s.perm = dmalloc<uint32_t>(Gcap);
             s.sflag = dmalloc<uint32_t>(Gcap);
-            s.ocnt = dmalloc<uint32_t>(64);
         }
         ensure_tmp(s, Gcap + 1);
         s.T_cap = 1ull << (cfg.seen_log2 ? cfg.seen_log2 : 22);
@@ -1000,9 +1004,10 @@ struct rmc_ctx {
         s.flags = dmalloc<uint32_t>(4);
         HIPCHK(hipMemsetAsync(s.err, 0xFF, ERR_NSLOTS * 8, stream));
         HIPCHK(hipMemsetAsync(s.flags, 0, 16, stream));
-        s.sum = dmalloc<unsigned long long>(160);
-        HIPCHK(hipMemsetAsync(s.sum, 0, 160 * 8, stream));  // (the self-loop stripes are 0 between launches)
-        HIPCHK(hipHostMalloc((void **)&s.hsum, 160 * 8, hipHostMallocDefault));
+        s.sum = dmalloc<unsigned long long>(SUM_WORDS_TOTAL);
+        HIPCHK(hipMemsetAsync(s.sum, 0, SUM_WORDS_TOTAL * 8, stream));  // (the self-loop stripes are 0 between launches)
+        s.ocnt = reinterpret_cast<uint32_t *>(s.sum + SUM_OCNT);
+        HIPCHK(hipHostMalloc((void **)&s.hsum, SUM_WORDS_TOTAL * 8, hipHostMallocDefault));
         s.rcap = 1ull << 14;
         s.R = dmalloc<uint32_t>(s.rcap);
         s.cur_off_cap = s.nxt_off_cap = 1 << 16;
@@ -1017,11 +1022,12 @@ struct rmc_ctx {
         dfree(s.R); dfree(s.cur_off); dfree(s.nxt_off); dfree(s.T); dfree(s.Tc); dfree(s.par); dfree(s.pslot);
         dfree(s.cnt);
         dfree(s.lslot); dfree(s.wpos); dfree(s.fp); dfree(s.E); dfree(s.tmp);
-        dfree(s.xs); dfree(s.xr); dfree(s.perm); dfree(s.sflag); dfree(s.rslot); dfree(s.rflag); dfree(s.ocnt);
+        dfree(s.xs); dfree(s.xr); dfree(s.perm); dfree(s.sflag); dfree(s.rslot); dfree(s.rflag);
+        s.ocnt = nullptr;  // (inside sum)
         dfree(s.OT); dfree(s.ob); dfree(s.ib); dfree(s.oside); dfree(s.iside); dfree(s.ooff);
         dfree(s.isz); dfree(s.ioff);
         dfree(s.err); dfree(s.sum); dfree(s.flags);
-        dfree(s.score); dfree(s.wcnt); dfree(s.wacc); dfree(s.pnm); dfree(s.hcnt); dfree(s.wposw); dfree(s.ctick);
+        dfree(s.score); dfree(s.wcnt); dfree(s.wacc); dfree(s.pnm); dfree(s.hcnt); dfree(s.hoff); dfree(s.wposw); dfree(s.ctick);
         dfree(s.bw); dfree(s.bg); dfree(s.boff); dfree(s.bww); dfree(s.boffw); dfree(s.tickets);
         dfree(s.bn); dfree(s.boffn); dfree(s.plist); dfree(s.hctx);
         dfree(s.ctl); dfree(s.lrec);
@@ -1948,7 +1954,11 @@ struct rmc_ctx {
                 Q.plist = split ? s.plist : nullptr;
                 // (a split chunk's self-loops are staged after the successors to fingerprint)
                 Q.hcnt = split ? s.hcnt : nullptr;
+                // (the dense slot layout: chunks whose winners the items commit takes -- k_insert_winners and
+                // k_commit_split read the sparse one)
+                Q.hoff = fold ? s.hoff : nullptr;
                 s.chunk_sep = Q.hcnt != nullptr;
+                s.chunk_dense = Q.hoff != nullptr;
                 return Q;
             };
             // expand + fingerprint + seen-set probe + staging, one evaluation per parent (a split
@@ -2261,7 +2271,8 @@ struct rmc_ctx {
             unsigned long long best;
             const int kind = first_error(s.hsum + 2, &best);
             if (kind < 0) throw Fail(RMC_E_STATE, "device level loop stopped without an error");
-            s.chunk_sep = false;  // (device-loop levels stage every successor)
+            s.chunk_sep = false;  // (device-loop levels stage every successor, sparse)
+            s.chunk_dense = false;
             stop_on_error(kind, best, 0, 0, gid_cur, gid_cur + s.cur_n, 0, st);
         }
         HIPCHK(hipStreamSynchronize(stream));
@@ -2293,9 +2304,9 @@ struct rmc_ctx {
             if (!nslots) return 0;
             std::vector<uint32_t> ls(nslots);
             std::vector<uint4> st((size_t)nslots * sw4());
-            HIPCHK(hipMemcpy(ls.data(), s.lslot + pl * ks.maxsucc, nslots * 4, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(st.data(), s.score + pl * ks.maxsucc * sw4(), (size_t)nslots * sw4() * 16,
-                             hipMemcpyDeviceToHost));
+            const uint64_t q0 = s.chunk_dense ? (uint64_t)d2h(s.hoff + pl) : pl * ks.maxsucc;  // its first slot
+            HIPCHK(hipMemcpy(ls.data(), s.lslot + q0, nslots * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(st.data(), s.score + q0 * sw4(), (size_t)nslots * sw4() * 16, hipMemcpyDeviceToHost));
             uint64_t w = 0;
             for (uint32_t r = 0; r < nslots; r++) {
                 if ((st[(size_t)r * sw4() + 1].z & 0xFFFFu) >= bound) continue;
@@ -2382,6 +2393,7 @@ struct rmc_ctx {
         Q.next_base = 0;
         Q.xside = s.oside;
         Q.gid_next_base = 0;
+        Q.gblk = s.gblk;
         // a round of many parents: the commit visits only those with winners (k_nzlist, as a split
         // chunk of the single-GPU path; same switches), and its self-loops are set apart -- known seen
         // (the parent's fingerprint is in its owner's seen set), they are neither fingerprinted nor routed
@@ -2506,9 +2518,8 @@ struct rmc_ctx {
                 s.p0 = c * B;
                 s.np = s.cur_n > s.p0 ? std::min<uint64_t>(B, s.cur_n - s.p0) : 0;
                 s.gblk = (c * (uint64_t)W + (uint64_t)s.id) * B;
-                HIPCHK(hipMemsetAsync(s.ocnt, 0, 64 * 4, stream));
-                HIPCHK(hipMemsetAsync(s.sum + 9, 0, 8, stream));
-                HIPCHK(hipMemsetAsync(s.sum + SUM_SELF, 0, 8, stream));
+                // inserted counts, self-loops, successors per owner: one memset (sum[SUM_INS .. SUM_OCNT + 32))
+                HIPCHK(hipMemsetAsync(s.sum + SUM_INS, 0, (SUM_OCNT + 32 - SUM_INS) * 8, stream));
                 // (before any skip: a shard with no parents this round receives items, and they must
                 // not bid in E under an earlier round's tag)
                 s.lx_bid = false;
@@ -2625,19 +2636,26 @@ struct rmc_ctx {
                         OT = o.OT;
                         rnd = o.ot_round;
                     }
+                    // every bid counts the owner's own winners on their parents (owner_bid); a split round's commit
+                    // then decides the own candidates itself (no k_local_flags pass)
                     timed(PH_DEDUP, [&] {
                         const KParams Q = round_params(o, gbase);
-                        if (Rl && !lx)
+                        if (Rl && !lx) {
+                            // (bids the fingerprint pass made in E are void: they count again in the owner table)
+                            if (o.lx_bid) HIPCHK(hipMemsetAsync(o.wacc, 0, o.np * 4, stream));
                             ks.local_elect(Q, o.np, o.seen(), OT, mask, rnd, (uint32_t)W, (uint32_t)o.id, o.gblk,
                                            stream);
-                        if (R) {
-                            launch_owner_elect(o.xr, R, o.seen(), OT, mask, rnd, o.rslot, stream);
-                            launch_owner_flags(o.xr, R, o.rslot, OT, rnd, o.seen(), o.rflag, o.sum + 9, stream);
                         }
-                        if (Rl)
+                        if (R) {
+                            launch_owner_elect(o.xr, R, o.seen(), OT, mask, rnd, o.rslot, o.wacc, o.gblk, o.np, stream);
+                            launch_owner_flags(o.xr, R, o.rslot, OT, rnd, o.seen(), o.rflag, o.sum + SUM_INS, stream);
+                        }
+                        if (Rl && !round_sep(o))
                             ks.local_flags(Q, o.np, o.seen(), OT, rnd, (uint32_t)W, (uint32_t)o.id, o.gblk,
-                                           o.sum + 9, stream);
+                                           o.sum + SUM_INS, stream);
                     });
+                    o.rt_table = OT;
+                    o.rt_round = rnd;
                 });
                 // a failed owner answers "no winner" everywhere (the round is abandoned at the next agreement)
                 if (fail[li]) HIPCHK(hipMemsetAsync(o.rflag, 0, R * 4, stream));
@@ -2680,9 +2698,14 @@ struct rmc_ctx {
                     grow_outbox(s, wwords[li], wnum[li]);
                     if (wwords[li] >= s.rcap) ensure_ring(s, wwords[li], 0);  // P.rcap also bounds the outbox
                     timed(PH_MAT, [&] {
-                        const KParams Q = round_params(s, gbase);
-                        if (Q.plist) ks.commit_split(Q, s.np, stream);  // a lane per successor slot
-                        else ks.commit(Q, stream);
+                        KParams Q = round_params(s, gbase);
+                        if (Q.plist) {  // a lane per successor slot; the own candidates decided in the round's table
+                            Q.OT = s.rt_table;
+                            Q.ot_round = s.rt_round;
+                            ks.commit_split(Q, s.np, stream);
+                        } else {
+                            ks.commit(Q, stream);
+                        }
                     });
                 });
             }
@@ -2690,9 +2713,11 @@ struct rmc_ctx {
                 Shard &s = sh[li];
                 s.T_count += ins[li];
                 if (!s.np || fail[li]) continue;
-                HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
+                HIPCHK(hipMemcpyAsync(s.hsum, s.sum, (SUM_INS_COMMIT + 1) * 8, hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
                 HIPCHK(hipGetLastError());
+                ins[li] += s.hsum[SUM_INS_COMMIT];  // (a split round's own winners, inserted by its commit)
+                s.T_count += s.hsum[SUM_INS_COMMIT];
                 if (s.hsum[2 + ERR_NSLOTS] && !fail[li]) {
                     fail[li] = flag_code(s.hsum[2 + ERR_NSLOTS]);
                     fail_msg = flag_msg(s.hsum[2 + ERR_NSLOTS]);
@@ -2960,6 +2985,7 @@ struct rmc_ctx {
                 const uint64_t p = s.p0 + (g - s.gblk);
                 const unsigned long long ek = (((p << 16) | slot) << 8) | (gk & 0xFF);
                 s.chunk_sep = round_sep(s);  // (a split round stages its successors but its self-loops)
+            s.chunk_dense = false;       // (sparse: the owners' verdicts come back by slot index)
                 const ErrCounts ec = error_counts(s, kind, ek, s.p0, true);
                 loc[0] = ec.gen;
                 loc[1] = ec.win;

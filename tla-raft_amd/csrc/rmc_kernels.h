@@ -78,14 +78,20 @@ struct HostLoop {
 constexpr uint32_t WTILE = 1024; // parents per tile of the winner-count scan
 constexpr uint32_t WTILES_MAX = 4096; // tiles per chunk (the last block scans four per thread)
 constexpr int SUM_WORDS = 7;     // chunk summary slot of the new states' record words
+constexpr int SUM_INS = 9;       // ... a sharded round's fingerprints inserted into the owner's seen set by k_owner_flags /
+                                 // k_local_flags, and (SUM_INS_COMMIT) by a split round's commit (its own winners)
+constexpr int SUM_INS_COMMIT = 10;
 constexpr int SUM_NZ = 16;       // ... and of the parents with winners (KParams::plist)
 constexpr int SUM_SELF = 17;     // ... and the self-loops set apart (KParams::hcnt, or a host-driven fused chunk's;
                                  // zeroed by the host per chunk)
 constexpr int SUM_HFP = 18;      // ... and a split chunk's successors to fingerprint (its expansion counts them; the
                                  // election of k_hash_probe takes a table of twice as many slots; zeroed with SUM_SELF)
+constexpr int SUM_OCNT = 20;     // ... a sharded round's successors per owner shard (u32[64] over sum[20 .. 52): zeroed
+                                 // with SUM_INS .. SUM_HFP by one memset per round)
 // the fused expansion's self-loop counters: SELF_STRIPES words a 128-B line apart (block b adds to stripe
 // b % SELF_STRIPES), folded by finish_level (k_set_ctl zeroes them for the device loop; 0 between levels)
-constexpr int SUM_SELF_STRIPE = 32, SELF_STRIDE = 16, SELF_STRIPES = 8;  // sum[32 .. 144]
+constexpr int SUM_SELF_STRIPE = 64, SELF_STRIDE = 16, SELF_STRIPES = 8;  // sum[64 .. 176]
+constexpr int SUM_WORDS_TOTAL = 192;  // the chunk summary's words
 
 // In device-loop mode the host sizes every grid on a bound of the level's parents (p_end -
 // p_begin of the KParams it passes); the kernels read the real range from the LevelCtl.
@@ -110,6 +116,11 @@ struct KParams {
     // the seen set with the parent) after them, and every later pass of the chunk visits hcnt[pl] slots
     // only; nullptr: cnt (every successor)
     uint32_t *hcnt;
+    // split chunk (single GPU): the first of each parent's successor slots, dense over the chunk -- the
+    // expansion allocates a round's slots at a time (SUM_HFP), so fp / lslot / score are written and read
+    // without the MAXS-per-parent stride of the sparse layout (q = parent * MAXS + rank, which the
+    // election keys keep as TLC's order either way); nullptr: the sparse layout
+    uint32_t *hoff;
     const uint32_t *off;       // exclusive scan of cnt (chunk-local successor index)
     // per successor (chunk-local index j)
     ulonglong2 *fp;
@@ -239,14 +250,15 @@ void launch_rebase(const uint64_t *in, uint64_t n, uint64_t sub, uint64_t *out, 
 void launch_nzlist(const KParams &P, uint64_t np, hipStream_t s);
 
 // sharded round (W > 1), rmc_engine.hip step_sharded: a successor on its way to its fingerprint's
-// owner shard -- the fingerprint and its global key (parent's index in the level << 8 | rank)
+// owner shard -- the fingerprint and its global key (owner_order: parent's index in the level, rank)
 struct XItem { unsigned long long x, y, key; };
 void launch_route_count(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
                         uint32_t *ocnt, hipStream_t s);
 void launch_route_place(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, uint32_t maxsucc, uint32_t W,
                         uint32_t *cursor, uint64_t g0, XItem *items, uint32_t *perm, uint32_t self, hipStream_t s);
+// (wacc, g0, np: the owner's own parents of the round, whose winners the bids count -- owner_bid)
 void launch_owner_elect(const XItem *it, uint64_t R, Seen seen, ESlot *OT, uint64_t mask,
-                        uint32_t round, uint32_t *rslot, hipStream_t s);
+                        uint32_t round, uint32_t *rslot, uint32_t *wacc, uint64_t g0, uint64_t np, hipStream_t s);
 void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const ESlot *OT, uint32_t round,
                         Seen seen, uint32_t *flag, unsigned long long *inserted, hipStream_t s);
 void launch_scatter_win(const uint32_t *perm, const uint32_t *flag, uint64_t G, const uint4 *score, uint32_t sw4,

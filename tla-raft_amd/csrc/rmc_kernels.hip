@@ -1800,8 +1800,9 @@ __global__ __launch_bounds__(64, (expand_waves<N, MR, MODE, BFV>())) void k_expa
 //       commitIndex / logs / matchIndex / nextIndex of its server s, pendingResponse, the aux
 //       counters and msgs), `m \notin msgs` by a binary search of the parent's sorted ids in LDS;
 //   (d) each enabled successor's rank in TLC order (slot keys increase in TLC order, Next tla:416-430)
-//       from the parent's list of enabled keys, and its staged row at slot pl * MX + rank -- the
-//       layout k_hash_probe, k_insert_winners and the commits read, unchanged.
+//       from the parent's list of enabled keys, and its staged row at slot hoff[pl] + rank (a dense
+//       split chunk: each round's parents take a range of the chunk's slots with one atomic) or
+//       pl * MX + rank (fused levels, sharded rounds) -- the slots k_hash_probe and the commits read.
 #ifndef RMC_ITEMS_PB
 #define RMC_ITEMS_PB 64
 #endif
@@ -1835,7 +1836,8 @@ __device__ __forceinline__ uint32_t row_w0(uint32_t vf, uint32_t ct, uint32_t ro
     return vf | (ct << 4) | (role << 8) | (ci << 12) | (ll << 16) | (s << 20);
 }
 
-// g \in msgs of a parent whose sorted ids are ids[0 .. nm) (LDS): branch-free lower bound
+// g \in msgs of a parent whose sorted ids are ids[0 .. nm) (LDS): branch-free lower bound (a two-step search --
+// the first id of every block of eight, then the block's eight -- issues twice the LDS reads and measured slower)
 template <int MCAP>
 __device__ __forceinline__ bool ids_contain(const uint16_t *ids, uint32_t nm, uint32_t g) {
     uint32_t pos = 0;
@@ -2169,6 +2171,9 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
     __shared__ uint32_t sLive[PB];                 // per parent: messages some action may receive
     __shared__ unsigned long long sSlot[PB];       // slot_range per server, 8 bits each
     __shared__ uint32_t sCnt[PB], sAk[PB];         // enabled successors (self-loops apart), smallest Assert key
+    __shared__ uint32_t sHo[FUSE ? 1 : PB];        // dense split chunk: each parent's first successor slot -- the
+    __shared__ uint32_t sAlloc;                    // batch's successors packed from the start of its parents' sparse
+                                                   // range (b0 * MX ..), each round's after the last (sAlloc used)
     __shared__ uint32_t sSelf[PB];                 // self-loops (P.hcnt: staged nowhere, never fingerprinted)
     __shared__ uint32_t sCc[IC_N];                 // the round's items per class
     // the batch's hash sums (until the hash context is written), then the rounds' item lists and keys
@@ -2182,7 +2187,7 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
     uint16_t *sKey = sQ + IC_N * NT;                    // [NT * NCI] the round's enabled keys, per parent at its items' offset
     __shared__ uint32_t sSpan;
     __shared__ uint32_t sSelfN;                    // fused level: the block's self-loops (finish_level adds them up)
-    __shared__ uint32_t sHfp;                      // split chunk: the block's successors to fingerprint (SUM_HFP)
+    __shared__ uint32_t sHfp;                      // sparse split chunk: the block's successors to fingerprint (SUM_HFP)
     const int tid = threadIdx.x;
     if (tid == 0) {
         sSelfN = 0u;
@@ -2205,6 +2210,7 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
         const uint32_t nb = (uint32_t)(np - b0 < (uint64_t)PB ? np - b0 : (uint64_t)PB);
         // (a) the batch's records: consecutive in the ring (every level is laid out in parent order)
         if (tid < 64) {  // wave 0: a lane per parent
+            if (tid == 0) sAlloc = 0u;
             const uint64_t o = (uint32_t)tid < nb ? P.foff[P.p_begin + b0 + tid] : 0ull;
             const uint64_t first = rdlane64(o, 0);
             const uint64_t last = rdlane64(o, (int)nb - 1);
@@ -2330,7 +2336,9 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
             for (uint32_t st = PB; st; st >>= 1) b = (b + st <= nb && sItm[b + st] <= ibase + NT) ? b + st : b;
             b = b > a ? b : a + 1;  // (a parent's items always fit a round: MCAP + N * SLOTS_PER_SERVER <= NT)
             const uint32_t nI = sItm[b] - ibase < (uint32_t)NT ? sItm[b] - ibase : (uint32_t)NT;
-            // the round's items into their class lists: live messages, then each parent's slots
+            // the round's items into their class lists: live messages, then each parent's slots (one LDS atomic
+            // per item; appending a wave's items per class with ballots and one atomic per class, or finding the
+            // parent by a two-step search, measured slower: profiles/r06_ab_expansion.txt)
             for (uint32_t m = sMsc[a] + (uint32_t)tid; m < sMsc[b]; m += NT) {
                 const uint32_t c = sMI[m];
                 if (c == 15u) continue;
@@ -2386,16 +2394,51 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
             }
             __syncthreads();
             PHASE(4);
+            // per parent: successor count, |msgs|, Assert and deadlock keys (level-local index p); a dense split
+            // chunk's slots for the round's parents: wave 0 scans their counts, the round's slots follow the batch's
+            // earlier rounds' from the start of the batch's sparse range (an LDS counter: a global atomic per round
+            // on the critical path cost the expansion 14 %, profiles/r06_ab_expansion.txt)
+            if (tid < 64) {
+                const uint32_t jj = a + (uint32_t)tid;
+                const bool in = (uint32_t)tid < b - a;
+                if (in) {
+                    const uint64_t pl = b0 + jj, p = P.p_begin + pl;
+                    const uint32_t total = sCnt[jj] + sSelf[jj], ak = sAk[jj];
+                    P.cnt[pl] = total;
+                    if (P.hcnt) P.hcnt[pl] = sCnt[jj];
+                    if (!FUSE && sCnt[jj]) atomicAdd(&sHfp, sCnt[jj]);
+                    P.pnm[pl] = (sCore[jj * NWP + Lo::W_MISC] >> 16) & 0xFFu;
+                    if (ak != KEY_NONE) atomicMin(&P.err[ERR_ASSERT], (((unsigned long long)p << 16) | ak) << 8);
+                    else if (total == 0 && P.check_deadlock)
+                        atomicMin(&P.err[ERR_DEADLOCK], ((unsigned long long)p << 16) << 8);
+                }
+                if (!FUSE && P.hoff) {
+                    uint32_t tot;
+                    const uint32_t x = wave_excl_scan(in ? sCnt[jj] : 0u, tid, &tot);
+                    const uint32_t b32 = (uint32_t)(b0 * (uint64_t)MX) + sAlloc + x;
+                    if (in) {
+                        sHo[jj] = b32;
+                        P.hoff[b0 + jj] = b32;
+                    }
+                    if (tid == 0) sAlloc += tot;
+                }
+            }
+            if (tid < IC_N) sCc[tid] = 0u;  // (every lane has read its item: the sync above)
+            __syncthreads();
+            PHASE(6);
+            // each enabled successor's rank in TLC order and its slot (the next round's class lists touch neither
+            // the key lists nor these parents' counts: no barrier before them)
             if ((uint32_t)tid < nI) {
                 const uint32_t kb = (sItm[j] - ibase) * NCI, cn = sCnt[j];
                 const uint64_t pl = b0 + j;
+                const uint64_t q0 = (!FUSE && P.hoff) ? (uint64_t)sHo[j] : pl * (uint64_t)MX;  // the parent's first slot
 #pragma unroll
                 for (int c = 0; c < NCI; c++) {
                     const RowSucc<S::NADD> &x = c ? ob : o;
                     if (x.key == KEY_NONE || (!FUSE && x.self && P.hcnt)) continue;
                     uint32_t rank = 0;
                     for (uint32_t e = 0; e < cn; e++) rank += (uint32_t)sKey[kb + e] < x.key ? 1u : 0u;
-                    const uint64_t q = pl * (uint64_t)MX + rank;
+                    const uint64_t q = q0 + rank;
                     if constexpr (FUSE) {
                         // a fused level: a self-loop takes its slot as seen (the parent is in the seen set);
                         // any other successor is staged for the commit, fingerprinted from the parent's core
@@ -2423,22 +2466,6 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
                 }
             }
             PHASE(5);
-            // per parent: successor count, |msgs|, Assert and deadlock keys (level-local index p)
-            if ((uint32_t)tid < b - a) {
-                const uint32_t jj = a + (uint32_t)tid;
-                const uint64_t pl = b0 + jj, p = P.p_begin + pl;
-                const uint32_t total = sCnt[jj] + sSelf[jj], ak = sAk[jj];
-                P.cnt[pl] = total;
-                if (P.hcnt) P.hcnt[pl] = sCnt[jj];
-                if (!FUSE && sCnt[jj]) atomicAdd(&sHfp, sCnt[jj]);
-                P.pnm[pl] = (sCore[jj * NWP + Lo::W_MISC] >> 16) & 0xFFu;
-                if (ak != KEY_NONE) atomicMin(&P.err[ERR_ASSERT], (((unsigned long long)p << 16) | ak) << 8);
-                else if (total == 0 && P.check_deadlock)
-                    atomicMin(&P.err[ERR_DEADLOCK], ((unsigned long long)p << 16) << 8);
-            }
-            if (tid < IC_N) sCc[tid] = 0u;  // (every lane has read its item: the sync above)
-            __syncthreads();
-            PHASE(6);
             a = b;
         }
     }
@@ -2454,7 +2481,8 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
 
 // Every successor slot of a split chunk, a lane each: a wave takes 64 consecutive parents, their
 // successor counts are scanned across the wave and successor i of the group goes to lane i % 64 of
-// round i / 64 (its parent found by a binary search over the scan); f(parent pl, rank r).
+// round i / 64 (its parent found by a binary search over the scan); f(parent pl, rank r, its slot sq):
+// sq = pl * MX + r in the sparse layout, P.hoff[pl] + r in a dense split chunk's.
 template <int MX, class F>
 __device__ __forceinline__ void each_successor(const KParams &P, F &&f) {
     const int lane = threadIdx.x & 63;
@@ -2464,6 +2492,7 @@ __device__ __forceinline__ void each_successor(const KParams &P, F &&f) {
          g0 += nwaves * 64) {
         const uint64_t pl = g0 + (uint64_t)lane;
         const uint32_t t = pl < np ? (P.hcnt ? P.hcnt : P.cnt)[pl] : 0u;  // (a split chunk: its self-loops are not visited)
+        const uint32_t h0 = (pl < np && P.hoff) ? P.hoff[pl] : 0u;
         uint32_t tot;
         const uint32_t ex = wave_excl_scan(t, lane, &tot);
         for (uint32_t b0 = 0; b0 < tot; b0 += 64) {
@@ -2476,7 +2505,9 @@ __device__ __forceinline__ void each_successor(const KParams &P, F &&f) {
                 j = v <= i ? j + st : j;
             }
             const uint32_t exj = (uint32_t)__shfl(ex, j, 64);
-            if (i < tot) f(g0 + (uint64_t)j, i - exj);
+            const uint32_t hj = (uint32_t)__shfl(h0, j, 64);
+            const uint64_t pj = g0 + (uint64_t)j;
+            if (i < tot) f(pj, i - exj, P.hoff ? (uint64_t)hj + (i - exj) : pj * (uint64_t)MX + (i - exj));
         }
     }
 }
@@ -2488,12 +2519,26 @@ __device__ __forceinline__ void each_successor(const KParams &P, F &&f) {
 // round + 1 in their low bits, so a slot of an earlier round reads as free, and a key word is the
 // round's key below ((0xFFFF - tag) << 48) -- smaller than any earlier round's -- so every bid just
 // takes the minimum (OT: fingerprint, OK: smallest tagged key; the same protocol as the fused
-// election).  key = (parent's global index in the level << 10) | rank: TLC's order of the level.
+// election).  key = ((parent's global index in the level << 10 | rank) << 2) | e: TLC's order of the level,
+// and in its two low bits the record words a winner adds (elect_key's e; 0 in a received item's key).
 __device__ __forceinline__ unsigned long long owner_key(uint32_t tag, uint64_t key) {
-    return ((unsigned long long)(0xFFFFu - tag) << 48) | key;  // key = global parent index << 10 | rank < 2^48
+    return ((unsigned long long)(0xFFFFu - tag) << 48) | key;  // key < 2^48
 }
+__device__ __forceinline__ uint64_t owner_order(uint64_t gparent, uint32_t rank, uint32_t e) {
+    return (((gparent << 10) | rank) << 2) | e;
+}
+// the same successor: the keys without e
+__device__ __forceinline__ bool owner_same(unsigned long long k, unsigned long long want) { return (k | 3ull) == (want | 3ull); }
+// The shard's own parents of the round (global indices g0 .. g0 + np - 1) and their winner accumulator:
+// a bid that becomes its slot's minimum counts on its parent if the parent is one of these, and takes the
+// displaced bid off its parent if that one is -- so the winners per parent are exact once every bid is in
+// (the fused election's wacc protocol), and no pass over the own successors' verdicts has to count them.
+struct OwnerLocal {
+    uint32_t *wacc;
+    uint64_t g0, np;
+};
 __device__ __forceinline__ uint32_t owner_bid(ESlot *OT, uint64_t mask, uint32_t tag32,
-                                              const ulonglong2 f, uint64_t key) {
+                                              const ulonglong2 f, uint64_t key, const OwnerLocal &loc) {
     const unsigned long long tag = tag32;
     const unsigned long long xk = (f.x & ~0xFFFFull) | tag, yk = (f.y & ~0xFFFFull) | tag;
     // one exit at the bottom (no break): a claimer stores its y inside the loop, in the same
@@ -2531,7 +2576,16 @@ __device__ __forceinline__ uint32_t owner_bid(ESlot *OT, uint64_t mask, uint32_t
             v = __hip_atomic_load(&OT[g].x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    atomicMin(&OT[g].k, owner_key(tag32, key));
+    const unsigned long long nk = owner_key(tag32, key);
+    const unsigned long long old = atomicMin(&OT[g].k, nk);
+    if (loc.wacc && nk < old) {
+        const uint64_t gp = key >> 12;
+        if (gp - loc.g0 < loc.np) atomicAdd(&loc.wacc[gp - loc.g0], 1u + ((uint32_t)(key & 3u) << 12));
+        if ((old >> 48) == (unsigned long long)(0xFFFFu - tag32)) {  // a bid of this round displaced
+            const uint64_t ok = old & ((1ull << 48) - 1ull), op = ok >> 12;
+            if (op - loc.g0 < loc.np) atomicSub(&loc.wacc[op - loc.g0], 1u + ((uint32_t)(ok & 3u) << 12));
+        }
+    }
     return (uint32_t)g;
 }
 
@@ -2568,10 +2622,10 @@ __global__ __launch_bounds__(256, RMC_PROBE_WAVES) void k_hash_probe(KParams P) 
         Lmask = want - 1 < Lmask ? want - 1 : Lmask;
     }
     __syncthreads();
-    each_successor<MX>(P, [&](uint64_t pl, uint32_t r) {
-        const uint64_t q = pl * (uint64_t)MX + r;
+    each_successor<MX>(P, [&](uint64_t pl, uint32_t r, uint64_t sq) {
+        const uint64_t q = pl * (uint64_t)MX + r;  // TLC's order (the election key); sq: the slot
         const uint4 *cx = reinterpret_cast<const uint4 *>(P.hctx + pl * (uint64_t)CTXW);
-        const uint4 *st = P.score + q * (uint64_t)S::SW4;
+        const uint4 *st = P.score + sq * (uint64_t)S::SW4;
         const uint4 sa = st[0], sb = st[1];
         const uint4 sc = S::SW4 > 2 ? st[2] : make_uint4(0u, 0u, 0u, 0u);
         uint32_t pk[CC4 * 4];
@@ -2590,21 +2644,25 @@ __global__ __launch_bounds__(256, RMC_PROBE_WAVES) void k_hash_probe(KParams P) 
             return make_ulonglong2((uint64_t)m.y << 32 | m.x, (uint64_t)m.w << 32 | m.z);
         }, [&](int, uint32_t id) { return P.t.info[id]; }, sa, sb, sc, sK);
         const uint32_t nadd = sb.z >> 16;
-        P.fp[q] = f;
+        P.fp[sq] = f;
         if (P.route) {  // the owners probe and elect; the round's counts per owner (k_route_count's)
             const uint32_t o = fp_owner(f, P.nown);
             if (P.ocnt) atomicAdd(&sOwn[o], 1u);
             // the shard's own successors bid in its owner table right here (k_local_elect's work;
             // the others are marked for the exchange)
-            if (P.OT)
-                P.lslot[q] = o != P.self ? LS_ELECT
-                             : seen_contains(P.seen, f)
-                                 ? LS_SEEN
-                                 : owner_bid(P.OT, P.ot_mask, P.ot_round + 1u, f, ((P.gblk + pl) << 10) | r);
+            if (P.OT) {
+                const uint32_t nm = (pc[Lo::W_MISC] >> 16) & 0xFFu;
+                P.lslot[sq] = o != P.self ? LS_ELECT
+                              : seen_contains(P.seen, f)
+                                  ? LS_SEEN
+                                  : owner_bid(P.OT, P.ot_mask, P.ot_round + 1u, f,
+                                              owner_order(P.gblk + pl, r, (nadd + (nm & 1u) + 1u) >> 1),
+                                              OwnerLocal{P.wacc, P.gblk, P.p_end - P.p_begin});
+            }
             return;
         }
         const uint32_t nm = (pc[Lo::W_MISC] >> 16) & 0xFFu;
-        P.lslot[q] = probe_elect<MX>(P, f, q, (nadd + (nm & 1u) + 1u) >> 1, Lmask);
+        P.lslot[sq] = probe_elect<MX>(P, f, q, (nadd + (nm & 1u) + 1u) >> 1, Lmask);
     });
     if (P.route && P.ocnt) {
         __syncthreads();
@@ -2618,13 +2676,13 @@ __global__ __launch_bounds__(256, RMC_PROBE_WAVES) void k_hash_probe(KParams P) 
 // dependent round trips per parent with winners
 template <int MX>
 __global__ __launch_bounds__(256) void k_insert_winners(KParams P) {
-    each_successor<MX>(P, [&](uint64_t pl, uint32_t r) {
+    each_successor<MX>(P, [&](uint64_t pl, uint32_t r, uint64_t sq) {
         const uint64_t q = pl * (uint64_t)MX + r;
-        const uint32_t g = P.lslot[q];
+        const uint32_t g = P.lslot[sq];
         if (g >= LS_ELECT) return;
         const bool w = elect_q(P.ET[g].k) == (uint32_t)q;
-        if (w) seen_insert(P.seen, P.fp[q]);
-        if (P.split & 4) P.lslot[q] = w ? LS_WIN : LS_SEEN;  // the verdict: the commit needs no election word
+        if (w) seen_insert(P.seen, P.fp[sq]);
+        if (P.split & 4) P.lslot[sq] = w ? LS_WIN : LS_SEEN;  // the verdict: the commit needs no election word
     });
 }
 
@@ -3335,6 +3393,18 @@ __global__ __launch_bounds__(256) void k_commit_split(KParams P) {
     }
 }
 
+// a block's counts into one global counter: one atomic per block, not per wave (every block of a
+// launch adds into the same word -- per-wave atomics on it cost ~0.7 s over Raft.cfg's rounds)
+__device__ __forceinline__ void block_count_add(uint32_t mine, unsigned long long *total) {
+    __shared__ uint32_t blk;
+    if (threadIdx.x == 0) blk = 0u;
+    __syncthreads();
+    for (int d = 32; d >= 1; d >>= 1) mine += __shfl_xor(mine, d, 64);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&blk, mine);
+    __syncthreads();
+    if (threadIdx.x == 0 && blk) atomicAdd(total, (unsigned long long)blk);
+}
+
 // ---- split chunk / sharded round commit, records staged in LDS ------------------------------------
 // k_commit_split gives each winner a lane but leaves it a chain of dependent global loads: its parent's
 // record offset, then the core words, then -- one load per two ids -- the parent's message ids while it
@@ -3360,6 +3430,7 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
     __shared__ uint32_t sOff[PB + 1];           // record offsets in sRec (exclusive scan of record words)
     __shared__ uint32_t sSl[PB + 1];            // successor slots: exclusive scan of cnt
     __shared__ uint32_t sPl[PB];                // chunk-local parent index
+    __shared__ uint32_t sHo[PB];                // its first successor slot (dense split chunk: P.hoff; else pl * MX)
     __shared__ uint32_t sOut[PB];               // next-level index of the parent's first winner (chunk-relative)
     __shared__ uint32_t sWd[PB];                // ... and its record's first word (chunk-relative)
     __shared__ uint32_t sWc[PB];                // the round's winners per parent
@@ -3368,6 +3439,7 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
     __shared__ uint32_t sWr[NT];                // ... and each one's parent | slot << 8
     __shared__ uint32_t sNW;
     const int tid = threadIdx.x;
+    uint32_t own_ins = 0;  // a split sharded round: its own winners this thread put into the seen set
     if constexpr (FUSE) {
 #ifdef RMC_RACE_PROBE
         if (P.ctl) {  // the first block without a parent reads its block after the level advanced (k_commit)
@@ -3398,6 +3470,7 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
                 t = t < (uint32_t)MX ? t : (uint32_t)MX;
                 words = has ? (uint32_t)CCW + ((P.pnm[pl] + 1u) >> 1) : 0u;
                 sPl[tid] = pl;
+                sHo[tid] = P.hoff ? P.hoff[pl] : pl * (uint32_t)MX;
                 sOut[tid] = P.boff[tile] + P.wpos[pl];
                 sWd[tid] = P.boffw[tile] + P.wposw[pl];
                 sWc[tid] = 0u;
@@ -3431,20 +3504,24 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
 #pragma unroll
                 for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < b && sSl[j + st] <= i) ? j + st : j;
                 const uint32_t r = i - sSl[j];
-                const uint64_t q = (uint64_t)sPl[j] * MX + r;
-                // the verdict (LS_WIN: k_insert_winners', an owner's), or -- no insert pass -- the election word
-                const uint32_t g = P.lslot[q];
-                const bool win = (P.route || (P.split & 4)) ? g == LS_WIN
+                const uint64_t q = (uint64_t)sPl[j] * MX + r, sq = (uint64_t)sHo[j] + r;  // TLC's order, the slot
+                // the verdict (LS_WIN: k_insert_winners', an owner's), or -- no insert pass -- the election word; a
+                // split sharded round's own candidates (their slot in the round's owner table) are decided here
+                const uint32_t g = P.lslot[sq];
+                const bool own = P.route && P.OT && g < LS_WIN;  // (a table slot; LS_WIN < LS_ELECT < LS_SEEN)
+                const bool win = own ? owner_same(P.OT[g].k, owner_key(P.ot_round + 1u, owner_order(P.gblk + sPl[j], r, 0u)))
+                               : (P.route || (P.split & 4)) ? g == LS_WIN
                                                             : (g < LS_ELECT && elect_q(P.ET[g].k) == (uint32_t)q);
+                if (own) P.lslot[sq] = win ? LS_WIN : LS_SEEN;  // (the verdict, as k_local_flags leaves it: error counts)
                 if (win) {
-                    const uint4 *src = P.score + q * (uint64_t)SW4;
+                    const uint4 *src = P.score + sq * (uint64_t)SW4;
                     uint4 st4[SW4];
 #pragma unroll
                     for (int x = 0; x < SW4; x++) st4[x] = src[x];
                     const uint32_t w = atomicAdd(&sNW, 1u);
 #pragma unroll
                     for (int x = 0; x < SW4; x++) sSt[w * SW4 + x] = st4[x];
-                    sWr[w] = j | (r << 8);
+                    sWr[w] = j | (r << 8) | (own ? 0x10000u : 0u);
                     const uint32_t words = (uint32_t)CCW + ((P.pnm[sPl[j]] + (st4[1].z >> 16) + 1u) >> 1);
                     sWl[(sSl[j] - sbase) + atomicAdd(&sWc[j], 1u)] = (r << 16) | words;
                 }
@@ -3452,7 +3529,7 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
             __syncthreads();
             // (b) a lane per winner
             if ((uint32_t)tid < sNW) {
-                const uint32_t e = sWr[tid], j = e & 0xFFu, r = e >> 8;
+                const uint32_t e = sWr[tid], j = e & 0xFFu, r = (e >> 8) & 0xFFu;
                 const uint32_t lb = sSl[j] - sbase, wc = sWc[j];
                 uint32_t ord = 0, wofs = 0;
                 for (uint32_t x = 0; x < wc; x++) {
@@ -3473,7 +3550,10 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
                 const uint32_t pl = sPl[j];
                 const uint64_t p = P.p_begin + pl;
                 const uint64_t out = P.next_base + sOut[j] + ord;
-                if (!P.route && !(P.split & 2)) seen_insert(P.seen, P.fp[(uint64_t)pl * MX + r]);  // (no insert pass)
+                if ((!P.route && !(P.split & 2)) || (e & 0x10000u)) {  // (no insert pass; a sharded round's own winner)
+                    seen_insert(P.seen, P.fp[(uint64_t)sHo[j] + r]);
+                    own_ins++;
+                }
                 const uint64_t wd = P.next_wbase + sWd[j] + wofs;  // level-relative
                 const uint64_t rs = ring_wrap(P.nbase + wd, P.rcap);
                 P.noff[out] = wd;
@@ -3539,6 +3619,9 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
             a = b;
         }
     }
+    if constexpr (!FUSE) {
+        if (P.route) block_count_add(own_ins, &P.sum[SUM_INS_COMMIT]);
+    }
     if constexpr (FUSE) {
         // the last block to arrive finishes the level (k_commit's protocol); every wave's atomics and
         // stores are complete before its block's arrival (the barrier)
@@ -3554,17 +3637,6 @@ __global__ __launch_bounds__(64) void k_commit_finish(KParams P) {
     finish_level<MX, RECW_MAX>(P);
 }
 
-// a block's counts into one global counter: one atomic per block, not per wave (every block of a
-// launch adds into the same word -- per-wave atomics on it cost ~0.7 s over Raft.cfg's rounds)
-__device__ __forceinline__ void block_count_add(uint32_t mine, unsigned long long *total) {
-    __shared__ uint32_t blk;
-    if (threadIdx.x == 0) blk = 0u;
-    __syncthreads();
-    for (int d = 32; d >= 1; d >>= 1) mine += __shfl_xor(mine, d, 64);
-    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&blk, mine);
-    __syncthreads();
-    if (threadIdx.x == 0 && blk) atomicAdd(total, (unsigned long long)blk);
-}
 
 // ---- sharded round: the owner's election (W > 1, and the one-rank rehearsal) -------------------
 
@@ -3572,39 +3644,42 @@ __device__ __forceinline__ void block_count_add(uint32_t mine, unsigned long lon
 // straight from the expansion's slots -- no item through the exchange -- and the slot (or LS_SEEN)
 // waits in lslot for k_local_flags.  Successors other shards own are marked LS_ELECT and left to
 // the exchange (their verdicts arrive by k_scatter_win).
-template <int MX>
+template <int MX, int SW4>
 __global__ __launch_bounds__(256) void k_local_elect(KParams P, Seen seen, ESlot *OT,
                                                      uint64_t mask, uint32_t round, uint32_t W, uint32_t self,
                                                      uint64_t g0) {
-    each_successor<MX>(P, [&](uint64_t pl, uint32_t r) {
-        const uint64_t q = pl * (uint64_t)MX + r;
+    const OwnerLocal loc{P.wacc, g0, P.p_end - P.p_begin};
+    each_successor<MX>(P, [&](uint64_t pl, uint32_t r, uint64_t q) {  // (sharded rounds: the sparse layout)
         const ulonglong2 f = P.fp[q];
-        P.lslot[q] = fp_owner(f, W) != self ? LS_ELECT
-                     : seen_contains(seen, f) ? LS_SEEN
-                                              : owner_bid(OT, mask, round + 1u, f, ((g0 + pl) << 10) | r);
+        if (fp_owner(f, W) != self) {
+            P.lslot[q] = LS_ELECT;
+            return;
+        }
+        if (seen_contains(seen, f)) {
+            P.lslot[q] = LS_SEEN;
+            return;
+        }
+        const uint32_t nadd = P.score[q * (uint64_t)SW4 + 1].z >> 16;
+        P.lslot[q] = owner_bid(OT, mask, round + 1u, f, owner_order(g0 + pl, r, (nadd + (P.pnm[pl] & 1u) + 1u) >> 1), loc);
     });
 }
 
-// ... once every bid of the round is in (the received ones too): the verdict in lslot (LS_WIN /
-// LS_SEEN), each winner into the seen set and counted on its parent as k_scatter_win counts a
-// received verdict (wacc = winners | extra words << 12), *inserted counting them.
-template <int MX, int SW4>
+// ... once every bid of the round is in (the received ones too), a round below the split size (a split
+// round's commit decides its own candidates itself): the verdict in lslot (LS_WIN / LS_SEEN) and each
+// winner into the seen set, *inserted counting them (the bids counted the winners on their parents).
+template <int MX>
 __global__ __launch_bounds__(256) void k_local_flags(KParams P, Seen seen, const ESlot *OT, uint32_t round,
                                                      uint32_t W, uint32_t self, uint64_t g0,
                                                      unsigned long long *inserted) {
     const uint32_t tag = round + 1u;
     uint32_t mine = 0;
-    each_successor<MX>(P, [&](uint64_t pl, uint32_t r) {
-        const uint64_t q = pl * (uint64_t)MX + r;
+    each_successor<MX>(P, [&](uint64_t pl, uint32_t r, uint64_t q) {  // (sharded rounds: the sparse layout)
         const uint32_t g = P.lslot[q];
         if (g == LS_ELECT || g == LS_SEEN) return;  // another shard's, or seen: nothing to decide
-        const bool w = OT[g].k == owner_key(tag, ((g0 + pl) << 10) | r);
+        const bool w = owner_same(OT[g].k, owner_key(tag, owner_order(g0 + pl, r, 0u)));
         P.lslot[q] = w ? LS_WIN : LS_SEEN;
         if (w) {
             seen_insert(seen, P.fp[q]);
-            const uint32_t nadd = P.score[q * (uint64_t)SW4 + 1].z >> 16;
-            const uint32_t e = (nadd + (P.pnm[pl] & 1u) + 1u) >> 1;
-            atomicAdd(&P.wacc[pl], 1u + (e << 12));
             mine++;
         }
     });
@@ -3682,13 +3757,13 @@ struct Launch {
     static void local_elect(const KParams &P, uint64_t np, Seen seen, ESlot *OT,
                             uint64_t mask, uint32_t round, uint32_t W, uint32_t self, uint64_t g0, hipStream_t s) {
         const uint64_t blocks = (np + 255) / 256;  // a wave per 64 parents (each_successor)
-        hipLaunchKernelGGL((k_local_elect<MX>), dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u),
+        hipLaunchKernelGGL((k_local_elect<MX, Spec<N, V, MR>::SW4>), dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u),
                            dim3(256), 0, s, P, seen, OT, mask, round, W, self, g0);
     }
     static void local_flags(const KParams &P, uint64_t np, Seen seen, const ESlot *OT, uint32_t round,
                             uint32_t W, uint32_t self, uint64_t g0, unsigned long long *inserted, hipStream_t s) {
         const uint64_t blocks = (np + 255) / 256;
-        hipLaunchKernelGGL((k_local_flags<MX, Spec<N, V, MR>::SW4>),
+        hipLaunchKernelGGL((k_local_flags<MX>),
                            dim3(blocks ? (unsigned)(blocks < 16384ull ? blocks : 16384ull) : 1u), dim3(256), 0, s, P,
                            seen, OT, round, W, self, g0, inserted);
     }
@@ -3862,7 +3937,7 @@ __global__ __launch_bounds__(256) void k_route_place(const ulonglong2 *__restric
             const uint32_t o = fp_owner(f, W);
             if (o == self) continue;
             const uint32_t pos = base[o] + atomicAdd(&h[o], 1u);
-            items[pos] = XItem{f.x, f.y, ((g0 + pl) << 10) | r};
+            items[pos] = XItem{f.x, f.y, owner_order(g0 + pl, r, 0u)};
             perm[pos] = (uint32_t)q;
         }
         __syncthreads();
@@ -3872,12 +3947,12 @@ __global__ __launch_bounds__(256) void k_route_place(const ulonglong2 *__restric
 // Owner: the received successors of the round -- bids (owner_bid) by k_owner_elect, and by the
 // owner's own successors in k_local_elect.
 __global__ __launch_bounds__(256) void k_owner_elect(const XItem *__restrict__ it, uint64_t R, Seen seen,
-                                                     ESlot *OT, uint64_t mask,
-                                                     uint32_t round, uint32_t *__restrict__ rslot) {
+                                                     ESlot *OT, uint64_t mask, uint32_t round,
+                                                     uint32_t *__restrict__ rslot, OwnerLocal loc) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
         const XItem e = it[i];
         const ulonglong2 f = make_ulonglong2(e.x, e.y);
-        rslot[i] = seen_contains(seen, f) ? LS_SEEN : owner_bid(OT, mask, round + 1u, f, e.key);
+        rslot[i] = seen_contains(seen, f) ? LS_SEEN : owner_bid(OT, mask, round + 1u, f, e.key, loc);
     }
 }
 
@@ -3892,7 +3967,7 @@ __global__ __launch_bounds__(256) void k_owner_flags(const XItem *__restrict__ i
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t g = rslot[i];
         const XItem e = it[i];
-        const bool w = g != LS_SEEN && OT[g].k == owner_key(tag, e.key);
+        const bool w = g != LS_SEEN && owner_same(OT[g].k, owner_key(tag, e.key));
         flag[i] = w ? 1u : 0u;
         if (w) {
             seen_insert(seen, make_ulonglong2(e.x, e.y));
@@ -3955,8 +4030,10 @@ void launch_route_place(const ulonglong2 *fp, const uint32_t *cnt, uint64_t np, 
                            perm, self);
 }
 void launch_owner_elect(const XItem *it, uint64_t R, Seen seen, ESlot *OT, uint64_t mask,
-                        uint32_t round, uint32_t *rslot, hipStream_t s) {
-    if (R) hipLaunchKernelGGL(k_owner_elect, dim3(grid256(R)), dim3(256), 0, s, it, R, seen, OT, mask, round, rslot);
+                        uint32_t round, uint32_t *rslot, uint32_t *wacc, uint64_t g0, uint64_t np, hipStream_t s) {
+    if (R)
+        hipLaunchKernelGGL(k_owner_elect, dim3(grid256(R)), dim3(256), 0, s, it, R, seen, OT, mask, round, rslot,
+                           OwnerLocal{wacc, g0, np});
 }
 void launch_owner_flags(const XItem *it, uint64_t R, const uint32_t *rslot, const ESlot *OT, uint32_t round,
                         Seen seen, uint32_t *flag, unsigned long long *inserted, hipStream_t s) {
