@@ -2164,6 +2164,7 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
     __shared__ uint32_t sRec[PB * RECW];           // the batch's records, as in the ring
     __shared__ uint32_t sCore[PB * NWP];           // their nibble cores
     __shared__ uint8_t sMI[PB * S::MCAP];          // per message of the batch: its class (15: none)
+    __shared__ uint8_t sMJ[PB * S::MCAP];          // ... and its parent (the class lists' item codes)
     __shared__ uint32_t sInf[FUSE ? PB * S::MCAP : 1];  // fused level: ... and its info word (one round trip less)
     __shared__ uint32_t sVp[PB * N];               // per parent and server: VoteResps to it in its term (tla:160-164)
     __shared__ uint32_t sOff[PB];                  // record's first word in sRec
@@ -2292,6 +2293,7 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
             if (mi_type(inf) == VRESP && mi_term(inf) == ct) atomicAdd(&sVp[j * N + dst], 1u);
             const uint32_t c = msg_class(inf, ct, nib(pc[Lo::W_ROLE], dst));
             sMI[m] = (uint8_t)(c == IC_DEAD ? 15u : c);
+            sMJ[m] = (uint8_t)j;
             if constexpr (FUSE) sInf[m] = inf;
             if (c != IC_DEAD) atomicAdd(&sLive[j], 1u);
         }
@@ -2336,24 +2338,27 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
             for (uint32_t st = PB; st; st >>= 1) b = (b + st <= nb && sItm[b + st] <= ibase + NT) ? b + st : b;
             b = b > a ? b : a + 1;  // (a parent's items always fit a round: MCAP + N * SLOTS_PER_SERVER <= NT)
             const uint32_t nI = sItm[b] - ibase < (uint32_t)NT ? sItm[b] - ibase : (uint32_t)NT;
-            // the round's items into their class lists: live messages, then each parent's slots (one LDS atomic
-            // per item; appending a wave's items per class with ballots and one atomic per class, or finding the
-            // parent by a two-step search, measured slower: profiles/r06_ab_expansion.txt)
+            // the round's items into their class lists: live messages (each one's parent noted by the message pass:
+            // no search), then each parent's slots, a server's positions all taken before any is written so its
+            // LDS atomics are in flight together (round 6: expansion -8 %, profiles/r06_ab_class_lists.txt); one LDS
+            // atomic per item -- appending a wave's items per class with ballots and one atomic per class, or
+            // finding the parent by a two-step search, measured slower (profiles/r06_ab_expansion.txt)
             for (uint32_t m = sMsc[a] + (uint32_t)tid; m < sMsc[b]; m += NT) {
                 const uint32_t c = sMI[m];
                 if (c == 15u) continue;
-                uint32_t j = a;  // the last parent j with sMsc[j] <= m
-#pragma unroll
-                for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < b && sMsc[j + st] <= m) ? j + st : j;
+                const uint32_t j = sMJ[m];
                 sQ[c * NT + atomicAdd(&sCc[c], 1u)] = (uint16_t)((j << 8) | (m - sMsc[j]));
             }
             for (uint32_t q = (uint32_t)tid; q < (b - a) * (uint32_t)N; q += NT) {  // a lane per (parent, server)
                 const uint32_t j = a + q / N, u = q % N;
-                const uint32_t rg = (uint32_t)(sSlot[j] >> (8 * u)) & 0xFFu;
-                for (uint32_t r = 0; r < (rg >> 4); r++) {
-                    const uint32_t t = (rg & 15u) + r, c = slot_class<N, V>(t);
-                    sQ[c * NT + atomicAdd(&sCc[c], 1u)] = (uint16_t)((j << 8) | 0x80u | (u << 4) | t);
-                }
+                const uint32_t rg = (uint32_t)(sSlot[j] >> (8 * u)) & 0xFFu, n = rg >> 4, t0 = rg & 15u;
+                uint32_t pos[S::SLOTS_PER_SERVER];
+#pragma unroll
+                for (uint32_t r = 0; r < (uint32_t)S::SLOTS_PER_SERVER; r++)
+                    if (r < n) pos[r] = atomicAdd(&sCc[slot_class<N, V>(t0 + r)], 1u);
+#pragma unroll
+                for (uint32_t r = 0; r < (uint32_t)S::SLOTS_PER_SERVER; r++)
+                    if (r < n) sQ[slot_class<N, V>(t0 + r) * NT + pos[r]] = (uint16_t)((j << 8) | 0x80u | (u << 4) | (t0 + r));
             }
             __syncthreads();
             PHASE(7);

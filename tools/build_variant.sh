@@ -9,6 +9,8 @@ FLAGS=""
 for part in ${1//+/ }; do  # several specs joined by '+', e.g. fpb16+fw4
 case "$part" in
   prof) FLAGS="$FLAGS -DRMC_PHASE_PROF" ;;
+  # the sources as they are, beside the default build (an A/B of a source change: tools/ab_bench.sh)
+  plain) ;;
   w1) FLAGS="$FLAGS -DRMC_WIDE_WAVES=1" ;;
   # the item-parallel split expansion: waves / SIMD its registers are cut for (e.g. iw6)
   iw*) FLAGS="$FLAGS -DRMC_ITEMS_WAVES=${part#iw}" ;;
@@ -27,10 +29,10 @@ case "$part" in
   # n = 3 occupancy: expansion waves / SIMD, commit waves / SIMD, grid blocks / CU (e.g. n3w6c4g32)
   n3w*) X=${part#n3w}; W=${X%%c*}; X=${X#*c}; C=${X%%g*}; G=${X#*g}
         FLAGS="$FLAGS -DRMC_N3_WAVES=$W -DRMC_N3_COMMIT_WAVES=$C -DRMC_GRID_PER_CU=$G" ;;
-  *) echo "usage: $0 prof|w1|iw<W>|pw<W>|nt<T>|pb<P>|fpb<P>|fcpb<P>|fw<W>|n3w<W>c<C>g<G>[+...]" >&2; exit 2 ;;
+  *) echo "usage: $0 prof|plain|w1|iw<W>|pw<W>|nt<T>|pb<P>|fpb<P>|fcpb<P>|fw<W>|n3w<W>c<C>g<G>[+...]" >&2; exit 2 ;;
 esac
 done
-OUT=build_$1
+OUT=${VARIANT_DIR:-build_$1}  # (VARIANT_DIR: another directory for the same flags)
 mkdir -p "$OUT"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 $HIPCC --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function -DRMC_WITH_RCCL $FLAGS -Iinclude -I../include -Icsrc \

@@ -8,6 +8,7 @@
 #   prof_bench   rocprofv3 kernel stats of bench's headline (Raft.cfg, 2 timed steps)
 #   prof_c2      rocprofv3 kernel stats of bench --workload c2 (configs[1])
 #   pmc_bench    tools/pmc.sh over bench's headline (one Raft.cfg exhaustion per pass) + pmc_summary.py
+#   pmc_c2       ... over bench.py --workload c2 (configs[1])
 #   c4           configs[3] as deep as one GPU goes  rccl1       Raft.cfg through a one-rank RCCL communicator
 #   prof_rccl1   rocprofv3 kernel stats of the rccl1 run
 #   c4split      configs[3] on one GPU with the 48 GB seen set / 200 GB ring split
@@ -39,10 +40,14 @@ for s in "$@"; do
            cut -c1-600 "$O/benchd.json" ;;
     prof_bench) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof_bench" -o bench -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-configs1 --no-cpu-baseline --no-probe-peak > "$O/prof_bench.log" 2>&1 || { tail -20 "$O/prof_bench.log"; exit 1; }
            tail -c 700 "$O/prof_bench.log"; find "$O/prof_bench" -name '*kernel_stats.csv' -exec head -12 {} \; ;;
+    c2) timeout -k 10 300 python -u bench.py --workload c2 --steps 20 --warmup 5 --no-cpu-baseline --no-probe-peak > "$O/c2.json" 2> "$O/c2.err" || { tail "$O/c2.err"; exit 1; }
+           cut -c1-400 "$O/c2.json" ;;
     prof_c2) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof_c2" -o bench -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-probe-peak --workload c2 > "$O/prof_c2.log" 2>&1 || { tail -20 "$O/prof_c2.log"; exit 1; }
            find "$O/prof_c2" -name '*kernel_stats.csv' -exec head -12 {} \; ;;
-    pmc_bench) WORKLOAD=raftcfg bash tools/pmc.sh || exit 1
-           python tools/pmc_summary.py gpurun_out/pmc "$O/pmc_raftcfg.json" ;;
+    pmc_bench) rm -rf gpurun_out/pmc; WORKLOAD=raftcfg bash tools/pmc.sh || exit 1
+           python tools/pmc_summary.py gpurun_out/pmc "$O/pmc_raftcfg.json" && rm -rf gpurun_out/pmc ;;
+    pmc_c2) rm -rf gpurun_out/pmc; WORKLOAD=c2 bash tools/pmc.sh || exit 1
+           python tools/pmc_summary.py gpurun_out/pmc "$O/pmc_c2.json" && rm -rf gpurun_out/pmc ;;
     c4) timeout -k 10 300 python -u tools/explore.py 5 1 3 3 --budget 150 > "$O/c4.log" 2>&1 || { tail -20 "$O/c4.log"; exit 1; }
            tail -4 "$O/c4.log" ;;
     c4split) timeout -k 10 300 python -u tools/explore.py 5 1 3 3 --seen-mem-gb 48 --frontier-mem-gb 200 --budget 200 > "$O/c4split.log" 2>&1 || { tail -20 "$O/c4split.log"; exit 1; }
