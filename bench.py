@@ -622,6 +622,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe-peak", action="store_true")
     ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] leg (N = 1)")
+    ap.add_argument("--chunk-successors", type=int, default=0,
+                    help="successor slots per chunk (0: the engine's default; a tuning run)")
     ap.add_argument("--configs3", action="store_true", help="N > 1: first take configs[3] as deep as the node's "
                     "HBM and a time budget allow (child processes, before the bench touches the GPU)")
     ap.add_argument("--sharded-child", action="store_true", help=argparse.SUPPRESS)
@@ -648,7 +650,7 @@ def main():
     w = WORKLOADS[args.workload]
     cfg = raftmc.ModelConfig(n_servers=w["n"], n_vals=w["V"], max_election=w["E"], max_restart=w["R"],
                              invariants=("Inv",), check_deadlock=False, device=local,
-                             timing_phases=TIMED_PHASES)
+                             timing_phases=TIMED_PHASES, chunk_successors=args.chunk_successors)
     parallelism = "single-gpu"
     if world > 1:
         # rank 0 creates the RCCL id; the control-plane group (gloo) broadcasts it

@@ -2159,6 +2159,7 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
     constexpr int NCI = BFV ? 2 : 1;  // candidates of a message item
     constexpr int NPR = N * (N - 1);
     constexpr int CTXW = ctx_words<N, V>(), CC = ((CCW + 3) / 4) * 4;
+    constexpr int RC = FUSE ? 1 : 4;  // record words per lane in flight in the batch's copy (a fused batch: one)
     static_assert(S::MCAP + N * S::SLOTS_PER_SERVER <= NT, "a parent's items fit one evaluation round");
     static_assert(S::MCAP <= 128 && PB <= 64, "item codes: parent << 8 | slot bit << 7 | message index or s << 4 | t");
     __shared__ uint32_t sRec[PB * RECW];           // the batch's records, as in the ring
@@ -2230,7 +2231,16 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
             const uint64_t f0 = P.foff[P.p_begin + b0];
             const uint64_t start = ring_wrap(P.fbase + f0, P.rcap);
             const uint32_t span = sSpan;
-            for (uint32_t w = (uint32_t)tid; w < span; w += NT) sRec[w] = ring_word(P.front, start, w, P.rcap);
+            // (RC words per lane in flight at once: the loads go out together, then the LDS stores)
+            for (uint32_t w0 = (uint32_t)tid; w0 < span; w0 += RC * NT) {
+                uint32_t v[RC];
+#pragma unroll
+                for (int k = 0; k < RC; k++)
+                    if (w0 + k * NT < span) v[k] = ring_word(P.front, start, w0 + k * NT, P.rcap);
+#pragma unroll
+                for (int k = 0; k < RC; k++)
+                    if (w0 + k * NT < span) sRec[w0 + k * NT] = v[k];
+            }
         }
         __syncthreads();
         PHASE(0);
@@ -3438,6 +3448,7 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
     __shared__ uint32_t sHo[PB];                // its first successor slot (dense split chunk: P.hoff; else pl * MX)
     __shared__ uint32_t sOut[PB];               // next-level index of the parent's first winner (chunk-relative)
     __shared__ uint32_t sWd[PB];                // ... and its record's first word (chunk-relative)
+    __shared__ uint64_t sRs[PB];                // its record's first word in the ring
     __shared__ uint32_t sWc[PB];                // the round's winners per parent
     __shared__ uint32_t sWl[NT];                // per parent at its slots' round offset: (slot << 16) | record words
     __shared__ uint4 sSt[NT * SW4];             // the round's winners' staged rows, dense
@@ -3475,6 +3486,7 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
                 t = t < (uint32_t)MX ? t : (uint32_t)MX;
                 words = has ? (uint32_t)CCW + ((P.pnm[pl] + 1u) >> 1) : 0u;
                 sPl[tid] = pl;
+                sRs[tid] = words ? ring_wrap(P.fbase + P.foff[P.p_begin + pl], P.rcap) : 0ull;
                 sHo[tid] = P.hoff ? P.hoff[pl] : pl * (uint32_t)MX;
                 sOut[tid] = P.boff[tile] + P.wpos[pl];
                 sWd[tid] = P.boffw[tile] + P.wposw[pl];
@@ -3486,13 +3498,25 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
             if (tid == 0) { sSl[nb] = ts; sOff[nb] = tw; sNW = 0u; }
         }
         __syncthreads();
-        // the records, a lane per word
-        for (uint32_t w = (uint32_t)tid; w < sOff[nb]; w += NT) {
-            uint32_t j = 0;
+        // the records, a lane per word (from each parent's ring start, read once by wave 0), RC words per lane
+        // in flight at once (a fused batch of 16 parents is one pass of the block: RC = 1)
+        constexpr int RC = FUSE ? 1 : 4;
+        const uint32_t tw = sOff[nb];
+        for (uint32_t w0 = (uint32_t)tid; w0 < tw; w0 += RC * NT) {
+            uint32_t v[RC];
 #pragma unroll
-            for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < nb && sOff[j + st] <= w) ? j + st : j;
-            const uint64_t start = ring_wrap(P.fbase + P.foff[P.p_begin + sPl[j]], P.rcap);
-            sRec[w] = ring_word(P.front, start, w - sOff[j], P.rcap);
+            for (int k = 0; k < RC; k++) {
+                const uint32_t w = w0 + k * NT;
+                if (w < tw) {
+                    uint32_t j = 0;
+#pragma unroll
+                    for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < nb && sOff[j + st] <= w) ? j + st : j;
+                    v[k] = ring_word(P.front, sRs[j], w - sOff[j], P.rcap);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < RC; k++)
+                if (w0 + k * NT < tw) sRec[w0 + k * NT] = v[k];
         }
         __syncthreads();
         for (uint32_t a = 0; a < nb;) {
