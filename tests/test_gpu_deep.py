@@ -13,9 +13,14 @@ oracle/raft_oracle.c as the checker:
         order) is in its exact symmetry class (orc_canon_hash);
   (iv)  distinct sampled states are distinct exact classes (the seen set kept one state per class);
   (v)   its whole-state fingerprint (k_fp_states) is in the seen set: the split chunks' lane-per-
-        successor fingerprints (k_hash_probe) and the single-state path agree at depth.
+        successor fingerprints (k_hash_probe) and the single-state path agree at depth;
+  (vi)  its five server-permuted images (SYMMETRY symmServers, Raft.cfg:24) and a copy with every variable
+        outside the VIEW changed (Raft.tla:38, Raft.cfg:26) have its fingerprint: the fingerprint is a function
+        of the symmetry class at the deep levels, so no class is split in two -- which (iv) alone, on a
+        sample, could only see if both halves were drawn.
 Parity is still unpinned by TLC (no TLC anywhere here); this pins the deep levels to the restatement."""
 import ctypes
+import itertools
 import os
 import random
 
@@ -32,6 +37,27 @@ ORC_SO = os.path.join(ROOT, "oracle", "build", "libraft_oracle.so")
 N, V, E, RR = 3, 2, 3, 3
 SAMPLES = 10_000
 LO, HI = 35, 72
+
+
+def _images(u):
+    """(vi): the state's server-permuted images and a copy with its non-VIEW variables changed (unpacked)."""
+    st = R.state_from_json(raftmc.unpacked_to_state(list(u), N, V))
+    out = []
+    for pi in itertools.permutations(range(N)):
+        if list(pi) == list(range(N)):
+            continue
+        vf, ct, logs, mi, ni, ci, msgs, role = R.permute_view(st.view(), pi)
+        img = R.State(votedFor=vf, currentTerm=ct, logs=logs, matchIndex=mi, nextIndex=ni, commitIndex=ci,
+                      msgs=frozenset(msgs), role=role, electionCount=st.electionCount,
+                      restartCount=st.restartCount, pendingResponse=st.pendingResponse, valSent=st.valSent)
+        out.append(img)
+    # outside the VIEW: electionCount, restartCount, pendingResponse, valSent (Raft.tla:29, 34)
+    out.append(R.State(votedFor=st.votedFor, currentTerm=st.currentTerm, logs=st.logs, matchIndex=st.matchIndex,
+                       nextIndex=st.nextIndex, commitIndex=st.commitIndex, msgs=st.msgs, role=st.role,
+                       electionCount=(st.electionCount + 1) % (E + 1), restartCount=(st.restartCount + 1) % (RR + 1),
+                       pendingResponse=tuple(tuple(not x for x in r) for r in st.pendingResponse),
+                       valSent=tuple(0 if x == R.NONE else R.NONE for x in st.valSent)))
+    return [raftmc.state_to_unpacked(R.state_to_json(x), N, V) for x in out]
 
 
 def _orc():
@@ -78,6 +104,7 @@ def test_raft_cfg_deep_levels_sampled():
         skeys = (ctypes.c_uint32 * 512)()
         h = (ctypes.c_uint64 * 2)()
         batch, classes, n_succ = [], set(), 0
+        images, owner = [], []  # (vi): each image and the batch index of its state
         for L, gid in picks:
             keys, gids = mc.state_path(gid)
             # (i) L - 1 steps, through the levels in order
@@ -103,6 +130,9 @@ def test_raft_cfg_deep_levels_sampled():
             assert mine not in classes, f"level {L} state {gid}: a second state of one symmetry class"
             classes.add(mine)
             # (ii) + (v): the state and every oracle successor of it
+            for img in _images(out[:r]):
+                images.append(np.asarray(img + [0] * (stride - len(img)), dtype=np.int32))
+                owner.append(len(batch))
             batch.append(np.frombuffer(out, dtype=np.int32, count=stride).copy())
             ns = lib.orc_successors(N, V, E, RR, 0, out, succ, stride, 512, skeys)
             assert ns >= 0
@@ -114,5 +144,10 @@ def test_raft_cfg_deep_levels_sampled():
         present = mc.seen_contains(fps)
         missing = sum(1 for p in present if not p)
         assert missing == 0, f"{missing} of {len(batch)} sampled states / oracle successors not in the seen set"
-    print(f"deep check: {len(picks)} states over levels {LO}-{HI}, {n_succ} oracle successors, all in the seen set")
+        # (vi) the images' fingerprints are their states'
+        ifp = mc.fingerprints_unpacked(np.ascontiguousarray(np.stack(images)), stride, len(images))
+        split = sum(1 for k, f in enumerate(ifp) if tuple(f) != tuple(fps[owner[k]]))
+        assert split == 0, f"{split} of {len(images)} symmetric / non-VIEW images fingerprint apart from their states"
+    print(f"deep check: {len(picks)} states over levels {LO}-{HI}, {n_succ} oracle successors, all in the seen set; "
+          f"{len(images)} images, each with its state's fingerprint")
     assert len(picks) == SAMPLES

@@ -1922,9 +1922,13 @@ struct rmc_ctx {
             // without a host round trip; large ones read the winner count back before commit.
             const uint64_t Gub = np_ * (uint64_t)ks.maxsucc;
             maybe_migrate(s, s.T_count + Gub);
-            const uint64_t consumed = (s.ring_fixed && p0) ? d2h(s.cur_off + p0) : 0;
+            // where the chunk's first record starts (the ring words before it are consumed): read here only
+            // for a chunk that may size on its bound; a larger one reads it with its winner count (no round
+            // trip of its own while the device idles)
+            const bool may_small = Gub <= (1ull << 20);
+            uint64_t consumed = (s.ring_fixed && p0 && may_small) ? d2h(s.cur_off + p0) : 0;
             // bounds that a fixed ring or a compact seen set cannot take go the exact way
-            const bool small = Gub <= (1ull << 20) && seen_room(s, s.T_count + Gub) && ring_room(s, np_ * MSW, consumed);
+            const bool small = may_small && seen_room(s, s.T_count + Gub) && ring_room(s, np_ * MSW, consumed);
             if (small) {
                 ensure_ring(s, np_ * MSW, consumed);
                 ensure_off(s.nxt_off, s.nxt_off_cap, s.nxt_n, s.nxt_n + Gub);
@@ -1978,7 +1982,11 @@ struct rmc_ctx {
             });
             if (!small) {
                 HIPCHK(hipMemcpyAsync(s.hsum, s.sum, 8 * 8, hipMemcpyDeviceToHost, stream));
+                unsigned long long *hc = s.hsum + SUM_WORDS_TOTAL - 1;  // (a pinned word nothing else uses here)
+                const bool read_consumed = s.ring_fixed && p0 && !may_small;
+                if (read_consumed) HIPCHK(hipMemcpyAsync(hc, s.cur_off + p0, 8, hipMemcpyDeviceToHost, stream));
                 HIPCHK(hipStreamSynchronize(stream));
+                if (read_consumed) consumed = *hc;
                 collect_times(st);
                 const uint64_t Wub = s.hsum[1], Wwords = s.hsum[SUM_WORDS];
                 ensure_ring(s, Wwords, consumed);
