@@ -3454,6 +3454,8 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
     __shared__ uint4 sSt[NT * SW4];             // the round's winners' staged rows, dense
     __shared__ uint32_t sWr[NT];                // ... and each one's parent | slot << 8
     __shared__ uint32_t sNW;
+    __shared__ uint8_t sWj[FUSE ? 1 : PB * RECW];  // per record word of the batch: its parent
+    __shared__ uint8_t sSj[FUSE ? 1 : PB * MX];    // per successor slot of the batch: its parent
     const int tid = threadIdx.x;
     uint32_t own_ins = 0;  // a split sharded round: its own winners this thread put into the seen set
     if constexpr (FUSE) {
@@ -3496,10 +3498,16 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
             const uint32_t xs = wave_excl_scan(t, tid, &ts), xw = wave_excl_scan(words, tid, &tw);
             if ((uint32_t)tid < nb) { sSl[tid] = xs; sOff[tid] = xw; }
             if (tid == 0) { sSl[nb] = ts; sOff[nb] = tw; sNW = 0u; }
+            // each record word's and each successor slot's parent (the copy and the rounds: no search; a fused
+            // level's 16-parent batches search -- the notes cost configs[1] 5 %, profiles/r06_ab_commit_parents.txt)
+            if constexpr (!FUSE) {
+                for (uint32_t k = 0; k < words; k++) sWj[xw + k] = (uint8_t)tid;
+                for (uint32_t k = 0; k < t; k++) sSj[xs + k] = (uint8_t)tid;
+            }
         }
         __syncthreads();
-        // the records, a lane per word (from each parent's ring start, read once by wave 0), RC words per lane
-        // in flight at once (a fused batch of 16 parents is one pass of the block: RC = 1)
+        // the records, a lane per word (its parent noted by wave 0, whose ring start wave 0 read once), RC words
+        // per lane in flight at once (a fused batch of 16 parents is one pass of the block: RC = 1)
         constexpr int RC = FUSE ? 1 : 4;
         const uint32_t tw = sOff[nb];
         for (uint32_t w0 = (uint32_t)tid; w0 < tw; w0 += RC * NT) {
@@ -3509,8 +3517,12 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
                 const uint32_t w = w0 + k * NT;
                 if (w < tw) {
                     uint32_t j = 0;
+                    if constexpr (FUSE) {
 #pragma unroll
-                    for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < nb && sOff[j + st] <= w) ? j + st : j;
+                        for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < nb && sOff[j + st] <= w) ? j + st : j;
+                    } else {
+                        j = sWj[w];
+                    }
                     v[k] = ring_word(P.front, sRs[j], w - sOff[j], P.rcap);
                 }
             }
@@ -3530,8 +3542,12 @@ __global__ __launch_bounds__(XB_THREADS) void k_commit_items(KParams P) {
             if ((uint32_t)tid < nS) {
                 const uint32_t i = sbase + (uint32_t)tid;
                 uint32_t j = a;
+                if constexpr (FUSE) {
 #pragma unroll
-                for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < b && sSl[j + st] <= i) ? j + st : j;
+                    for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < b && sSl[j + st] <= i) ? j + st : j;
+                } else {
+                    j = sSj[i];
+                }
                 const uint32_t r = i - sSl[j];
                 const uint64_t q = (uint64_t)sPl[j] * MX + r, sq = (uint64_t)sHo[j] + r;  // TLC's order, the slot
                 // the verdict (LS_WIN: k_insert_winners', an owner's), or -- no insert pass -- the election word; a
