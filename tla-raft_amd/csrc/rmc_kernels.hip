@@ -2148,8 +2148,11 @@ __device__ __forceinline__ uint32_t slot_class(uint32_t t) {
          : t == 2 + (uint32_t)V + (N - 1) ? IC_LCC : IC_RS;
 }
 
+// (the fused BecomeFollower kernel is not cut to RMC_FUSED_WAVES: at 4 waves per SIMD it spills 23 VGPRs, and with
+// the message-parent notes that build gave wrong BecomeFollower n3 counts while the uncut one matches the oracle --
+// profiles/r06_ab_message_parents.txt)
 template <int N, int V, int MR, bool BFV, bool FUSE, int PB>
-__global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ? RMC_FUSED_WAVES : 0) : RMC_ITEMS_WAVES) void k_expand_items(KParams P) {
+__global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? ((N <= 3 && !BFV) ? RMC_FUSED_WAVES : 0) : RMC_ITEMS_WAVES) void k_expand_items(KParams P) {
     using S = Spec<N, V, MR>;
     using Lo = Layout<N, V>;
     constexpr int NT = items_threads<N, V, MR, FUSE>();
@@ -2281,15 +2284,16 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
             const uint32_t xm = wave_excl_scan(nmj, tid, &tm);
             if ((uint32_t)tid < nb) sMsc[tid] = xm;
             if (tid == 0) sMsc[nb] = tm;
+            // each message's parent, for the message pass and the class lists (no search per message; round 6:
+            // expansion -5.7 %, profiles/r06_ab_message_parents.txt)
+            for (uint32_t k = 0; k < nmj; k++) sMJ[xm + k] = (uint8_t)tid;
         }
         __syncthreads();
         PHASE(1);
         // (b) a lane per message: hash sums per server pair, votes per server, its class
         const uint32_t tmsg = sMsc[nb];
         for (uint32_t m = (uint32_t)tid; m < tmsg; m += NT) {
-            uint32_t j = 0;  // the last parent j with sMsc[j] <= m
-#pragma unroll
-            for (uint32_t st = PB / 2; st; st >>= 1) j = (j + st < nb && sMsc[j + st] <= m) ? j + st : j;
+            const uint32_t j = sMJ[m];  // its parent
             const uint32_t k = m - sMsc[j];
             const uint32_t id = reinterpret_cast<const uint16_t *>(sRec + sOff[j] + CCW)[k];
             const uint32_t inf = P.t.info[id];
@@ -2303,7 +2307,6 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
             if (mi_type(inf) == VRESP && mi_term(inf) == ct) atomicAdd(&sVp[j * N + dst], 1u);
             const uint32_t c = msg_class(inf, ct, nib(pc[Lo::W_ROLE], dst));
             sMI[m] = (uint8_t)(c == IC_DEAD ? 15u : c);
-            sMJ[m] = (uint8_t)j;
             if constexpr (FUSE) sInf[m] = inf;
             if (c != IC_DEAD) atomicAdd(&sLive[j], 1u);
         }
@@ -2348,8 +2351,8 @@ __global__ __launch_bounds__((items_threads<N, V, MR, FUSE>()), FUSE ? (N <= 3 ?
             for (uint32_t st = PB; st; st >>= 1) b = (b + st <= nb && sItm[b + st] <= ibase + NT) ? b + st : b;
             b = b > a ? b : a + 1;  // (a parent's items always fit a round: MCAP + N * SLOTS_PER_SERVER <= NT)
             const uint32_t nI = sItm[b] - ibase < (uint32_t)NT ? sItm[b] - ibase : (uint32_t)NT;
-            // the round's items into their class lists: live messages (each one's parent noted by the message pass:
-            // no search), then each parent's slots, a server's positions all taken before any is written so its
+            // the round's items into their class lists: live messages (each one's parent noted with the message
+            // scan: no search), then each parent's slots, a server's positions all taken before any is written so its
             // LDS atomics are in flight together (round 6: expansion -8 %, profiles/r06_ab_class_lists.txt); one LDS
             // atomic per item -- appending a wave's items per class with ballots and one atomic per class, or
             // finding the parent by a two-step search, measured slower (profiles/r06_ab_expansion.txt)
