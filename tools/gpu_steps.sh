@@ -45,7 +45,7 @@ for s in "$@"; do
     prof_c2) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof_c2" -o bench -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-probe-peak --workload c2 > "$O/prof_c2.log" 2>&1 || { tail -20 "$O/prof_c2.log"; exit 1; }
            find "$O/prof_c2" -name '*kernel_stats.csv' -exec head -12 {} \; ;;
     pmc_bench) rm -rf gpurun_out/pmc; WORKLOAD=raftcfg bash tools/pmc.sh || exit 1
-           python tools/pmc_summary.py gpurun_out/pmc "$O/pmc_raftcfg.json" && rm -rf gpurun_out/pmc ;;
+           python tools/pmc_summary.py gpurun_out/pmc "$O/pmc_headline_raftcfg.json" && rm -rf gpurun_out/pmc ;;
     pmc_c2) rm -rf gpurun_out/pmc; WORKLOAD=c2 bash tools/pmc.sh || exit 1
            python tools/pmc_summary.py gpurun_out/pmc "$O/pmc_c2.json" && rm -rf gpurun_out/pmc ;;
     c4) timeout -k 10 300 python -u tools/explore.py 5 1 3 3 --budget 150 > "$O/c4.log" 2>&1 || { tail -20 "$O/c4.log"; exit 1; }
